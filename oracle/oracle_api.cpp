@@ -1,0 +1,241 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see oracle.hpp header).
+// extern "C" surface of the oracle for ctypes (tests/, bench.py cpu_baseline, smoke()).
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <random>
+#include <thread>
+
+#include "oracle.hpp"
+#include "oracle_dsp.hpp"
+
+using namespace orc;
+
+static psdef_t to_psdef(const uint32_t* p) { return psdef_t{p[0], p[1], p[2], p[3], p[4], p[5], p[6]}; }
+static cfg_t to_cfg(const uint32_t* c) {
+    cfg_t g;
+    g.u_max = c[0];
+    g.b_max = c[1];
+    g.os_min = c[2];
+    g.L = c[3];
+    g.M = c[4];
+    g.chestim_mode_lr = c[5] != 0;
+    g.stride = c[6];
+    return g;
+}
+
+extern "C" {
+
+// out: N_PACKET_symb, N_DF_symb, N_PDC_subc, N_DRS_subc, G, N_PDC_bits, N_TB_bits, C,
+//      N_samples_STF, N_samples_STF_CP_only, N_samples_DF, N_samples_GI, N_samples_packet_no_GI,
+//      N_samples_packet, N_bps, N_eff_TX, N_SS, N_TS, N_TX, N_b_DFT, N_b_OCC
+int oracle_packet_sizes(const uint32_t* psdef, uint32_t* out) {
+    try {
+        packet_sizes_t q;
+        if (!get_packet_sizes(to_psdef(psdef), q)) return -1;
+        const uint32_t v[] = {q.N_PACKET_symb, q.N_DF_symb, q.N_PDC_subc, q.N_DRS_subc, q.G, q.N_PDC_bits,
+                              q.N_TB_bits, q.C, q.N_samples_STF, q.N_samples_STF_CP_only, q.N_samples_DF,
+                              q.N_samples_GI, q.N_samples_packet_no_GI, q.N_samples_packet, q.mcs.N_bps,
+                              q.tm.N_eff_TX, q.tm.N_SS, q.tm.N_TS, q.tm.N_TX, q.num.N_b_DFT, q.num.N_b_OCC};
+        std::memcpy(out, v, sizeof(v));
+        return 0;
+    } catch (...) {
+        return -2;
+    }
+}
+
+// out: N_b_DFT_os, off_lower, CP_os, STF_CP_os, N_no_GI_os, N_no_GI_os_rs, N_packet_os_rs
+int oracle_dims(const uint32_t* cfg, const uint32_t* psdef, uint32_t* out) {
+    try {
+        packet_sizes_t q;
+        if (!get_packet_sizes(to_psdef(psdef), q)) return -1;
+        dims_t d;
+        d.init(to_cfg(cfg), q);
+        const uint32_t v[] = {d.N_b_DFT_os, d.off_lower, d.CP_os, d.STF_CP_os, d.N_no_GI_os, d.N_no_GI_os_rs,
+                              d.N_packet_os_rs};
+        std::memcpy(out, v, sizeof(v));
+        return 0;
+    } catch (...) {
+        return -2;
+    }
+}
+
+int oracle_kaiser(float fp, float fs_, float ripple, float att, uint32_t max_n, float* out) {
+    const auto k = kaiser(fp, fs_, ripple, att, 1.0f, true);
+    if (k.size() > max_n) return -1;
+    std::memcpy(out, k.data(), k.size() * sizeof(float));
+    return static_cast<int>(k.size());
+}
+
+int oracle_gold(uint32_t c_init, uint32_t len, uint8_t* out) {
+    const auto c = gold_sequence(c_init, len);
+    std::memcpy(out, c.data(), len);
+    return 0;
+}
+
+int oracle_stf(uint32_t b, uint32_t N_eff_TX, double* out_re_im) {
+    const auto v = stf_values(b, N_eff_TX);
+    for (size_t i = 0; i < v.size(); ++i) {
+        out_re_im[2 * i] = v[i].real();
+        out_re_im[2 * i + 1] = v[i].imag();
+    }
+    return static_cast<int>(v.size());
+}
+
+// flattened per-symbol PDC lists: out_cnt[l] for l in [0,N_DF], out_k concatenated
+int oracle_pdc_cells(uint32_t b, uint32_t N_TS, uint32_t N_DF, uint32_t* out_cnt, uint32_t* out_k) {
+    const auto v = pdc_cells_packet(b, N_TS, N_DF);
+    uint32_t o = 0;
+    for (uint32_t l = 0; l <= N_DF; ++l) {
+        out_cnt[l] = static_cast<uint32_t>(v[l].size());
+        for (uint32_t k : v[l]) out_k[o++] = k;
+    }
+    return static_cast<int>(o);
+}
+
+int oracle_pcc_cells(uint32_t b, uint32_t N_TS, uint32_t* out_l, uint32_t* out_k) {
+    std::vector<uint32_t> l;
+    std::vector<std::vector<uint32_t>> k;
+    pcc_cells(b, N_TS, l, k);
+    uint32_t o = 0;
+    for (size_t s = 0; s < l.size(); ++s)
+        for (uint32_t kk : k[s]) {
+            out_l[o] = l[s];
+            out_k[o++] = kk;
+        }
+    return static_cast<int>(o);
+}
+
+// LUT export: returns number of weight vectors; idx arrays sized T*4*(56b+1)
+int oracle_chest_lut(uint32_t Nsv, uint32_t b, uint32_t b_max, uint32_t u_max, uint32_t profile,
+                     uint32_t* idx_pilot, uint32_t* idx_weight, float* weights, uint32_t max_w) {
+    try {
+        const auto prof = chest_profiles(u_max);
+        const auto L = build_chest_lut(Nsv, b, b_max, prof.at(profile));
+        std::memcpy(idx_pilot, L.idx_pilot.data(), L.idx_pilot.size() * 4);
+        std::memcpy(idx_weight, L.idx_weight.data(), L.idx_weight.size() * 4);
+        if (L.weights.size() > max_w) return -1;
+        std::memcpy(weights, L.weights.data(), L.weights.size() * 4);
+        return static_cast<int>(L.weights.size() / L.nof_interp);
+    } catch (...) {
+        return -2;
+    }
+}
+
+// desc_u: codebook, network_id, plcf_type, GI_percentage ; desc_f: DAC_scale, phase, phase_inc
+int oracle_tx(const uint32_t* cfg, const uint32_t* psdef, const uint32_t* desc_u, const double* desc_f,
+              const uint8_t* pcc_d, const uint8_t* pdc_d, float* out, uint32_t S_slot, int use_float) {
+    try {
+        packet_sizes_t q;
+        if (!get_packet_sizes(to_psdef(psdef), q)) return -1;
+        tx_desc_t d;
+        d.codebook_index = desc_u[0];
+        d.network_id = desc_u[1];
+        d.plcf_type = desc_u[2];
+        d.GI_percentage = desc_u[3];
+        d.DAC_scale = static_cast<float>(desc_f[0]);
+        d.iq_phase_rad = desc_f[1];
+        d.iq_phase_increment_rad = desc_f[2];
+        const cfg_t c = to_cfg(cfg);
+        auto store = [&](const auto& v) {
+            for (size_t a = 0; a < v.size(); ++a)
+                for (uint32_t m = 0; m < S_slot; ++m) {
+                    out[(a * S_slot + m) * 2] = static_cast<float>(v[a][m].real());
+                    out[(a * S_slot + m) * 2 + 1] = static_cast<float>(v[a][m].imag());
+                }
+        };
+        if (use_float) {
+            std::vector<std::vector<std::complex<float>>> v;
+            tx_packet<float>(c, q, d, pcc_d, pdc_d, v, S_slot);
+            store(v);
+        } else {
+            std::vector<std::vector<std::complex<double>>> v;
+            tx_packet<double>(c, q, d, pcc_d, pdc_d, v, S_slot);
+            store(v);
+        }
+        dims_t dm;
+        dm.init(c, q);
+        return static_cast<int>(dm.transmit_len(d.GI_percentage));
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle_tx: %s\n", e.what());
+        return -2;
+    }
+}
+
+// meta out: [0..7] rms, 8 cfo_fine_rad, 9 sto_fractional, 10 snr_pcc_db, 11 snr_pdc_db
+int oracle_rx(const uint32_t* cfg, const uint32_t* psdef, uint32_t N_RX, const float* iq, uint32_t S_in,
+              int64_t fine_peak, double cfo_rad, uint32_t network_id, uint32_t plcf_type, int16_t* pcc_llr,
+              int16_t* pdc_llr, float* pcc_llr_f, float* pdc_llr_f, float* meta, int use_float) {
+    try {
+        packet_sizes_t q;
+        if (!get_packet_sizes(to_psdef(psdef), q)) return -1;
+        rx_in_t in{iq, N_RX, S_in, fine_peak, cfo_rad, network_id, plcf_type};
+        rx_out_t o;
+        if (use_float)
+            rx_packet<float>(to_cfg(cfg), q, in, o);
+        else
+            rx_packet<double>(to_cfg(cfg), q, in, o);
+        std::memcpy(pcc_llr, o.pcc_llr.data(), 196 * 2);
+        std::memcpy(pdc_llr, o.pdc_llr.data(), q.G * 2);
+        if (pcc_llr_f) std::memcpy(pcc_llr_f, o.pcc_llr_f.data(), 196 * 4);
+        if (pdc_llr_f) std::memcpy(pdc_llr_f, o.pdc_llr_f.data(), q.G * 4);
+        for (uint32_t a = 0; a < 8; ++a) meta[a] = a < o.rms.size() ? o.rms[a] : 0.0f;
+        meta[8] = o.cfo_fine_rad;
+        meta[9] = o.sto_fractional;
+        meta[10] = o.snr_pcc_db;
+        meta[11] = o.snr_pdc_db;
+        return 0;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle_rx: %s\n", e.what());
+        return -2;
+    }
+}
+
+// CPU baseline: n_packets TX+RX loopback slot-pairs (float path), one packet per thread at a time
+// (worker_tx_rx_t model). Returns wall seconds, or negative on error.
+double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_t n_packets, uint32_t n_threads,
+                             uint64_t seed) {
+    try {
+        packet_sizes_t q;
+        if (!get_packet_sizes(to_psdef(psdef), q)) return -1.0;
+        const cfg_t c = to_cfg(cfg);
+        dims_t dm;
+        dm.init(c, q);
+        const uint32_t S = dm.N_packet_os_rs;
+        std::atomic<uint32_t> next{0};
+        std::atomic<int> err{0};
+        auto worker = [&](uint32_t tid) {
+            std::mt19937_64 rng(seed + tid);
+            std::vector<uint8_t> pcc(25), pdc((q.G + 7) / 8);
+            std::vector<float> iq(2ull * q.tm.N_TX * S);
+            while (true) {
+                const uint32_t i = next.fetch_add(1);
+                if (i >= n_packets) break;
+                for (auto& b : pcc) b = static_cast<uint8_t>(rng());
+                for (auto& b : pdc) b = static_cast<uint8_t>(rng());
+                tx_desc_t d;
+                d.network_id = 100 + i % 6;
+                d.plcf_type = 1 + i % 2;
+                std::vector<std::vector<std::complex<float>>> v;
+                tx_packet<float>(c, q, d, pcc.data(), pdc.data(), v, S);
+                for (size_t a = 0; a < v.size(); ++a)
+                    std::memcpy(&iq[2ull * a * S], v[a].data(), S * 8);
+                rx_in_t in{iq.data(), q.tm.N_TX, S, 0, 0.0, d.network_id, d.plcf_type};
+                rx_out_t o;
+                rx_packet<float>(c, q, in, o);
+                if (o.pdc_llr.size() != q.G) err = 1;
+            }
+        };
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        for (uint32_t t = 0; t < n_threads; ++t) th.emplace_back(worker, t);
+        for (auto& t : th) t.join();
+        const auto t1 = std::chrono::steady_clock::now();
+        if (err) return -3.0;
+        return std::chrono::duration<double>(t1 - t0).count();
+    } catch (...) {
+        return -2.0;
+    }
+}
+
+}  // extern "C"

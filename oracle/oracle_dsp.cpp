@@ -1,0 +1,758 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see oracle.hpp header).
+// Per-packet scalar restatement of tx_t::generate_tx_packet (lib/src/phy/tx/tx.cpp:165-314) and
+// rx_synced_t::demoddecod_rx_pcc/_pdc (lib/src/phy/rx/rx_synced/rx_synced.cpp:186-436),
+// templated on the sample type so the same code serves as the double-precision checker and as
+// the float CPU baseline.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+
+#include "oracle.hpp"
+#include "oracle_dsp.hpp"
+
+namespace orc {
+
+// ---------------------------------------------------------------- FFT (mixed radix 2/3, recursive DIT)
+template <typename R>
+struct fft_plan_t {
+    using C = std::complex<R>;
+    uint32_t N = 0;
+    int sign = -1;
+    std::vector<C> tw;
+    std::vector<C> scratch;
+    void init(uint32_t N_, int sign_) {
+        N = N_;
+        sign = sign_;
+        tw.resize(N);
+        for (uint32_t j = 0; j < N; ++j) {
+            const double a = sign * 2.0 * M_PI * static_cast<double>(j) / static_cast<double>(N);
+            tw[j] = C(static_cast<R>(std::cos(a)), static_cast<R>(std::sin(a)));
+        }
+        scratch.resize(N);
+    }
+    void rec(const C* in, C* out, uint32_t n, uint32_t stride) const {
+        if (n == 1) {
+            out[0] = in[0];
+            return;
+        }
+        const uint32_t r = (n % 2 == 0) ? 2 : 3;
+        const uint32_t m = n / r;
+        for (uint32_t q = 0; q < r; ++q) rec(in + q * stride, out + q * m, m, stride * r);
+        const uint32_t ts = N / n;
+        if (r == 2) {
+            for (uint32_t k = 0; k < m; ++k) {
+                const C a = out[k], b = out[m + k] * tw[k * ts];
+                out[k] = a + b;
+                out[m + k] = a - b;
+            }
+        } else {
+            const C w3 = tw[N / 3], w3b = tw[2 * N / 3];
+            for (uint32_t k = 0; k < m; ++k) {
+                const C a = out[k], b = out[m + k] * tw[k * ts], c = out[2 * m + k] * tw[2 * k * ts];
+                out[k] = a + b + c;
+                out[m + k] = a + b * w3 + c * w3b;
+                out[2 * m + k] = a + b * w3b + c * w3;
+            }
+        }
+    }
+    void run(const C* in, C* out) const { rec(in, out, N, 1); }
+};
+
+template <typename R>
+static fft_plan_t<R>& get_plan(uint32_t N, int sign) {
+    thread_local std::map<std::pair<uint32_t, int>, fft_plan_t<R>> plans;
+    auto& p = plans[{N, sign}];
+    if (p.N != N) p.init(N, sign);
+    return p;
+}
+
+// float phasor emulation of mixer_t::set_phase/set_phase_increment (mixer.cpp:27-39)
+static double phasor_arg(double rad) {
+    const float c = std::cos(static_cast<float>(rad)), s = std::sin(static_cast<float>(rad));
+    return std::atan2(static_cast<double>(s), static_cast<double>(c));
+}
+static double phasor_mul_arg(double rad0, double rad1) {
+    const cf a{std::cos(static_cast<float>(rad0)), std::sin(static_cast<float>(rad0))};
+    const cf b{std::cos(static_cast<float>(rad1)), std::sin(static_cast<float>(rad1))};
+    const cf c = a * b;
+    return std::atan2(static_cast<double>(c.imag()), static_cast<double>(c.real()));
+}
+
+void dims_t::init(const cfg_t& cfg, const packet_sizes_t& ps) {
+    const uint64_t rate_max = static_cast<uint64_t>(cfg.u_max) * cfg.b_max * 1728000ull * cfg.os_min;
+    N_b_DFT_os = static_cast<uint32_t>(rate_max / (ps.num.u * 27000ull));
+    N_b_DFT = ps.num.N_b_DFT;
+    N_b_OCC = ps.num.N_b_OCC;
+    const uint32_t guard_os = (N_b_DFT_os - N_b_DFT) / 2;
+    off_lower = N_b_DFT / 2 + 2 * guard_os + ps.num.N_guards_bottom;
+    CP_os = ps.num.N_b_CP * N_b_DFT_os / N_b_DFT;
+    STF_CP_os = ps.N_samples_STF_CP_only * N_b_DFT_os / N_b_DFT;
+    N_no_GI_os = ps.N_samples_packet_no_GI * N_b_DFT_os / N_b_DFT;
+    const uint32_t N_packet_os = ps.N_samples_packet * N_b_DFT_os / N_b_DFT;
+    N_no_GI_os_rs = static_cast<uint32_t>((static_cast<uint64_t>(N_no_GI_os) * cfg.L + cfg.M - 1) / cfg.M);
+    N_packet_os_rs = N_packet_os / cfg.M * cfg.L;
+    n_pattern = ps.num.u == 1 ? 7 : 9;
+    pattern_len = 16 * ps.num.b * N_b_DFT_os / N_b_DFT;
+}
+
+uint32_t dims_t::transmit_len(uint32_t gi_percentage) const {
+    return N_no_GI_os_rs + (N_packet_os_rs - N_no_GI_os_rs) * gi_percentage / 100;
+}
+
+static const float COVER[9] = {1, -1, 1, 1, -1, -1, -1, -1, -1};  // stf.hpp:146-151
+
+static std::vector<uint8_t> unpack_bits(const uint8_t* d, uint32_t nbits) {
+    std::vector<uint8_t> b(nbits);
+    for (uint32_t i = 0; i < nbits; ++i) b[i] = (d[i / 8] >> (7 - i % 8)) & 1u;
+    return b;
+}
+
+static std::vector<cd> modulate(const std::vector<uint8_t>& bits, uint32_t N_bps) {
+    const auto tab = constellation(N_bps);
+    std::vector<cd> s(bits.size() / N_bps);
+    for (size_t j = 0; j < s.size(); ++j) {
+        uint32_t idx = 0;
+        for (uint32_t k = 0; k < N_bps; ++k) idx = (idx << 1) | bits[j * N_bps + k];
+        s[j] = tab[idx];
+    }
+    return s;
+}
+
+static bool is_txdiv(uint32_t tm_index) { return tm_index == 1 || tm_index == 5 || tm_index == 10; }
+
+uint32_t pdc_c_init(uint32_t network_id, uint32_t plcf_type) {  // scrambling_pdc.cpp:41-48
+    return plcf_type == 1 ? (network_id & 0xFFu) : (network_id >> 8);
+}
+
+// ================================================================= TX
+template <typename R>
+void tx_packet(const cfg_t& cfg, const packet_sizes_t& ps, const tx_desc_t& d, const uint8_t* pcc_d,
+               const uint8_t* pdc_d, std::vector<std::vector<std::complex<R>>>& out, uint32_t S_slot) {
+    using C = std::complex<R>;
+    dims_t dm;
+    dm.init(cfg, ps);
+    const auto& tm = ps.tm;
+    const uint32_t N = dm.N_b_OCC, Nf = N + 1, Nd = dm.N_b_DFT_os;
+
+    // scrambling (pcc_enc.cpp:104-106,212; pdc_enc.cpp:218-221)
+    auto pcc_bits = unpack_bits(pcc_d, 196);
+    const auto cp = gold_sequence(0x44454354u, 200);
+    for (uint32_t i = 0; i < 196; ++i) pcc_bits[i] ^= cp[i];
+    auto pdc_bits = unpack_bits(pdc_d, ps.G);
+    const auto cs = gold_sequence(pdc_c_init(d.network_id, d.plcf_type), ps.G);
+    for (uint32_t i = 0; i < ps.G; ++i) pdc_bits[i] ^= cs[i];
+
+    // modulation (tx.cpp:602-677, 1004-1116; fix/mod.cpp)
+    const auto pcc_s = modulate(pcc_bits, 2);
+    const auto pdc_s = modulate(pdc_bits, ps.mcs.N_bps);
+    auto flip = [](const std::vector<cd>& s, size_t j) {  // pairwise swap + (-re,+im)/(+re,-im)
+        return (j % 2 == 0) ? cd{-s[j + 1].real(), s[j + 1].imag()} : cd{s[j - 1].real(), -s[j - 1].imag()};
+    };
+
+    // scaling (tx.cpp:579-599)
+    float scale_common = d.DAC_scale;
+    if (!d.optimal_scaling_DAC)
+        scale_common *= static_cast<float>(W_scaling(tm.N_TS, tm.N_TX, d.codebook_index));
+    else
+        throw std::runtime_error("optimal_scaling_DAC not supported by oracle");
+    const float scale_stf = 1.0f / std::sqrt(static_cast<float>(N / 4)) * scale_common;
+    const float scale_df = 1.0f / std::sqrt(static_cast<float>(N)) * scale_common;
+    const auto W = W_matrix(tm.N_TS, tm.N_TX, d.codebook_index);
+
+    // geometry
+    std::vector<uint32_t> pcc_l;
+    std::vector<std::vector<uint32_t>> pcc_k;
+    pcc_cells(ps.num.b, tm.N_TS, pcc_l, pcc_k);
+    const auto pdc_k = pdc_cells_packet(ps.num.b, tm.N_TS, ps.N_DF_symb);
+    const auto drs = drs_schedule(tm.N_TS, ps.N_DF_symb);
+    const auto stf = stf_values(ps.num.b, tm.N_eff_TX);
+    const bool txdiv = is_txdiv(tm.index);
+    const uint32_t mod = tm.N_TS > 1 ? txdiv_modulo(tm.N_TS) : 1;
+
+    auto& plan = get_plan<R>(Nd, +1);
+    std::vector<std::vector<C>> x(tm.N_TX);  // DECT-rate stream per antenna
+    for (auto& v : x) v.reserve(dm.N_no_GI_os);
+    std::vector<std::vector<cd>> ts(tm.N_TS, std::vector<cd>(Nf));
+    std::vector<C> bins(Nd), tdom(Nd);
+    uint32_t pcc_idx = 0, pdc_idx = 0, pcc_sym = 0, drs_i = 0;
+
+    for (uint32_t l = 0; l <= ps.N_DF_symb; ++l) {
+        for (auto& v : ts) std::fill(v.begin(), v.end(), cd{0, 0});
+        uint32_t n_ts_nonzero = tm.N_TS;
+        if (l == 0) {
+            ts[0] = stf;
+            n_ts_nonzero = 1;
+        } else {
+            if (pcc_sym < pcc_l.size() && pcc_l[pcc_sym] == l) {
+                for (uint32_t k : pcc_k[pcc_sym]) {
+                    if (tm.N_TS == 1) {
+                        ts[0][k] = pcc_s[pcc_idx];
+                    } else {
+                        uint32_t A, B;
+                        txdiv_pair(tm.N_TS, (pcc_idx / 2) % mod, A, B);
+                        ts[A][k] = pcc_s[pcc_idx];
+                        ts[B][k] = flip(pcc_s, pcc_idx);
+                    }
+                    ++pcc_idx;
+                }
+                ++pcc_sym;
+            }
+            if (drs_i < drs.size() && drs[drs_i].l == l) {
+                const auto& ds = drs[drs_i];
+                for (uint32_t t = ds.ts_first; t <= ds.ts_last; ++t) {
+                    const auto kk = drs_k_i(ps.num.b, t % 4, ds.k_parity);
+                    const auto yy = drs_y(ps.num.b, t);
+                    for (size_t i = 0; i < kk.size(); ++i) ts[t][kk[i]] = cd{yy[i], 0};
+                }
+                ++drs_i;
+            }
+            for (uint32_t k : pdc_k[l]) {
+                if (!txdiv) {
+                    for (uint32_t j = 0; j < tm.N_SS; ++j) ts[j][k] = pdc_s[pdc_idx * tm.N_SS + j];
+                } else {
+                    uint32_t A, B;
+                    txdiv_pair(tm.N_TS, (pdc_idx / 2) % mod, A, B);
+                    ts[A][k] = pdc_s[pdc_idx];
+                    ts[B][k] = flip(pdc_s, pdc_idx);
+                }
+                ++pdc_idx;
+            }
+        }
+        const float sc = l == 0 ? scale_stf : scale_df;
+        const uint32_t CP = l == 0 ? dm.STF_CP_os : dm.CP_os;
+        for (uint32_t a = 0; a < tm.N_TX; ++a) {
+            std::fill(bins.begin(), bins.end(), C(0, 0));
+            for (uint32_t k = 0; k < Nf; ++k) {
+                cd v{0, 0};
+                for (uint32_t i = 0; i < n_ts_nonzero; ++i) v += W[a * tm.N_TS + i] * ts[i][k];
+                v *= static_cast<double>(sc);
+                const uint32_t bin = (k >= N / 2) ? (k - N / 2) : (dm.off_lower + k);
+                bins[bin] = C(static_cast<R>(v.real()), static_cast<R>(v.imag()));
+            }
+            plan.run(bins.data(), tdom.data());
+            for (uint32_t i = 0; i < CP + Nd; ++i) {
+                C s = tdom[(i + Nd - (CP % Nd)) % Nd];
+                if (l == 0) s *= static_cast<R>(COVER[std::min<uint32_t>(i / dm.pattern_len, 8)]);
+                x[a].push_back(s);
+            }
+        }
+    }
+    if (pcc_idx != 98 || pdc_idx != ps.N_PDC_subc) throw std::runtime_error("TX cell count mismatch");
+
+    // resampling (resampler.cpp:330-454 closed form) + phase-continuous mixer (mixer.cpp:41-65)
+    resampler_t rs;
+    rs.design(cfg.L, cfg.M, cfg.os_min);
+    const double ph0 = phasor_arg(d.iq_phase_rad), inc = phasor_arg(d.iq_phase_increment_rad);
+    out.assign(tm.N_TX, std::vector<C>(S_slot, C(0, 0)));
+    const uint32_t n_keep = std::min(dm.N_no_GI_os_rs, S_slot);
+    const int64_t Nx = static_cast<int64_t>(x[0].size());
+    for (uint32_t a = 0; a < tm.N_TX; ++a) {
+        for (uint32_t m = 0; m < n_keep; ++m) {
+            std::complex<double> acc{0, 0};
+            if (cfg.L == 1 && cfg.M == 1) {
+                acc = std::complex<double>(x[a][m].real(), x[a][m].imag());
+            } else {
+                const uint64_t t = rs.delay + static_cast<uint64_t>(m) * rs.M;
+                const int64_t p = static_cast<int64_t>(t / rs.L);
+                const uint32_t ph = static_cast<uint32_t>(t % rs.L);
+                for (uint32_t dd = 0; dd <= rs.hl; ++dd) {
+                    const int64_t n = p - dd;
+                    if (n < 0 || n >= Nx) continue;
+                    acc += std::complex<double>(x[a][n].real(), x[a][n].imag()) *
+                           static_cast<double>(rs.h[ph + dd * rs.L]);
+                }
+            }
+            const double phi = ph0 + static_cast<double>(m) * inc;
+            acc *= std::complex<double>(std::cos(phi), std::sin(phi));
+            out[a][m] = C(static_cast<R>(acc.real()), static_cast<R>(acc.imag()));
+        }
+    }
+}
+
+// ================================================================= RX
+// srsRAN demod_soft int16 restatement (LTE max-log approximation with fixed scale constants)
+void demap_float(const cd& y, uint32_t N_bps, double* L) {
+    const double re = y.real(), im = y.imag();
+    switch (N_bps) {
+        case 1:
+            L[0] = -100.0 * (re + im);
+            break;
+        case 2:
+            L[0] = -100.0 * re;
+            L[1] = -100.0 * im;
+            break;
+        case 4: {
+            const double S = 400.0, yr = S * re, yi = S * im, o = 2.0 * S / std::sqrt(10.0);
+            L[0] = -yr;
+            L[1] = -yi;
+            L[2] = std::fabs(yr) - o;
+            L[3] = std::fabs(yi) - o;
+            break;
+        }
+        case 6: {
+            const double S = 700.0, yr = S * re, yi = S * im, q = S / std::sqrt(42.0);
+            L[0] = -yr;
+            L[1] = -yi;
+            L[2] = std::fabs(yr) - 4.0 * q;
+            L[3] = std::fabs(yi) - 4.0 * q;
+            L[4] = std::fabs(L[2]) - 2.0 * q;
+            L[5] = std::fabs(L[3]) - 2.0 * q;
+            break;
+        }
+        case 8: {
+            const double S = 1000.0, yr = S * re, yi = S * im, q = S / std::sqrt(170.0);
+            L[0] = -yr;
+            L[1] = -yi;
+            L[2] = std::fabs(yr) - 8.0 * q;
+            L[3] = std::fabs(yi) - 8.0 * q;
+            L[4] = std::fabs(L[2]) - 4.0 * q;
+            L[5] = std::fabs(L[3]) - 4.0 * q;
+            L[6] = std::fabs(L[4]) - 2.0 * q;
+            L[7] = std::fabs(L[5]) - 2.0 * q;
+            break;
+        }
+        default:
+            throw std::runtime_error("unsupported N_bps");
+    }
+}
+
+int16_t llr_to_i16(double v) {
+    const double r = std::nearbyint(v);
+    return static_cast<int16_t>(std::max(-32768.0, std::min(32767.0, r)));
+}
+
+namespace {
+template <typename R>
+struct rx_state_t {
+    using C = std::complex<R>;
+    const cfg_t& cfg;
+    const packet_sizes_t& ps;
+    const rx_in_t& in;
+    rx_out_t& out;
+    dims_t dm;
+    uint32_t N_RX, N_eff_TX, N_step, ps_len, Nf;
+    std::vector<std::vector<C>> y;  // resampled stream per antenna (DECT rate)
+    uint64_t rpos = 0;              // next resampled sample to consume
+    double mix_inc0 = 0, mix_inc1 = 0;
+    uint64_t n_stf = 0;
+    // processing stage [rel][rx][Nf]
+    std::vector<std::vector<std::vector<cd>>> stage;
+    std::vector<std::vector<std::vector<cd>>> zf, zfi, chest;  // [rx][ts][..]
+    double sto_inc = 0;
+    double snr_SN = 0, snr_N = 0;
+    uint64_t snr_SN_cnt = 0, snr_N_cnt = 0;
+    std::vector<chest_stats_t> prof;
+    std::vector<chest_lut_t> lut0, lut_lr;
+    int lut_eff = -1;
+    uint32_t ps_idx = 0, rel = 0, l_abs = 1, ts_first = 0, ts_last = 0;
+    bool mode_lr = false;
+    std::vector<drs_sym_t> drs;
+    uint32_t drs_next = 0;
+    std::vector<uint32_t> pcc_l;
+    std::vector<std::vector<uint32_t>> pcc_k, pdc_k;
+    uint32_t pcc_sym = 0, pcc_idx = 0, pdc_idx = 0, bits_idx = 0;
+    std::vector<cd> stf_y;
+    uint32_t mod = 1;
+
+    rx_state_t(const cfg_t& c, const packet_sizes_t& p, const rx_in_t& i, rx_out_t& o)
+        : cfg(c), ps(p), in(i), out(o) {}
+
+    void resample_all() {
+        resampler_t rs;
+        rs.design(cfg.M, cfg.L, cfg.os_min);  // L and M swapped at RX (rx_synced.cpp:65-73)
+        const uint64_t need = dm.N_no_GI_os;
+        y.assign(N_RX, std::vector<C>(need));
+        for (uint32_t a = 0; a < N_RX; ++a) {
+            const float* src = in.iq + 2ull * a * in.S_in;
+            auto xs = [&](int64_t n) -> std::complex<double> {
+                const int64_t idx = in.fine_peak + n;
+                if (n < 0 || idx < 0 || idx >= static_cast<int64_t>(in.S_in)) return {0, 0};
+                return {src[2 * idx], src[2 * idx + 1]};
+            };
+            for (uint64_t m = 0; m < need; ++m) {
+                std::complex<double> acc{0, 0};
+                if (rs.L == 1 && rs.M == 1) {
+                    acc = xs(static_cast<int64_t>(m));
+                } else {
+                    const uint64_t t = rs.delay + m * rs.M;
+                    const int64_t pp = static_cast<int64_t>(t / rs.L);
+                    const uint32_t ph = static_cast<uint32_t>(t % rs.L);
+                    for (uint32_t dd = 0; dd <= rs.hl; ++dd)
+                        acc += xs(pp - dd) * static_cast<double>(rs.h[ph + dd * rs.L]);
+                }
+                y[a][m] = C(static_cast<R>(acc.real()), static_cast<R>(acc.imag()));
+            }
+        }
+    }
+
+    // mix one symbol of length len starting at rpos (mixer.cpp:41-65 closed form)
+    std::vector<std::vector<C>> take_mixed(uint32_t len) {
+        std::vector<std::vector<C>> s(N_RX, std::vector<C>(len));
+        for (uint32_t a = 0; a < N_RX; ++a)
+            for (uint32_t i = 0; i < len; ++i) {
+                const uint64_t m = rpos + i;
+                const double phi = m < n_stf ? static_cast<double>(m) * mix_inc0
+                                             : static_cast<double>(n_stf) * mix_inc0 +
+                                                   static_cast<double>(m - n_stf) * mix_inc1;
+                const std::complex<double> v =
+                    std::complex<double>(y[a][m].real(), y[a][m].imag()) * std::complex<double>(std::cos(phi), std::sin(phi));
+                s[a][i] = C(static_cast<R>(v.real()), static_cast<R>(v.imag()));
+            }
+        rpos += len;
+        return s;
+    }
+
+    // rx_synced.cpp:748-771 (FFT, bin extraction, amplitude scaling, STO derotation)
+    void fft_scale(const std::vector<std::vector<C>>& s, uint32_t CP, std::vector<std::vector<cd>>& dst) {
+        const uint32_t Nd = dm.N_b_DFT_os, N = dm.N_b_OCC;
+        auto& plan = get_plan<R>(Nd, -1);
+        std::vector<C> f(Nd);
+        const double scale = static_cast<double>(std::sqrt(static_cast<float>(N)) / static_cast<float>(Nd));
+        const double ph_start = -sto_inc * static_cast<double>(N / 2);
+        for (uint32_t a = 0; a < N_RX; ++a) {
+            plan.run(&s[a][CP], f.data());
+            dst[a].assign(Nf, cd{0, 0});
+            for (uint32_t j = 0; j <= N / 2; ++j) dst[a][N / 2 + j] = cd(f[j].real(), f[j].imag());
+            for (uint32_t j = 0; j < N / 2; ++j) dst[a][j] = cd(f[dm.off_lower + j].real(), f[dm.off_lower + j].imag());
+            for (uint32_t k = 0; k < Nf; ++k) {
+                const double ang = ph_start + sto_inc * static_cast<double>(k);
+                dst[a][k] *= scale * cd(std::cos(ang), std::sin(ang));
+            }
+        }
+    }
+
+    void stf_zf(const std::vector<std::vector<cd>>& Y) {  // rx_synced.cpp:663-709
+        const uint32_t n = ps.num.b * 14;
+        for (uint32_t a = 0; a < N_RX; ++a) {
+            auto& z = zf[a][0];
+            z.assign(n, cd{0, 0});
+            uint32_t r = 0, w = 0;
+            for (uint32_t i = 0; i < n / 2 - 1; ++i, r += 4) z[w++] = Y[a][r] / stf_y[r];
+            z[w++] = Y[a][r] / stf_y[r];
+            r += 8;
+            for (uint32_t i = 0; i < n / 2; ++i, r += 4) z[w++] = Y[a][r] / stf_y[r];
+        }
+    }
+
+    void snr_add(const std::vector<cd>& z, uint32_t n) {  // estimator_snr.cpp:104-146
+        double sn = 0, nn = 0;
+        for (uint32_t i = 0; i < n; ++i) sn += std::norm(z[i]);
+        for (uint32_t i = 0; i + 1 < n; ++i) nn += std::norm(z[i] - z[i + 1]);
+        snr_SN += sn;
+        snr_SN_cnt += n;
+        snr_N += nn / 2.0;
+        snr_N_cnt += n - 1;
+    }
+    double snr_db() const {
+        if (snr_SN <= 0 || snr_N <= 0) return 0.0;
+        const double S = (snr_SN - snr_N) / static_cast<double>(snr_SN_cnt);
+        const double Nn = snr_N / static_cast<double>(snr_N_cnt);
+        return 10.0 * std::log10(S / Nn);
+    }
+
+    void run_stf() {  // rx_synced.cpp:503-619
+        const uint32_t len = dm.STF_CP_os + dm.N_b_DFT_os;
+        auto s = take_mixed(len);
+        out.rms.assign(N_RX, 0.0f);
+        for (uint32_t a = 0; a < N_RX; ++a) {
+            double e = 0;
+            for (uint32_t i = 0; i < len; ++i) e += std::norm(std::complex<double>(s[a][i].real(), s[a][i].imag()));
+            out.rms[a] = static_cast<float>(std::sqrt(e / len));
+            for (uint32_t i = 0; i < len; ++i) s[a][i] *= static_cast<R>(COVER[std::min<uint32_t>(i / dm.pattern_len, 8)]);
+        }
+        std::complex<double> sum{0, 0};
+        const uint32_t P = len / dm.n_pattern;
+        for (uint32_t a = 0; a < N_RX; ++a)
+            for (uint32_t j = 0; j + 1 < dm.n_pattern; ++j)
+                for (uint32_t i = 0; i < P; ++i) {
+                    const auto u = std::complex<double>(s[a][j * P + i].real(), s[a][j * P + i].imag());
+                    const auto v = std::complex<double>(s[a][(j + 1) * P + i].real(), s[a][(j + 1) * P + i].imag());
+                    sum += u * std::conj(v);
+                }
+        const double delta = static_cast<double>(static_cast<float>(std::arg(sum)) / static_cast<float>(P));
+        out.cfo_fine_rad = static_cast<float>(delta);
+        mix_inc1 = phasor_mul_arg(in.cfo_rad, delta);
+        std::vector<std::vector<cd>> Y(N_RX);
+        fft_scale(s, dm.STF_CP_os, Y);
+        stf_zf(Y);
+        // estimator_sto.cpp:47-62,124-146
+        double inc = 0;
+        const uint32_t n = ps.num.b * 14;
+        for (uint32_t a = 0; a < N_RX; ++a) {
+            std::vector<cd> p(n - 1);
+            for (uint32_t i = 0; i + 1 < n; ++i) p[i] = zf[a][0][i] * std::conj(zf[a][0][i + 1]);
+            const uint32_t c = n / 2 - 1;
+            const double A = std::atan2(p[c].imag(), p[c].real());
+            p[c] *= cd(std::cos(-A / 2.0), std::sin(-A / 2.0));
+            cd B{0, 0};
+            for (const auto& v : p) B += v;
+            inc += std::atan2(B.imag(), B.real()) / 4.0;
+        }
+        sto_inc = inc / static_cast<double>(N_RX);
+        out.sto_fractional = static_cast<float>(std::arg(cd(std::cos(sto_inc), std::sin(sto_inc))) / 2.0 / M_PI *
+                                                 static_cast<double>(dm.N_b_DFT_os));
+        // derotate the STF symbol and re-estimate (rx_synced.cpp:574-601)
+        for (uint32_t a = 0; a < N_RX; ++a)
+            for (uint32_t k = 0; k < Nf; ++k) {
+                const double ang = -sto_inc * static_cast<double>(dm.N_b_OCC / 2) + sto_inc * static_cast<double>(k);
+                Y[a][k] *= cd(std::cos(ang), std::sin(ang));
+            }
+        stf_zf(Y);
+        for (uint32_t a = 0; a < N_RX; ++a) snr_add(zf[a][0], n);
+        const double S = snr_SN - snr_N;  // estimator_snr.cpp:58-62 STF boost removal
+        snr_SN = S / 4.0 + snr_N;
+    }
+
+    void next_symbol() {  // run_mix_resample + run_cp_fft_scale onto the processing stage
+        auto s = take_mixed(dm.CP_os + dm.N_b_DFT_os);
+        fft_scale(s, dm.CP_os, stage[rel]);
+    }
+
+    void drs_zf() {  // rx_synced.cpp:773-861
+        const auto& ds = drs.at(drs_next++);
+        ts_first = ds.ts_first;
+        ts_last = ds.ts_last;
+        const uint32_t n = ps.num.b * 14;
+        for (uint32_t a = 0; a < N_RX; ++a)
+            for (uint32_t t = ts_first; t <= ts_last; ++t) {
+                const auto kk = drs_k_i(ps.num.b, t % 4, ds.k_parity);
+                const auto yy = drs_y(ps.num.b, t);
+                // channel_antenna.hpp:38-63 interlacing offsets
+                const bool lhs = rel <= 1;
+                const bool off1 = (ps_idx % 2 == 0) ? (lhs ? ((t % 4) >= 2) : ((t % 4) < 2))
+                                                    : (lhs ? ((t % 4) < 2) : ((t % 4) >= 2));
+                zf[a][t].assign(n, cd{0, 0});
+                if (zfi[a][t].size() != 2 * n) zfi[a][t].assign(2 * n, cd{0, 0});
+                for (uint32_t i = 0; i < n; ++i) {
+                    const cd v = stage[rel][a][kk[i]] / cd(yy[i], 0.0);
+                    zf[a][t][i] = v;
+                    zfi[a][t][2 * i + (off1 ? 1 : 0)] = v;
+                }
+            }
+        for (uint32_t a = 0; a < N_RX; ++a)
+            for (uint32_t t = ts_first; t <= std::min(ts_last, 7u); ++t) snr_add(zf[a][t], n);
+        // rx_synced.cpp:863-891 LUT pick, nearest SNR, ties to the later profile
+        const float snr = static_cast<float>(snr_db());
+        int idx = 0;
+        float best = static_cast<float>(std::fabs(snr - prof[0].snr_db));
+        for (int i = 1; i < 3; ++i) {
+            const float s2 = static_cast<float>(std::fabs(snr - prof[i].snr_db));
+            if (s2 <= best) {
+                best = s2;
+                idx = i;
+            }
+        }
+        lut_eff = idx;
+    }
+
+    void interpolate() {  // rx_synced.cpp:893-949 + channel_lut.cpp:66-165
+        const chest_lut_t& L = mode_lr ? lut_lr[lut_eff] : lut0[lut_eff];
+        const uint32_t n = L.nof_interp;
+        const uint32_t t0 = mode_lr ? 0 : ts_first;
+        if (rel >= L.ps_t_length) throw std::runtime_error("interpolation outside LUT stage");
+        for (uint32_t a = 0; a < N_RX; ++a)
+            for (uint32_t t = t0; t <= ts_last; ++t) {
+                const uint32_t tl = (ps_idx % 2 == 1) ? ((t % 4) ^ 2) : (t % 4);
+                const auto& z = mode_lr ? zfi[a][t] : zf[a][t];
+                auto& h = chest[a][t];
+                h.assign(Nf, cd{0, 0});
+                for (uint32_t f = 0; f < Nf; ++f) {
+                    const uint32_t ip = L.pilot(rel, tl, f), iw = L.weight(rel, tl, f);
+                    cd acc{0, 0};
+                    for (uint32_t i = 0; i < n; ++i) acc += z[ip + i] * static_cast<double>(L.weights[iw * n + i]);
+                    h[f] = acc;
+                }
+            }
+    }
+
+    void emit_llr(const cd& v, uint32_t N_bps, std::vector<int16_t>& dst_i, std::vector<float>& dst_f,
+                  uint32_t& pos) {
+        double Lr[8];
+        demap_float(v, N_bps, Lr);
+        for (uint32_t k = 0; k < N_bps; ++k) {
+            dst_f[pos] = static_cast<float>(Lr[k]);
+            dst_i[pos] = llr_to_i16(Lr[k]);
+            ++pos;
+        }
+    }
+
+    // rx_synced.cpp:1335-1392 transmit diversity combining; returns equalised symbols
+    std::vector<cd> combine(const std::vector<uint32_t>& kk, uint32_t base_idx) {
+        std::vector<cd> num(kk.size(), cd{0, 0}), den(kk.size(), cd{0, 0});
+        const auto& Y = stage[rel];
+        if (N_eff_TX == 1) {
+            for (uint32_t a = 0; a < N_RX; ++a)
+                for (size_t c = 0; c < kk.size(); ++c) {
+                    const cd h = chest[a][0][kk[c]];
+                    num[c] += Y[a][kk[c]] * std::conj(h);
+                    den[c] += h * std::conj(h);
+                }
+        } else {
+            for (uint32_t a = 0; a < N_RX; ++a)
+                for (size_t c = 0; c + 1 < kk.size(); c += 2) {
+                    const uint32_t k0 = kk[c], k1 = kk[c + 1];
+                    const cd r0 = Y[a][k0], r1 = Y[a][k1];
+                    uint32_t A, B;
+                    txdiv_pair(N_eff_TX, ((base_idx + c) / 2) % mod, A, B);
+                    const cd h0 = (chest[a][A][k0] + chest[a][A][k1]) / 2.0;
+                    const cd h1 = (chest[a][B][k0] + chest[a][B][k1]) / 2.0;
+                    num[c] += std::conj(h0) * r0 + h1 * std::conj(r1);
+                    num[c + 1] += -h1 * std::conj(r0) + std::conj(h0) * r1;
+                    const cd e = h0 * std::conj(h0) + h1 * std::conj(h1);
+                    den[c] += e;
+                    den[c + 1] += e;
+                }
+        }
+        for (size_t c = 0; c < kk.size(); ++c) num[c] /= den[c];
+        return num;
+    }
+
+    void pcc_collect() {
+        const auto& kk = pcc_k[pcc_sym];
+        const auto eq = combine(kk, pcc_idx);
+        uint32_t pos = pcc_idx * 2;
+        for (const auto& v : eq) emit_llr(v, 2, out.pcc_llr, out.pcc_llr_f, pos);
+        pcc_idx += static_cast<uint32_t>(kk.size());
+        ++pcc_sym;
+    }
+
+    void pdc_collect(uint32_t l) {
+        const auto& kk = pdc_k[l];
+        if (kk.empty()) return;
+        const auto eq = combine(kk, pdc_idx);
+        for (const auto& v : eq) emit_llr(v, ps.mcs.N_bps, out.pdc_llr, out.pdc_llr_f, bits_idx);
+        pdc_idx += static_cast<uint32_t>(kk.size());
+    }
+
+    bool is_drs(uint32_t l) const { return drs_next < drs.size() && drs[drs_next].l == l; }
+
+    void run() {
+        dm.init(cfg, ps);
+        N_RX = in.N_RX;
+        N_eff_TX = ps.tm.N_eff_TX;
+        if (N_eff_TX > 4) throw std::runtime_error("oracle RX supports N_eff_TX <= 4");
+        if (ps.tm.N_SS > 1) throw std::runtime_error("spatial multiplexing not demodulated (rx_synced.cpp:1331)");
+        N_step = N_eff_TX <= 2 ? 5 : 10;
+        ps_len = N_eff_TX <= 2 ? 6 : 11;
+        Nf = dm.N_b_OCC + 1;
+        mod = N_eff_TX > 1 ? txdiv_modulo(N_eff_TX) : 1;
+        stage.assign(ps_len, std::vector<std::vector<cd>>(N_RX));
+        zf.assign(N_RX, std::vector<std::vector<cd>>(8));
+        zfi = zf;
+        chest = zf;
+        prof = chest_profiles(cfg.u_max);
+        for (int i = 0; i < 3; ++i) {
+            lut0.push_back(build_chest_lut(0, ps.num.b, cfg.b_max, prof[i]));
+            lut_lr.push_back(build_chest_lut(N_step, ps.num.b, cfg.b_max, prof[i]));
+        }
+        drs = drs_schedule(N_eff_TX, ps.N_DF_symb);
+        pcc_cells(ps.num.b, N_eff_TX, pcc_l, pcc_k);
+        pdc_k = pdc_cells_packet(ps.num.b, N_eff_TX, ps.N_DF_symb);
+        stf_y = stf_values(ps.num.b, N_eff_TX);
+        out.pcc_llr.assign(196, 0);
+        out.pcc_llr_f.assign(196, 0);
+        out.pdc_llr.assign(ps.G, 0);
+        out.pdc_llr_f.assign(ps.G, 0);
+
+        resample_all();
+        n_stf = dm.STF_CP_os + dm.N_b_DFT_os;
+        mix_inc0 = phasor_arg(in.cfo_rad);
+        mix_inc1 = mix_inc0;
+        run_stf();
+
+        // ---- PCC phase (rx_synced.cpp:283-302)
+        mode_lr = false;
+        ps_idx = 0;
+        rel = 0;
+        const uint32_t pcc_max = pcc_l.back();
+        for (l_abs = 1; l_abs <= pcc_max; ++l_abs) {
+            next_symbol();
+            if (is_drs(l_abs)) {
+                drs_zf();
+                interpolate();
+            }
+            if (pcc_sym < pcc_l.size() && pcc_l[pcc_sym] == l_abs) pcc_collect();
+            ++rel;
+        }
+        out.snr_pcc_db = static_cast<float>(snr_db());
+
+        // ---- PDC phase, mode lr (rx_synced.cpp:1028-1110)
+        const uint32_t nof_full_ps = (ps.N_DF_symb - (ps_len - N_step)) / N_step;
+        if (cfg.chestim_mode_lr && nof_full_ps > 0) {
+            mode_lr = true;
+            while (ps_idx < nof_full_ps) {
+                const uint32_t first = 1 + ps_idx * N_step, last = ps_len + ps_idx * N_step;
+                if (ps_idx > 0) rel = 1;
+                for (; l_abs <= last; ++l_abs) {
+                    next_symbol();
+                    if (is_drs(l_abs)) drs_zf();
+                    ++rel;
+                }
+                const uint32_t start = ps_idx == 0 ? 0 : 1;
+                for (rel = start; rel <= N_step; ++rel) {
+                    if ((rel - start) % cfg.stride == 0) interpolate();
+                    pdc_collect(first + rel);
+                }
+                ++ps_idx;
+                rel = 0;
+            }
+        }
+        // ---- PDC phase, mode l (rx_synced.cpp:1112-1163)
+        mode_lr = false;
+        if (ps_idx == 0) {
+            rel = 0;
+            for (uint32_t i = 1; i < l_abs; ++i) {
+                pdc_collect(i);
+                ++rel;
+            }
+        }
+        for (; l_abs <= ps.N_DF_symb; ++l_abs) {
+            next_symbol();
+            if (is_drs(l_abs)) {
+                drs_zf();
+                interpolate();
+            }
+            pdc_collect(l_abs);
+            ++rel;
+            if (rel == N_step) {
+                ++ps_idx;
+                rel = 0;
+            }
+        }
+        out.snr_pdc_db = static_cast<float>(snr_db());
+        if (pcc_idx != 98 || pdc_idx != ps.N_PDC_subc || bits_idx != ps.G)
+            throw std::runtime_error("RX cell count mismatch");
+
+        // descrambling (pcc_enc.cpp:297, pdc_enc.cpp:339-344)
+        const auto cp = gold_sequence(0x44454354u, 196);
+        for (uint32_t i = 0; i < 196; ++i)
+            if (cp[i]) {
+                out.pcc_llr[i] = static_cast<int16_t>(-out.pcc_llr[i]);
+                out.pcc_llr_f[i] = -out.pcc_llr_f[i];
+            }
+        const auto cs = gold_sequence(pdc_c_init(in.network_id, in.plcf_type), ps.G);
+        for (uint32_t i = 0; i < ps.G; ++i)
+            if (cs[i]) {
+                out.pdc_llr[i] = static_cast<int16_t>(-out.pdc_llr[i]);
+                out.pdc_llr_f[i] = -out.pdc_llr_f[i];
+            }
+    }
+};
+}  // namespace
+
+template <typename R>
+void rx_packet(const cfg_t& cfg, const packet_sizes_t& ps, const rx_in_t& in, rx_out_t& out) {
+    rx_state_t<R> st(cfg, ps, in, out);
+    st.run();
+}
+
+template void tx_packet<double>(const cfg_t&, const packet_sizes_t&, const tx_desc_t&, const uint8_t*,
+                                const uint8_t*, std::vector<std::vector<std::complex<double>>>&, uint32_t);
+template void tx_packet<float>(const cfg_t&, const packet_sizes_t&, const tx_desc_t&, const uint8_t*,
+                               const uint8_t*, std::vector<std::vector<std::complex<float>>>&, uint32_t);
+template void rx_packet<double>(const cfg_t&, const packet_sizes_t&, const rx_in_t&, rx_out_t&);
+template void rx_packet<float>(const cfg_t&, const packet_sizes_t&, const rx_in_t&, rx_out_t&);
+
+}  // namespace orc

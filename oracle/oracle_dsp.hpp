@@ -1,0 +1,58 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see oracle.hpp header).
+#pragma once
+
+#include <complex>
+#include <cstdint>
+#include <vector>
+
+#include "oracle.hpp"
+
+namespace orc {
+
+struct cfg_t {  // worker_pool_config_t subset: radio device class maxima + resampling
+    uint32_t u_max = 8, b_max = 16, os_min = 1, L = 10, M = 9;
+    bool chestim_mode_lr = true;  // phy.json chestim_mode_lr_default
+    uint32_t stride = 2;          // phy.json chestim_mode_lr_t_stride_default
+};
+
+struct tx_desc_t {  // tx_descriptor_t + tx_meta_t subset (tx_descriptor.hpp, tx_meta.hpp)
+    uint32_t codebook_index = 0, network_id = 0, plcf_type = 1, GI_percentage = 5;
+    float DAC_scale = 1.0f;
+    bool optimal_scaling_DAC = false;
+    double iq_phase_rad = 0.0, iq_phase_increment_rad = 0.0;
+};
+
+struct rx_in_t {  // sync_report_t subset + HARQ scrambling parameters
+    const float* iq;  // [N_RX][S_in] interleaved cf32
+    uint32_t N_RX, S_in;
+    int64_t fine_peak;  // sync_report_t::fine_peak_time_64 relative to iq[0]
+    double cfo_rad;     // cfo_fractional_rad + cfo_integer_rad
+    uint32_t network_id, plcf_type;
+};
+
+struct rx_out_t {
+    std::vector<int16_t> pcc_llr, pdc_llr;   // descrambled
+    std::vector<float> pcc_llr_f, pdc_llr_f; // pre-quantisation values, descrambled
+    std::vector<float> rms;
+    float cfo_fine_rad = 0, sto_fractional = 0, snr_pcc_db = 0, snr_pdc_db = 0;
+};
+
+struct dims_t {
+    uint32_t N_b_DFT_os, N_b_DFT, N_b_OCC, off_lower, CP_os, STF_CP_os;
+    uint32_t N_no_GI_os, N_no_GI_os_rs, N_packet_os_rs, n_pattern, pattern_len;
+    void init(const cfg_t& cfg, const packet_sizes_t& ps);
+    uint32_t transmit_len(uint32_t gi_percentage) const;
+};
+
+uint32_t pdc_c_init(uint32_t network_id, uint32_t plcf_type);
+void demap_float(const cd& y, uint32_t N_bps, double* L);
+int16_t llr_to_i16(double v);
+
+template <typename R>
+void tx_packet(const cfg_t& cfg, const packet_sizes_t& ps, const tx_desc_t& d, const uint8_t* pcc_d,
+               const uint8_t* pdc_d, std::vector<std::vector<std::complex<R>>>& out, uint32_t S_slot);
+
+template <typename R>
+void rx_packet(const cfg_t& cfg, const packet_sizes_t& ps, const rx_in_t& in, rx_out_t& out);
+
+}  // namespace orc

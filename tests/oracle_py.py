@@ -1,0 +1,122 @@
+"""ctypes bindings to oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg. The product path
+(dect-nr-plus-sdr_amd/) never imports this module.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+_lib = None
+
+U32P = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+F32P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+F64P = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+U8P = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+I16P = np.ctypeslib.ndpointer(dtype=np.int16, flags="C_CONTIGUOUS")
+
+PS_FIELDS = ["N_PACKET_symb", "N_DF_symb", "N_PDC_subc", "N_DRS_subc", "G", "N_PDC_bits", "N_TB_bits", "C",
+             "N_samples_STF", "N_samples_STF_CP_only", "N_samples_DF", "N_samples_GI",
+             "N_samples_packet_no_GI", "N_samples_packet", "N_bps", "N_eff_TX", "N_SS", "N_TS", "N_TX",
+             "N_b_DFT", "N_b_OCC"]
+DIM_FIELDS = ["N_b_DFT_os", "off_lower", "CP_os", "STF_CP_os", "N_no_GI_os", "N_no_GI_os_rs", "N_packet_os_rs"]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
+                           stdout=subprocess.DEVNULL)
+        L = C.CDLL(LIB_PATH)
+        L.oracle_packet_sizes.argtypes = [U32P, U32P]
+        L.oracle_dims.argtypes = [U32P, U32P, U32P]
+        L.oracle_kaiser.argtypes = [C.c_float, C.c_float, C.c_float, C.c_float, C.c_uint32, F32P]
+        L.oracle_gold.argtypes = [C.c_uint32, C.c_uint32, U8P]
+        L.oracle_stf.argtypes = [C.c_uint32, C.c_uint32, F64P]
+        L.oracle_pdc_cells.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, U32P, U32P]
+        L.oracle_pcc_cells.argtypes = [C.c_uint32, C.c_uint32, U32P, U32P]
+        L.oracle_chest_lut.argtypes = [C.c_uint32] * 5 + [U32P, U32P, F32P, C.c_uint32]
+        L.oracle_tx.argtypes = [U32P, U32P, U32P, F64P, U8P, U8P, F32P, C.c_uint32, C.c_int]
+        L.oracle_rx.argtypes = [U32P, U32P, C.c_uint32, F32P, C.c_uint32, C.c_int64, C.c_double, C.c_uint32,
+                                C.c_uint32, I16P, I16P, C.c_void_p, C.c_void_p, F32P, C.c_int]
+        L.oracle_loopback_timed.argtypes = [U32P, U32P, C.c_uint32, C.c_uint32, C.c_uint64]
+        L.oracle_loopback_timed.restype = C.c_double
+        _lib = L
+    return _lib
+
+
+def psdef(u, b, plt, pl, tm, mcs, Z=6144):
+    return np.array([u, b, plt, pl, tm, mcs, Z], dtype=np.uint32)
+
+
+def cfg(u_max, b_max, os_min=1, L=10, M=9, lr=1, stride=2):
+    return np.array([u_max, b_max, os_min, L, M, lr, stride], dtype=np.uint32)
+
+
+def packet_sizes(ps):
+    out = np.zeros(len(PS_FIELDS), dtype=np.uint32)
+    if lib().oracle_packet_sizes(np.asarray(ps, dtype=np.uint32), out) != 0:
+        return None
+    return dict(zip(PS_FIELDS, (int(x) for x in out)))
+
+
+def dims(cf, ps):
+    out = np.zeros(len(DIM_FIELDS), dtype=np.uint32)
+    assert lib().oracle_dims(cf, ps, out) == 0
+    return dict(zip(DIM_FIELDS, (int(x) for x in out)))
+
+
+def kaiser(fp, fs, ripple, att):
+    out = np.zeros(4096, dtype=np.float32)
+    n = lib().oracle_kaiser(fp, fs, ripple, att, 4096, out)
+    return out[:n].copy()
+
+
+def gold(c_init, n):
+    out = np.zeros(n, dtype=np.uint8)
+    lib().oracle_gold(c_init, n, out)
+    return out
+
+
+def tx(cf, ps, pcc_d, pdc_d, S_slot, codebook=0, network_id=100, plcf_type=1, gi=5, dac=1.0, phase=0.0,
+       phase_inc=0.0, use_float=False):
+    sz = packet_sizes(ps)
+    out = np.zeros((sz["N_TX"], S_slot, 2), dtype=np.float32)
+    du = np.array([codebook, network_id, plcf_type, gi], dtype=np.uint32)
+    df = np.array([dac, phase, phase_inc], dtype=np.float64)
+    n = lib().oracle_tx(cf, ps, du, df, np.ascontiguousarray(pcc_d, dtype=np.uint8),
+                        np.ascontiguousarray(pdc_d, dtype=np.uint8), out, S_slot, int(use_float))
+    assert n > 0, n
+    return out.view(np.complex64)[..., 0], n
+
+
+def rx(cf, ps, iq, fine_peak=0, cfo_rad=0.0, network_id=100, plcf_type=1, use_float=False):
+    """iq: complex64 [N_RX, S_in]. Returns dict with int16/float LLRs and meta."""
+    sz = packet_sizes(ps)
+    iq = np.ascontiguousarray(iq, dtype=np.complex64)
+    n_rx, s_in = iq.shape
+    pcc = np.zeros(196, dtype=np.int16)
+    pdc = np.zeros(sz["G"], dtype=np.int16)
+    pccf = np.zeros(196, dtype=np.float32)
+    pdcf = np.zeros(sz["G"], dtype=np.float32)
+    meta = np.zeros(12, dtype=np.float32)
+    r = lib().oracle_rx(cf, ps, n_rx, iq.view(np.float32).reshape(-1), s_in, int(fine_peak), float(cfo_rad),
+                        network_id, plcf_type, pcc, pdc, pccf.ctypes.data, pdcf.ctypes.data, meta,
+                        int(use_float))
+    assert r == 0, r
+    return dict(pcc_llr=pcc, pdc_llr=pdc, pcc_llr_f=pccf, pdc_llr_f=pdcf, rms=meta[:8].copy(),
+                cfo_fine=float(meta[8]), sto=float(meta[9]), snr_pcc=float(meta[10]), snr_pdc=float(meta[11]))
+
+
+def loopback_timed(cf, ps, n_packets, n_threads, seed=0xDEC7):
+    return lib().oracle_loopback_timed(cf, ps, n_packets, n_threads, seed)
+
+
+def pack_bits(bits):
+    return np.packbits(np.asarray(bits, dtype=np.uint8))
