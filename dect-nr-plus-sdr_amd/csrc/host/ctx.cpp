@@ -1,0 +1,737 @@
+// C-ABI implementation (include/dnrp.h): context, per-configuration device tables, network-ID
+// scrambling sequences, batched TX / RX phase launches.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../kernels/kernels.hpp"
+#include "dnrp.h"
+#include "geometry.hpp"
+
+using namespace dnrp;
+
+namespace {
+
+#define HIPCHK(x)                                  \
+    do {                                           \
+        if ((x) != hipSuccess) return DNRP_EDEVICE; \
+    } while (0)
+
+// device buffer owning wrapper
+struct dbuf {
+    void* p = nullptr;
+    size_t n = 0;
+    dbuf() = default;
+    dbuf(const dbuf&) = delete;
+    dbuf& operator=(const dbuf&) = delete;
+    ~dbuf() {
+        if (p) (void)hipFree(p);
+    }
+    bool ensure(size_t bytes) {
+        if (bytes <= n) return true;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) return false;
+        n = bytes;
+        return true;
+    }
+    template <typename T>
+    bool upload(const std::vector<T>& v) {
+        if (!ensure(std::max<size_t>(v.size() * sizeof(T), 16))) return false;
+        return hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
+    }
+    template <typename T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+struct pinned {
+    void* p = nullptr;
+    size_t n = 0;
+    hipEvent_t ev = nullptr;
+    ~pinned() {
+        if (p) (void)hipHostFree(p);
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    void* get(size_t bytes) {
+        if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        (void)hipEventSynchronize(ev);  // previous async copy out of this buffer is done
+        if (bytes > n) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            n = 0;
+            if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+            n = bytes;
+        }
+        return p;
+    }
+};
+
+dev::fft_plan make_plan(uint32_t N) {
+    dev::fft_plan p{};
+    p.N = N;
+    uint32_t r = N;
+    while (r % 4 == 0 && r > 1) {
+        p.radix[p.nr++] = 4;
+        r /= 4;
+    }
+    while (r % 2 == 0) {
+        p.radix[p.nr++] = 2;
+        r /= 2;
+    }
+    while (r % 3 == 0) {
+        p.radix[p.nr++] = 3;
+        r /= 3;
+    }
+    return p;  // r must be 1 (sizes 64..16384 of tx_rx.hpp:67-69)
+}
+
+std::vector<float2> twiddles(uint32_t N) {
+    std::vector<float2> t(N);
+    for (uint32_t j = 0; j < N; ++j) {
+        const double a = -2.0 * M_PI * static_cast<double>(j) / static_cast<double>(N);
+        t[j] = make_float2(static_cast<float>(std::cos(a)), static_cast<float>(std::sin(a)));
+    }
+    return t;
+}
+
+std::vector<float2> constellation(uint32_t N_bps) {  // 3GPP TS 36.211 §7.1, index bits MSB first
+    const uint32_t n = 1u << N_bps;
+    std::vector<float2> t(n);
+    auto bit = [&](uint32_t i, uint32_t k) { return static_cast<int>((i >> (N_bps - 1 - k)) & 1u); };
+    for (uint32_t i = 0; i < n; ++i) {
+        double re = 0, im = 0, nrm = 1;
+        switch (N_bps) {
+            case 1:
+                re = im = 1 - 2 * bit(i, 0);
+                nrm = std::sqrt(2.0);
+                break;
+            case 2:
+                re = 1 - 2 * bit(i, 0);
+                im = 1 - 2 * bit(i, 1);
+                nrm = std::sqrt(2.0);
+                break;
+            case 4:
+                re = (1 - 2 * bit(i, 0)) * (2 - (1 - 2 * bit(i, 2)));
+                im = (1 - 2 * bit(i, 1)) * (2 - (1 - 2 * bit(i, 3)));
+                nrm = std::sqrt(10.0);
+                break;
+            case 6:
+                re = (1 - 2 * bit(i, 0)) * (4 - (1 - 2 * bit(i, 2)) * (2 - (1 - 2 * bit(i, 4))));
+                im = (1 - 2 * bit(i, 1)) * (4 - (1 - 2 * bit(i, 3)) * (2 - (1 - 2 * bit(i, 5))));
+                nrm = std::sqrt(42.0);
+                break;
+            default:
+                re = (1 - 2 * bit(i, 0)) * (8 - (1 - 2 * bit(i, 2)) * (4 - (1 - 2 * bit(i, 4)) * (2 - (1 - 2 * bit(i, 6)))));
+                im = (1 - 2 * bit(i, 1)) * (8 - (1 - 2 * bit(i, 3)) * (4 - (1 - 2 * bit(i, 5)) * (2 - (1 - 2 * bit(i, 7)))));
+                nrm = std::sqrt(170.0);
+                break;
+        }
+        t[i] = make_float2(static_cast<float>(re / nrm), static_cast<float>(im / nrm));
+    }
+    return t;
+}
+
+double phasor_arg(double rad) {  // mixer_t::set_phase* builds float phasors (mixer.cpp:27-33)
+    const float c = std::cos(static_cast<float>(rad)), s = std::sin(static_cast<float>(rad));
+    return std::atan2(static_cast<double>(s), static_cast<double>(c));
+}
+
+void fill_pairs(uint32_t N_TS, uint32_t* pair, uint32_t& mod) {  // transmit_diversity_precoding.cpp:48-75
+    static const uint32_t P4[6][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {0, 3}, {1, 2}};
+    static const uint32_t P8[12][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 4}, {1, 5},
+                                       {2, 6}, {3, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}};
+    std::memset(pair, 0, 12 * sizeof(uint32_t));
+    if (N_TS <= 1) {
+        mod = 1;
+    } else if (N_TS == 2) {
+        mod = 1;
+        pair[0] = 0 | (1u << 4);
+    } else if (N_TS == 4) {
+        mod = 6;
+        for (int i = 0; i < 6; ++i) pair[i] = P4[i][0] | (P4[i][1] << 4);
+    } else {
+        mod = 12;
+        for (int i = 0; i < 12; ++i) pair[i] = P8[i][0] | (P8[i][1] << 4);
+    }
+}
+
+struct tx_tables {
+    dnrp_packet_sizes q{};
+    geo::tm_t tm{};
+    geo::dims_t dm{};
+    dev::fft_plan plan{};
+    geo::resampler_t rs;
+    dbuf code, stf, W, taps, tw, qam, qpsk;
+    std::vector<float> wscale;  // per codebook
+};
+
+struct rx1_tables {  // per (u, b, N_eff_TX): STF/PCC phase
+    uint32_t u, b, N_eff_TX, Nd, N_occ, off_lower, CP, STF_CP, n_pattern, pattern_len;
+    dev::fft_plan plan{};
+    geo::resampler_t rs;
+    geo::maps_t maps;
+    uint32_t pcc_max = 0, n_pcc_ops = 0;
+    dbuf stf, tw, taps, drs_l, drs_meta, drs_k, drs_v, pcc_k, pcc_off, pcc_ops;
+    dbuf lut_pw[2][3], lut_w[2][3];
+    uint32_t lut_n[2][3] = {}, lut_T[2] = {};
+};
+
+struct rx2_tables {  // per (psdef): PDC phase
+    dnrp_packet_sizes q{};
+    geo::maps_t maps;
+    uint32_t n_pdc_ops = 0;
+    dbuf drs_l, drs_meta, pdc_k, pdc_off, pdc_ops;
+};
+
+struct netid_seq {
+    uint32_t nbits = 0;
+    dbuf t1, t2;
+};
+
+}  // namespace
+
+struct dnrp_ctx {
+    dnrp_cfg cfg{};
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, std::unique_ptr<tx_tables>> txt;
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::unique_ptr<rx1_tables>> rx1t;
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, std::unique_ptr<rx2_tables>> rx2t;
+    std::map<uint32_t, std::unique_ptr<netid_seq>> netid;
+    dbuf pcc_seq;
+    // batch scratch
+    dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs;
+    pinned st_tx, st_rxin, st_seq, st_rep;
+    // retained RX phase-1 state
+    rx1_tables* rx1_last = nullptr;
+    uint32_t rx_n = 0, rx_S_in = 0, rx_nsym_cap = 0, rx_Nf_pad = 0;
+    const float* rx_iq = nullptr;
+    std::vector<dev::rx_pkt_in> rx_pin_host;
+    // timing
+    bool timing = false;
+    std::map<std::string, std::pair<hipEvent_t, hipEvent_t>> ev;
+    ~dnrp_ctx() {
+        for (auto& e : ev) {
+            (void)hipEventDestroy(e.second.first);
+            (void)hipEventDestroy(e.second.second);
+        }
+    }
+    void tic(const char* name, hipStream_t s) {
+        if (!timing) return;
+        auto& e = ev[name];
+        if (!e.first) {
+            (void)hipEventCreate(&e.first);
+            (void)hipEventCreate(&e.second);
+        }
+        (void)hipEventRecord(e.first, s);
+    }
+    void toc(const char* name, hipStream_t s) {
+        if (!timing) return;
+        (void)hipEventRecord(ev[name].second, s);
+    }
+};
+
+namespace {
+
+uint32_t G_cap_default(const dnrp_cfg& c) {
+    // scrambling sequences cover at least one PacketLength=2 slot packet of the device class
+    dnrp_psdef d{c.u_max, c.b_max, 1, 2, 0, 9, 6144};
+    dnrp_packet_sizes q;
+    if (geo::packet_sizes(d, q)) return q.G;
+    return 1u << 20;
+}
+
+int ensure_seq(dnrp_ctx* ctx, netid_seq& s, uint32_t nid, uint32_t nbits) {
+    if (s.nbits >= nbits) return DNRP_OK;
+    const uint32_t len = std::max(nbits, G_cap_default(ctx->cfg));
+    // scrambling_pdc.cpp:41-48: type 1 c_init = id & 0xFF, type 2 c_init = id >> 8
+    if (!s.t1.upload(geo::gold_bits_packed(nid & 0xFFu, len))) return DNRP_ENOMEM;
+    if (!s.t2.upload(geo::gold_bits_packed(nid >> 8, len))) return DNRP_ENOMEM;
+    s.nbits = len;
+    return DNRP_OK;
+}
+
+tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
+    const auto key = std::make_tuple(d.u, d.b, d.PacketLengthType, d.PacketLength, d.tm_mode_index, d.mcs_index, d.Z);
+    auto it = ctx->txt.find(key);
+    if (it != ctx->txt.end()) return it->second.get();
+    auto t = std::make_unique<tx_tables>();
+    if (!geo::packet_sizes(d, t->q, &t->tm)) {
+        *err = DNRP_ECONFIG;
+        return nullptr;
+    }
+    const auto& c = ctx->cfg;
+    if (d.u > c.u_max || d.b > c.b_max || t->q.N_TX > c.N_TX_max || t->q.N_bps > 8) {
+        *err = DNRP_EUNSUPPORTED;
+        return nullptr;
+    }
+    t->dm = geo::make_dims(c, d, t->q);
+    t->plan = make_plan(t->dm.Nd);
+    t->rs = geo::make_resampler(c.L, c.M, c.os_min);
+    const auto m = geo::build_maps(d.b, t->tm.N_TS, t->tm.N_eff_TX, t->q.N_DF_symb);
+    std::vector<float2> stf(m.Nf);
+    for (uint32_t k = 0; k < m.Nf; ++k) stf[k] = make_float2(m.stf[k].real(), m.stf[k].imag());
+    std::vector<float2> W;
+    const uint32_t ncb = geo::W_codebooks(t->tm.N_TS, t->tm.N_TX);
+    for (uint32_t cb = 0; cb < ncb; ++cb) {
+        float s = 1.0f;
+        for (const auto& w : geo::W_matrix(t->tm.N_TS, t->tm.N_TX, cb, &s)) W.push_back(make_float2(w.real(), w.imag()));
+        t->wscale.push_back(s);
+    }
+    if (!t->code.upload(m.code) || !t->stf.upload(stf) || !t->W.upload(W) || !t->taps.upload(t->rs.h) ||
+        !t->tw.upload(twiddles(t->dm.Nd)) || !t->qam.upload(constellation(t->q.N_bps)) ||
+        !t->qpsk.upload(constellation(2))) {
+        *err = DNRP_ENOMEM;
+        return nullptr;
+    }
+    auto* r = t.get();
+    ctx->txt[key] = std::move(t);
+    return r;
+}
+
+rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, int* err) {
+    const auto key = std::make_tuple(u, b, N_eff_TX);
+    auto it = ctx->rx1t.find(key);
+    if (it != ctx->rx1t.end()) return it->second.get();
+    const auto& c = ctx->cfg;
+    if (!(N_eff_TX == 1 || N_eff_TX == 2 || N_eff_TX == 4)) {  // N_eff_TX = 8 PCC ps LUT, see DESIGN.md
+        *err = DNRP_EUNSUPPORTED;
+        return nullptr;
+    }
+    if (u > c.u_max || b > c.b_max || N_eff_TX > c.N_TX_max) {
+        *err = DNRP_EUNSUPPORTED;
+        return nullptr;
+    }
+    auto t = std::make_unique<rx1_tables>();
+    t->u = u;
+    t->b = b;
+    t->N_eff_TX = N_eff_TX;
+    const uint64_t rate = uint64_t(c.u_max) * c.b_max * 1728000ull * c.os_min;
+    t->Nd = static_cast<uint32_t>(rate / (uint64_t(u) * 27000ull));
+    t->N_occ = 56 * b;
+    t->off_lower = 32 * b + (t->Nd - 64 * b) + 4 * b;
+    t->CP = 8 * b * t->Nd / (64 * b);
+    const uint32_t stf = u == 1 ? 112 * b : 144 * b;
+    t->STF_CP = (stf - 64 * b) * t->Nd / (64 * b);
+    t->n_pattern = u == 1 ? 7 : 9;
+    t->pattern_len = 16 * b * t->Nd / (64 * b);
+    t->plan = make_plan(t->Nd);
+    t->rs = geo::make_resampler(c.M, c.L, c.os_min);  // RX swaps L and M (rx_synced.cpp:65-73)
+    t->maps = geo::build_maps(b, N_eff_TX, N_eff_TX, 20);
+    std::vector<geo::op_t> pcc_ops, dummy;
+    geo::build_rx_ops(t->maps, N_eff_TX, 20, c.chestim_mode_lr != 0, std::max(1u, c.chestim_lr_stride), pcc_ops, dummy,
+                      t->pcc_max);
+    t->n_pcc_ops = static_cast<uint32_t>(pcc_ops.size());
+    std::vector<float2> stfv(t->maps.Nf);
+    for (uint32_t k = 0; k < t->maps.Nf; ++k) stfv[k] = make_float2(t->maps.stf[k].real(), t->maps.stf[k].imag());
+    std::vector<uint32_t> dl, dm;
+    for (const auto& d : t->maps.drs) {
+        dl.push_back(d.l);
+        dm.push_back(d.ts_first | (d.ts_last << 8) | (d.parity << 16));
+    }
+    bool ok = t->stf.upload(stfv) && t->tw.upload(twiddles(t->Nd)) && t->taps.upload(t->rs.h) && t->drs_l.upload(dl) &&
+              t->drs_meta.upload(dm) && t->drs_k.upload(t->maps.drs_k) && t->drs_v.upload(t->maps.drs_v) &&
+              t->pcc_k.upload(t->maps.pcc_k) && t->pcc_off.upload(t->maps.pcc_sym_off) && t->pcc_ops.upload(pcc_ops);
+    const uint32_t Nsv = N_eff_TX <= 2 ? 5 : 10;
+    for (uint32_t mode = 0; mode < 2 && ok; ++mode)
+        for (uint32_t p = 0; p < 3 && ok; ++p) {
+            const auto L = geo::build_lut(mode ? Nsv : 0, b, c.b_max, c.u_max, p);
+            ok = t->lut_pw[mode][p].upload(L.pilot_weight) && t->lut_w[mode][p].upload(L.weights);
+            t->lut_n[mode][p] = L.n;
+            t->lut_T[mode] = L.T;
+        }
+    if (!ok) {
+        *err = DNRP_ENOMEM;
+        return nullptr;
+    }
+    auto* r = t.get();
+    ctx->rx1t[key] = std::move(t);
+    return r;
+}
+
+rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
+    const auto key = std::make_tuple(d.u, d.b, d.PacketLengthType, d.PacketLength, d.tm_mode_index, d.mcs_index, d.Z);
+    auto it = ctx->rx2t.find(key);
+    if (it != ctx->rx2t.end()) return it->second.get();
+    auto t = std::make_unique<rx2_tables>();
+    geo::tm_t tm;
+    if (!geo::packet_sizes(d, t->q, &tm)) {
+        *err = DNRP_ECONFIG;
+        return nullptr;
+    }
+    if (tm.N_SS > 1 || tm.N_eff_TX > 4 || t->q.N_bps > 8) {  // rx_synced.cpp:1331-1333 (AxA MIMO is \todo)
+        *err = DNRP_EUNSUPPORTED;
+        return nullptr;
+    }
+    t->maps = geo::build_maps(d.b, tm.N_TS, tm.N_eff_TX, t->q.N_DF_symb);
+    std::vector<geo::op_t> pcc_ops, pdc_ops;
+    uint32_t pm;
+    geo::build_rx_ops(t->maps, tm.N_eff_TX, t->q.N_DF_symb, ctx->cfg.chestim_mode_lr != 0,
+                      std::max(1u, ctx->cfg.chestim_lr_stride), pcc_ops, pdc_ops, pm);
+    t->n_pdc_ops = static_cast<uint32_t>(pdc_ops.size());
+    std::vector<uint32_t> dl, dm;
+    for (const auto& x : t->maps.drs) {
+        dl.push_back(x.l);
+        dm.push_back(x.ts_first | (x.ts_last << 8) | (x.parity << 16));
+    }
+    if (!t->drs_l.upload(dl) || !t->drs_meta.upload(dm) || !t->pdc_k.upload(t->maps.pdc_k) ||
+        !t->pdc_off.upload(t->maps.pdc_sym_off) || !t->pdc_ops.upload(pdc_ops)) {
+        *err = DNRP_ENOMEM;
+        return nullptr;
+    }
+    auto* r = t.get();
+    ctx->rx2t[key] = std::move(t);
+    return r;
+}
+
+dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t) {
+    dev::rx_front_args a{};
+    a.plan = t->plan;
+    a.N_occ = t->N_occ;
+    a.off_lower = t->off_lower;
+    a.CP = t->CP;
+    a.STF_CP = t->STF_CP;
+    a.N_RX = ctx->cfg.N_TX_max;
+    a.S_in = ctx->rx_S_in;
+    a.n_pattern = t->n_pattern;
+    a.pattern_len = t->pattern_len;
+    a.b = t->b;
+    a.L = t->rs.L;
+    a.M = t->rs.M;
+    a.delay = t->rs.delay;
+    a.hl = t->rs.hl;
+    a.sym_per_block = 4;
+    a.Nf_pad = ctx->rx_Nf_pad;
+    a.n_sym_total = ctx->rx_nsym_cap + 1;
+    a.amp_scale = std::sqrt(static_cast<float>(t->N_occ)) / static_cast<float>(t->Nd);
+    a.taps = t->taps.as<float>();
+    a.tw = t->tw.as<float2>();
+    a.stf = t->stf.as<float2>();
+    a.iq = reinterpret_cast<const float2*>(ctx->rx_iq);
+    a.pin = ctx->rx_in.as<dev::rx_pkt_in>();
+    a.st = ctx->rx_st.as<dev::rx_pkt_state>();
+    a.Y = ctx->Y.as<float2>();
+    return a;
+}
+
+dev::rx_back_args back_args(dnrp_ctx* ctx, rx1_tables* t) {
+    dev::rx_back_args a{};
+    a.N_occ = t->N_occ;
+    a.N_RX = ctx->cfg.N_TX_max;
+    a.N_eff_TX = t->N_eff_TX;
+    a.Nf_pad = ctx->rx_Nf_pad;
+    a.n_sym_total = ctx->rx_nsym_cap + 1;
+    a.n_drs = t->N_occ / 4;
+    fill_pairs(t->N_eff_TX, a.pair, a.mod);
+    a.txdiv = t->N_eff_TX > 1;
+    a.drs_k = t->drs_k.as<uint32_t>();
+    a.drs_v = t->drs_v.as<float>();
+    a.pcc_k = t->pcc_k.as<uint32_t>();
+    a.pcc_off = t->pcc_off.as<uint32_t>();
+    for (int m = 0; m < 2; ++m) {
+        a.lut_T[m] = t->lut_T[m];
+        for (int p = 0; p < 3; ++p) {
+            a.lut_pw[m][p] = t->lut_pw[m][p].as<uint32_t>();
+            a.lut_w[m][p] = t->lut_w[m][p].as<float>();
+            a.lut_n[m][p] = t->lut_n[m][p];
+        }
+    }
+    for (int p = 0; p < 3; ++p) a.prof_snr[p] = geo::lut_profile_snr_db(p);
+    a.Y = ctx->Y.as<float2>();
+    a.st = ctx->rx_st.as<dev::rx_pkt_state>();
+    a.pcc_seq = ctx->pcc_seq.as<uint8_t>();
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dnrp_strerror(int code) {
+    switch (code) {
+        case DNRP_OK: return "ok";
+        case DNRP_EINVAL: return "invalid argument";
+        case DNRP_ECONFIG: return "invalid packet configuration";
+        case DNRP_EUNSUPPORTED: return "configuration not supported by the reference receiver";
+        case DNRP_ENOMEM: return "device memory allocation failed or batch too large";
+        case DNRP_EDEVICE: return "HIP runtime error";
+        case DNRP_ENETID: return "network ID not registered";
+        case DNRP_ESTATE: return "no preceding dnrp_rx_pcc_batch";
+        default: return "unknown error";
+    }
+}
+
+int dnrp_ctx_create(const dnrp_cfg* cfg, dnrp_ctx** out) {
+    if (!cfg || !out) return DNRP_EINVAL;
+    *out = nullptr;
+    const auto& c = *cfg;
+    const bool uok = c.u_max == 1 || c.u_max == 2 || c.u_max == 4 || c.u_max == 8;
+    const bool bok = c.b_max == 1 || c.b_max == 2 || c.b_max == 4 || c.b_max == 8 || c.b_max == 12 || c.b_max == 16;
+    const bool nok = c.N_TX_max == 1 || c.N_TX_max == 2 || c.N_TX_max == 4 || c.N_TX_max == 8;
+    const bool ook = c.os_min == 1 || c.os_min == 2 || c.os_min == 4 || c.os_min == 8;
+    if (!uok || !bok || !nok || !ook || c.L == 0 || c.M == 0 || c.max_batch == 0) return DNRP_EINVAL;
+    if (!((c.L == 1 && c.M == 1) || c.L > c.M)) return DNRP_EINVAL;  // TX up-samples (rx_pacer.cpp:50-52)
+    if (hipSetDevice(c.device) != hipSuccess) return DNRP_EDEVICE;
+    auto ctx = std::make_unique<dnrp_ctx>();
+    ctx->cfg = c;
+    if (ctx->cfg.chestim_lr_stride == 0) ctx->cfg.chestim_lr_stride = 1;
+    const char* tm = std::getenv("DNRP_TIMING");
+    ctx->timing = tm && tm[0] == '1';
+    if (!ctx->pcc_seq.upload(geo::gold_bits_packed(0x44454354u, 200))) return DNRP_ENOMEM;  // pcc_enc.cpp:46,104
+    *out = ctx.release();
+    return DNRP_OK;
+}
+
+int dnrp_ctx_destroy(dnrp_ctx* ctx) {
+    if (!ctx) return DNRP_EINVAL;
+    (void)hipSetDevice(ctx->cfg.device);
+    (void)hipDeviceSynchronize();
+    delete ctx;
+    return DNRP_OK;
+}
+
+int dnrp_add_network_id(dnrp_ctx* ctx, uint32_t network_id) {
+    if (!ctx) return DNRP_EINVAL;
+    auto& s = ctx->netid[network_id];
+    if (!s) s = std::make_unique<netid_seq>();
+    return ensure_seq(ctx, *s, network_id, G_cap_default(ctx->cfg));
+}
+
+int dnrp_get_packet_sizes(const dnrp_ctx* ctx, const dnrp_psdef* d, dnrp_packet_sizes* out) {
+    if (!ctx || !d || !out) return DNRP_EINVAL;
+    dnrp_packet_sizes q;
+    if (!geo::packet_sizes(*d, q)) return DNRP_ECONFIG;
+    if (d->u > ctx->cfg.u_max || d->b > ctx->cfg.b_max) return DNRP_EUNSUPPORTED;
+    const auto dm = geo::make_dims(ctx->cfg, *d, q);
+    q.N_b_DFT_os = dm.Nd;
+    q.N_samples_packet_no_GI_os_rs = dm.N_no_GI_rs;
+    q.N_samples_packet_os_rs = dm.N_packet_rs;
+    *out = q;
+    return DNRP_OK;
+}
+
+int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp_tx_desc* desc, const uint8_t* pcc_d,
+                  const uint8_t* pdc_d, uint32_t pdc_stride, float* iq_out, uint32_t S, void* stream) {
+    if (!ctx || !psdef || (n > 0 && (!desc || !pcc_d || !pdc_d || !iq_out))) return DNRP_EINVAL;
+    if (n == 0) return DNRP_OK;
+    if (n > ctx->cfg.max_batch) return DNRP_ENOMEM;
+    (void)hipSetDevice(ctx->cfg.device);
+    int err = DNRP_OK;
+    tx_tables* t = get_tx(ctx, *psdef, &err);
+    if (!t) return err;
+    if (S < t->dm.N_packet_rs || pdc_stride < (t->q.G + 7) / 8) return DNRP_EINVAL;
+    auto* pk = static_cast<dev::tx_pkt*>(ctx->st_tx.get(sizeof(dev::tx_pkt) * n));
+    if (!pk) return DNRP_ENOMEM;
+    for (uint32_t i = 0; i < n; ++i) {
+        const auto& d = desc[i];
+        if ((d.plcf_type != 1 && d.plcf_type != 2) || d.GI_percentage > 100) return DNRP_EINVAL;
+        if (d.codebook_index >= t->wscale.size()) return DNRP_EINVAL;
+        if (d.optimal_scaling_DAC) return DNRP_EUNSUPPORTED;
+        auto it = ctx->netid.find(d.network_id);
+        if (it == ctx->netid.end()) return DNRP_ENETID;
+        if ((err = ensure_seq(ctx, *it->second, d.network_id, t->q.G)) != DNRP_OK) return err;
+        pk[i].pdc_seq = (d.plcf_type == 1 ? it->second->t1 : it->second->t2).as<uint8_t>();
+        pk[i].codebook = d.codebook_index;
+        const float sc = d.DAC_scale * t->wscale[d.codebook_index];  // tx.cpp:582-594
+        pk[i].scale_stf = 1.0f / std::sqrt(static_cast<float>(t->q.N_b_OCC / 4)) * sc;
+        pk[i].scale_df = 1.0f / std::sqrt(static_cast<float>(t->q.N_b_OCC)) * sc;
+        pk[i].ph0 = phasor_arg(d.iq_phase_rad);
+        pk[i].inc = phasor_arg(d.iq_phase_increment_s2s_post_resampling_rad);
+        pk[i].do_mix = (pk[i].ph0 != 0.0 || pk[i].inc != 0.0) ? 1u : 0u;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (!ctx->tx_pk.ensure(sizeof(dev::tx_pkt) * ctx->cfg.max_batch)) return DNRP_ENOMEM;
+    HIPCHK(hipMemcpyAsync(ctx->tx_pk.p, pk, sizeof(dev::tx_pkt) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(ctx->st_tx.ev, st));
+    dev::tx_args a{};
+    a.plan = t->plan;
+    a.N_occ = t->q.N_b_OCC;
+    a.off_lower = t->dm.off_lower;
+    a.CP = t->dm.CP;
+    a.STF_CP = t->dm.STF_CP;
+    a.N_DF = t->q.N_DF_symb;
+    a.N_TS = t->tm.N_TS;
+    a.N_TX = t->tm.N_TX;
+    a.N_SS = t->tm.N_SS;
+    a.N_bps = t->q.N_bps;
+    a.txdiv = t->tm.txdiv;
+    fill_pairs(t->tm.N_TS, a.pair, a.mod);
+    a.pattern_len = t->dm.pattern_len;
+    a.L = t->rs.L;
+    a.M = t->rs.M;
+    a.delay = t->rs.delay;
+    a.hl = t->rs.hl;
+    a.n_keep = std::min(t->dm.N_no_GI_rs, S);
+    a.S = S;
+    a.pdc_stride = pdc_stride;
+    a.G = t->q.G;
+    a.xbuf_len = t->rs.hl + t->dm.STF_CP + t->dm.Nd + 16;
+    a.code = t->code.as<uint32_t>();
+    a.stf = t->stf.as<float2>();
+    a.W = t->W.as<float2>();
+    a.taps = t->taps.as<float>();
+    a.tw = t->tw.as<float2>();
+    a.qam = t->qam.as<float2>();
+    a.qpsk = t->qpsk.as<float2>();
+    a.pcc_seq = ctx->pcc_seq.as<uint8_t>();
+    a.pcc_d = pcc_d;
+    a.pdc_d = pdc_d;
+    a.out = iq_out;
+    a.pk = ctx->tx_pk.as<dev::tx_pkt>();
+    ctx->tic("tx", st);
+    if (dev::launch_tx(a, n, st) != hipSuccess) return DNRP_EDEVICE;
+    ctx->toc("tx", st);
+    return DNRP_OK;
+}
+
+int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, const float* iq_in, uint32_t S_in,
+                      int16_t* pcc_llr, dnrp_pcc_report* rep, void* stream) {
+    if (!ctx || (n > 0 && (!sr || !iq_in || !pcc_llr))) return DNRP_EINVAL;
+    if (n == 0) return DNRP_OK;
+    if (n > ctx->cfg.max_batch) return DNRP_ENOMEM;
+    (void)hipSetDevice(ctx->cfg.device);
+    for (uint32_t i = 1; i < n; ++i)
+        if (sr[i].u != sr[0].u || sr[i].b != sr[0].b || sr[i].N_eff_TX != sr[0].N_eff_TX) return DNRP_EINVAL;
+    int err = DNRP_OK;
+    rx1_tables* t = get_rx1(ctx, sr[0].u, sr[0].b, sr[0].N_eff_TX, &err);
+    if (!t) return err;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // symbols that fit into the window: (S_in * M/L - STF) / symbol
+    const uint64_t dect = uint64_t(S_in) * ctx->cfg.M / ctx->cfg.L;
+    const uint64_t n_stf = t->STF_CP + t->Nd;
+    if (dect < n_stf + t->CP + t->Nd) return DNRP_EINVAL;
+    ctx->rx_nsym_cap = static_cast<uint32_t>((dect - n_stf) / (t->CP + t->Nd));
+    if (ctx->rx_nsym_cap < t->pcc_max) return DNRP_EINVAL;
+    ctx->rx_Nf_pad = (t->N_occ + 1 + 63) / 64 * 64;
+    ctx->rx_S_in = S_in;
+    ctx->rx_iq = iq_in;
+    ctx->rx_n = n;
+    const size_t ybytes = size_t(n) * ctx->cfg.N_TX_max * (ctx->rx_nsym_cap + 1) * ctx->rx_Nf_pad * sizeof(float2);
+    if (!ctx->Y.ensure(ybytes) || !ctx->rx_in.ensure(sizeof(dev::rx_pkt_in) * ctx->cfg.max_batch) ||
+        !ctx->rx_st.ensure(sizeof(dev::rx_pkt_state) * ctx->cfg.max_batch))
+        return DNRP_ENOMEM;
+    auto* pin = static_cast<dev::rx_pkt_in*>(ctx->st_rxin.get(sizeof(dev::rx_pkt_in) * n));
+    if (!pin) return DNRP_ENOMEM;
+    for (uint32_t i = 0; i < n; ++i) {
+        pin[i].fine_peak = sr[i].fine_peak_time;
+        pin[i].cfo_rad = sr[i].cfo_fractional_rad + sr[i].cfo_integer_rad;
+        pin[i].inc0 = phasor_arg(pin[i].cfo_rad);
+    }
+    HIPCHK(hipMemcpyAsync(ctx->rx_in.p, pin, sizeof(dev::rx_pkt_in) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(ctx->st_rxin.ev, st));
+    auto fa = front_args(ctx, t);
+    ctx->tic("rx_stf", st);
+    if (dev::launch_rx_stf(fa, n, st) != hipSuccess) return DNRP_EDEVICE;
+    ctx->toc("rx_stf", st);
+    fa.sym_first = 1;
+    fa.sym_count = t->pcc_max;
+    ctx->tic("rx_fft_pcc", st);
+    if (dev::launch_rx_fft(fa, n, st) != hipSuccess) return DNRP_EDEVICE;
+    ctx->toc("rx_fft_pcc", st);
+    auto ba = back_args(ctx, t);
+    ba.ops = t->pcc_ops.as<dev::rx_op>();
+    ba.n_ops = t->n_pcc_ops;
+    ba.drs_l = t->drs_l.as<uint32_t>();
+    ba.drs_meta = t->drs_meta.as<uint32_t>();
+    ba.N_bps = 2;
+    ba.llr = pcc_llr;
+    ba.llr_stride = 196;
+    ba.is_pdc = 0;
+    ctx->tic("rx_pcc", st);
+    if (dev::launch_rx_back(ba, n, st) != hipSuccess) return DNRP_EDEVICE;
+    ctx->toc("rx_pcc", st);
+    ctx->rx1_last = t;
+    if (rep) {
+        std::vector<dev::rx_pkt_state> S(n);
+        HIPCHK(hipMemcpyAsync(S.data(), ctx->rx_st.p, sizeof(dev::rx_pkt_state) * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (uint32_t i = 0; i < n; ++i) {
+            rep[i].snr_dB = S[i].snr_pcc;
+            rep[i].cfo_fractional_rad = sr[i].cfo_fractional_rad + (S[i].cfo_fine - pin[i].cfo_rad);
+            rep[i].sto_fractional = S[i].sto_frac;
+            for (int a = 0; a < 8; ++a) rep[i].rms[a] = S[i].rms[a];
+        }
+    }
+    return DNRP_OK;
+}
+
+int dnrp_rx_pdc_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp_pdc_req* req, int16_t* pdc_llr,
+                      uint32_t llr_stride, dnrp_pdc_report* rep, void* stream) {
+    if (!ctx || !psdef || (n > 0 && (!req || !pdc_llr))) return DNRP_EINVAL;
+    if (n == 0) return DNRP_OK;
+    if (!ctx->rx1_last || n != ctx->rx_n) return DNRP_ESTATE;
+    (void)hipSetDevice(ctx->cfg.device);
+    int err = DNRP_OK;
+    rx2_tables* t2 = get_rx2(ctx, *psdef, &err);
+    if (!t2) return err;
+    rx1_tables* t = ctx->rx1_last;
+    if (psdef->u != t->u || psdef->b != t->b || t2->q.N_eff_TX != t->N_eff_TX) return DNRP_EINVAL;
+    if (t2->q.N_DF_symb > ctx->rx_nsym_cap || llr_stride < t2->q.G) return DNRP_EINVAL;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (!ctx->pdc_seq_ptrs.ensure(sizeof(void*) * ctx->cfg.max_batch)) return DNRP_ENOMEM;
+    auto** seqp = static_cast<const uint8_t**>(ctx->st_seq.get(sizeof(void*) * n));
+    if (!seqp) return DNRP_ENOMEM;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (req[i].plcf_type != 1 && req[i].plcf_type != 2) return DNRP_EINVAL;
+        auto it = ctx->netid.find(req[i].network_id);
+        if (it == ctx->netid.end()) return DNRP_ENETID;
+        if ((err = ensure_seq(ctx, *it->second, req[i].network_id, t2->q.G)) != DNRP_OK) return err;
+        seqp[i] = (req[i].plcf_type == 1 ? it->second->t1 : it->second->t2).as<uint8_t>();
+    }
+    HIPCHK(hipMemcpyAsync(ctx->pdc_seq_ptrs.p, seqp, sizeof(void*) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(ctx->st_seq.ev, st));
+    auto fa = front_args(ctx, t);
+    fa.sym_first = t->pcc_max + 1;
+    if (t2->q.N_DF_symb > t->pcc_max) {
+        fa.sym_count = t2->q.N_DF_symb - t->pcc_max;
+        ctx->tic("rx_fft_pdc", st);
+        if (dev::launch_rx_fft(fa, n, st) != hipSuccess) return DNRP_EDEVICE;
+        ctx->toc("rx_fft_pdc", st);
+    }
+    auto ba = back_args(ctx, t);
+    ba.ops = t2->pdc_ops.as<dev::rx_op>();
+    ba.n_ops = t2->n_pdc_ops;
+    ba.drs_l = t2->drs_l.as<uint32_t>();
+    ba.drs_meta = t2->drs_meta.as<uint32_t>();
+    ba.pdc_k = t2->pdc_k.as<uint32_t>();
+    ba.pdc_off = t2->pdc_off.as<uint32_t>();
+    ba.N_bps = t2->q.N_bps;
+    ba.pdc_seq = static_cast<const uint8_t* const*>(ctx->pdc_seq_ptrs.p);
+    ba.llr = pdc_llr;
+    ba.llr_stride = llr_stride;
+    ba.is_pdc = 1;
+    ctx->tic("rx_pdc", st);
+    if (dev::launch_rx_back(ba, n, st) != hipSuccess) return DNRP_EDEVICE;
+    ctx->toc("rx_pdc", st);
+    if (rep) {
+        std::vector<dev::rx_pkt_state> S(n);
+        HIPCHK(hipMemcpyAsync(S.data(), ctx->rx_st.p, sizeof(dev::rx_pkt_state) * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (uint32_t i = 0; i < n; ++i) rep[i].snr_dB = S[i].snr_pdc;
+    }
+    return DNRP_OK;
+}
+
+int dnrp_sync(dnrp_ctx* ctx, void* stream) {
+    if (!ctx) return DNRP_EINVAL;
+    return hipStreamSynchronize(static_cast<hipStream_t>(stream)) == hipSuccess ? DNRP_OK : DNRP_EDEVICE;
+}
+
+int dnrp_last_kernel_ms(const dnrp_ctx* ctx, const char* name, float* ms) {
+    if (!ctx || !name || !ms) return DNRP_EINVAL;
+    auto it = ctx->ev.find(name);
+    if (it == ctx->ev.end()) return DNRP_EINVAL;
+    if (hipEventSynchronize(it->second.second) != hipSuccess) return DNRP_EDEVICE;
+    return hipEventElapsedTime(ms, it->second.first, it->second.second) == hipSuccess ? DNRP_OK : DNRP_EDEVICE;
+}
+
+}  // extern "C"

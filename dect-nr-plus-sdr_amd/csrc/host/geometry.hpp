@@ -1,0 +1,97 @@
+// Host-side DECT NR+ geometry for the GPU path: packet sizes, per-symbol cell-code maps, DRS/STF
+// tables, beamforming matrices, resampler taps, Gold sequences, Wiener channel-estimation LUTs and
+// the RX operation schedules. Everything here runs once per configuration at context init (the
+// reference builds the same objects in its constructors: tx_rx.cpp:38-129, rx_synced.cpp:55-174)
+// and is uploaded to HBM as flat tables shared by every packet of a batch.
+#pragma once
+
+#include <complex>
+#include <cstdint>
+#include <vector>
+
+#include "dnrp.h"
+
+namespace dnrp::geo {
+
+using cf32 = std::complex<float>;
+
+// cell codes, one u32 per (symbol l, transmit-stream index k in [0, N_b_OCC])
+enum : uint32_t {
+    CODE_NONE = 0u << 29,
+    CODE_PCC = 1u << 29,  // bits 0..28: PCC cell index (0..97)
+    CODE_PDC = 2u << 29,  // bits 0..28: PDC cell index
+    CODE_DRS = 3u << 29,  // bits 0..2: transmit stream, bit 3: value is -1
+    CODE_STF = 4u << 29,  // value from the STF table at k
+    CODE_MASK = 7u << 29,
+};
+
+struct tm_t {
+    uint32_t index, N_eff_TX, N_SS, N_TS, N_TX;
+    bool cl, txdiv;
+};
+
+bool packet_sizes(const dnrp_psdef& d, dnrp_packet_sizes& q, tm_t* tm = nullptr);
+
+// FFT size and hw-rate lengths for a context (tx.cpp:429-600)
+struct dims_t {
+    uint32_t Nd, N_occ, Nf, off_lower, CP, STF_CP, N_no_GI, N_no_GI_rs, N_packet_rs;
+    uint32_t n_pattern, pattern_len;
+};
+dims_t make_dims(const dnrp_cfg& cfg, const dnrp_psdef& d, const dnrp_packet_sizes& q);
+
+struct drs_sym_t {
+    uint32_t l, ts_first, ts_last, parity;
+};
+
+// per-configuration maps (geometry of one (b, N_TS, N_DF) packet)
+struct maps_t {
+    uint32_t b, N_TS, N_DF, Nf;
+    std::vector<uint32_t> code;        // [(N_DF+1) * Nf]
+    std::vector<uint32_t> pcc_l;       // symbols carrying PCC (ascending)
+    std::vector<uint32_t> pcc_k;       // [98] cell index k, in PCC order
+    std::vector<uint32_t> pcc_sym_off; // [pcc_l.size()+1] offsets into pcc_k
+    std::vector<uint32_t> pdc_k;       // all PDC cells in order
+    std::vector<uint32_t> pdc_sym_off; // [N_DF+2] offsets into pdc_k per symbol (l = 0..N_DF)
+    std::vector<drs_sym_t> drs;
+    std::vector<cf32> stf;             // [Nf]
+    std::vector<uint32_t> drs_k;       // [2 parity][4 ts][N_occ/4]
+    std::vector<float> drs_v;          // [8 ts][N_occ/4], +-1
+};
+maps_t build_maps(uint32_t b, uint32_t N_TS, uint32_t N_eff_TX, uint32_t N_DF);
+
+std::vector<cf32> W_matrix(uint32_t N_TS, uint32_t N_TX, uint32_t codebook, float* scaling);
+uint32_t W_codebooks(uint32_t N_TS, uint32_t N_TX);
+
+std::vector<uint8_t> gold_bits_packed(uint32_t c_init, uint32_t nbits);  // MSB-first bytes
+
+// polyphase resampler taps (resampler.cpp:56-160): h[(hl+1)*L], delay, history length
+struct resampler_t {
+    uint32_t L = 1, M = 1, delay = 0, hl = 0, taps = 1;
+    std::vector<float> h;
+};
+resampler_t make_resampler(uint32_t L, uint32_t M, uint32_t os_min);
+
+// Wiener LUT for one (N_step_virtual, b, SNR profile) — channel_lut.cpp:168-620
+struct lut_t {
+    uint32_t T = 0, n = 0, Nf = 0;
+    std::vector<uint32_t> pilot_weight;  // [T][4][Nf] packed: pilot index | weight index << 16
+    std::vector<float> weights;          // [n_vec][n]
+};
+lut_t build_lut(uint32_t N_step_virtual, uint32_t b, uint32_t b_max, uint32_t u_max, uint32_t profile);
+float lut_profile_snr_db(uint32_t profile);
+
+// RX schedules: a WG-uniform op list interpreted by the RX kernels (rx_synced.cpp:283-302,
+// 1028-1163 restated as data instead of control flow)
+enum : uint32_t {
+    OP_DRS = 1,    // a = symbol l, b = index in maps.drs, c = rel (stage-relative index), d = ps_idx
+    OP_EVENT = 2,  // a = mode (0: l / 1: lr), b = rel (LUT t index), c = ps_idx, d = ts_first
+    OP_PCC = 3,    // a = symbol l, b = index into pcc_l
+    OP_PDC = 4,    // a = symbol l
+};
+struct op_t {
+    uint32_t kind, a, b, c, d;
+};
+void build_rx_ops(const maps_t& m, uint32_t N_eff_TX, uint32_t N_DF, bool mode_lr, uint32_t stride,
+                  std::vector<op_t>& pcc_ops, std::vector<op_t>& pdc_ops, uint32_t& pcc_max_symbol);
+
+}  // namespace dnrp::geo

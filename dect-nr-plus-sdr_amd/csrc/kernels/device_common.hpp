@@ -1,0 +1,135 @@
+// Device helpers shared by the DECT NR+ kernels: complex arithmetic, LDS Stockham FFT
+// (radix 4/2/3, autosort, one workgroup per transform), block reductions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dnrp::dev {
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {  // a * conj(b)
+    return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float cnorm(float2 a) { return a.x * a.x + a.y * a.y; }
+
+// exp(j*phi) for a double phase: exact range reduction in double, accurate sincos in float
+__device__ __forceinline__ float2 phasor(double phi) {
+    const double twopi = 6.283185307179586476925286766559;
+    const double r = phi - twopi * rint(phi / twopi);
+    float s, c;
+    sincosf(static_cast<float>(r), &s, &c);
+    return make_float2(c, s);
+}
+
+// FFT plan passed by value: radix sequence (each 2, 3 or 4), product = N
+struct fft_plan {
+    uint32_t N;
+    uint32_t nr;
+    uint32_t radix[16];
+};
+
+// R-point DFT in registers, SIGN = -1 forward, +1 inverse (unnormalised)
+template <int SIGN>
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3), t3 = csub(a1, a3);
+    // t3 * (SIGN * j)
+    const float2 t3j = SIGN < 0 ? make_float2(t3.y, -t3.x) : make_float2(-t3.y, t3.x);
+    a0 = cadd(t0, t2);
+    a2 = csub(t0, t2);
+    a1 = cadd(t1, t3j);
+    a3 = csub(t1, t3j);
+}
+
+// Stockham autosort passes on LDS ping-pong buffers; tw[j] = exp(-2*pi*i*j/N) (forward table).
+// Returns the buffer holding the result. Whole workgroup participates; ends with a barrier.
+template <int SIGN>
+__device__ float2* fft_lds(float2* x, float2* y, const float2* __restrict__ tw, const fft_plan& p) {
+    const uint32_t N = p.N;
+    uint32_t Ns = 1;
+    for (uint32_t s = 0; s < p.nr; ++s) {
+        const uint32_t R = p.radix[s];
+        const uint32_t NR = N / R;
+        const uint32_t tstep = N / (Ns * R);
+        for (uint32_t j = threadIdx.x; j < NR; j += blockDim.x) {
+            const uint32_t k = j % Ns;
+            const uint32_t od = (j / Ns) * Ns * R + k;
+            if (R == 4) {
+                float2 a0 = x[j], a1 = x[j + NR], a2 = x[j + 2 * NR], a3 = x[j + 3 * NR];
+                if (Ns > 1) {
+                    const uint32_t e = k * tstep;
+                    float2 w1 = tw[e % N], w2 = tw[(2 * e) % N], w3 = tw[(3 * e) % N];
+                    if (SIGN > 0) {
+                        w1 = cconj(w1);
+                        w2 = cconj(w2);
+                        w3 = cconj(w3);
+                    }
+                    a1 = cmul(a1, w1);
+                    a2 = cmul(a2, w2);
+                    a3 = cmul(a3, w3);
+                }
+                dft4<SIGN>(a0, a1, a2, a3);
+                y[od] = a0;
+                y[od + Ns] = a1;
+                y[od + 2 * Ns] = a2;
+                y[od + 3 * Ns] = a3;
+            } else if (R == 2) {
+                float2 a0 = x[j], a1 = x[j + NR];
+                if (Ns > 1) {
+                    float2 w1 = tw[(k * tstep) % N];
+                    if (SIGN > 0) w1 = cconj(w1);
+                    a1 = cmul(a1, w1);
+                }
+                y[od] = cadd(a0, a1);
+                y[od + Ns] = csub(a0, a1);
+            } else {  // R == 3
+                float2 a0 = x[j], a1 = x[j + NR], a2 = x[j + 2 * NR];
+                if (Ns > 1) {
+                    const uint32_t e = k * tstep;
+                    float2 w1 = tw[e % N], w2 = tw[(2 * e) % N];
+                    if (SIGN > 0) {
+                        w1 = cconj(w1);
+                        w2 = cconj(w2);
+                    }
+                    a1 = cmul(a1, w1);
+                    a2 = cmul(a2, w2);
+                }
+                // W3 = exp(SIGN * 2 pi i / 3)
+                const float c3 = -0.5f, s3 = SIGN * 0.86602540378443864676f;
+                const float2 s = cadd(a1, a2), d = csub(a1, a2);
+                const float2 m = make_float2(a0.x + c3 * s.x, a0.y + c3 * s.y);
+                const float2 jd = make_float2(-s3 * d.y, s3 * d.x);  // s3 * j * d
+                y[od] = cadd(a0, s);
+                y[od + Ns] = cadd(m, jd);
+                y[od + 2 * Ns] = csub(m, jd);
+            }
+        }
+        __syncthreads();
+        float2* t = x;
+        x = y;
+        y = t;
+        Ns *= R;
+    }
+    return x;
+}
+
+// block-wide sum of a double, result valid in all threads (blockDim.x multiple of 64, <= 1024)
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const uint32_t w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (uint32_t i = 0; i < nw; ++i) s += red[i];
+    __syncthreads();
+    return s;
+}
+
+}  // namespace dnrp::dev

@@ -1,0 +1,113 @@
+// Kernel argument blocks and launchers shared by the host context (host/ctx.cpp) and the HIP
+// kernels (kernels/*.hip). Plain structs, passed by value as kernel arguments.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_common.hpp"
+
+namespace dnrp::dev {
+
+enum : uint32_t {
+    CODE_PCC = 1u << 29,
+    CODE_PDC = 2u << 29,
+    CODE_DRS = 3u << 29,
+    CODE_STF = 4u << 29,
+    CODE_MASK = 7u << 29,
+};
+
+// ---------------------------------------------------------------- TX
+struct tx_pkt {
+    const uint8_t* pdc_seq;  // packed Gold sequence for (network_id, plcf_type)
+    uint32_t codebook, do_mix;
+    float scale_stf, scale_df;
+    double ph0, inc;  // effective mixer phase and per-sample increment (float phasor emulated)
+};
+
+struct tx_args {
+    fft_plan plan;  // IFFT size N_b_DFT_os
+    uint32_t N_occ, off_lower, CP, STF_CP, N_DF, N_TS, N_TX, N_SS, N_bps, txdiv, mod, pattern_len;
+    uint32_t L, M, delay, hl, n_keep, S, pdc_stride, G, xbuf_len;
+    uint32_t pair[12];  // transmit diversity TS pairs, A | B << 4
+    const uint32_t* code;
+    const float2* stf;
+    const float2* W;     // [codebooks][N_TX][N_TS]
+    const float* taps;   // [(hl+1)*L]
+    const float2* tw;    // forward twiddles exp(-2 pi i j / N)
+    const float2* qam;   // constellation for N_bps
+    const float2* qpsk;  // QPSK table for the PCC
+    const uint8_t* pcc_seq;
+    const uint8_t* pcc_d;
+    const uint8_t* pdc_d;
+    float* out;
+    const tx_pkt* pk;
+};
+hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st);
+
+// ---------------------------------------------------------------- RX
+struct rx_pkt_in {          // from sync_report_t
+    int64_t fine_peak;
+    double inc0;            // effective CFO phasor increment (float phasor emulated)
+    float cfo_rad;          // sync CFO (fractional + integer)
+};
+
+struct rx_pkt_state {       // written by rx_stf_kernel, read by the later RX kernels
+    double inc1;            // mixer increment after the STF fine CFO adjustment
+    double sto_inc;         // STO phase increment per subcarrier
+    double snr_SN, snr_N;   // SNR accumulators after the STF
+    uint32_t snr_SN_cnt, snr_N_cnt;
+    float cfo_fine, sto_frac;
+    float rms[8];
+    float snr_pcc, snr_pdc;
+};
+
+struct rx_front_args {
+    fft_plan plan;
+    uint32_t N_occ, off_lower, CP, STF_CP, N_RX, S_in, n_pattern, pattern_len, b;
+    uint32_t L, M, delay, hl;  // RX resampler (L and M already swapped)
+    uint32_t sym_first, sym_count, sym_per_block, Nf_pad, n_sym_total;
+    float amp_scale;           // sqrt(N_b_OCC) / N_b_DFT_os
+    const float* taps;
+    const float2* tw;
+    const float2* stf;         // STF values for (b, N_eff_TX)
+    const float2* iq;          // [n][N_RX][S_in]
+    const rx_pkt_in* pin;
+    rx_pkt_state* st;
+    float2* Y;                 // [n][N_RX][n_sym_total][Nf_pad]
+};
+hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);
+hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st);
+
+struct rx_op {
+    uint32_t kind, a, b, c, d;
+};
+
+struct rx_back_args {
+    uint32_t N_occ, N_RX, N_eff_TX, Nf_pad, n_sym_total, n_drs, N_bps, mod, n_ops, txdiv;
+    uint32_t pair[12];
+    const rx_op* ops;
+    const uint32_t* drs_l;      // per DRS index: symbol
+    const uint32_t* drs_meta;   // per DRS index: ts_first | ts_last << 8 | parity << 16
+    const uint32_t* drs_k;      // [2][4][n_drs]
+    const float* drs_v;         // [8][n_drs]
+    const uint32_t* pcc_k;
+    const uint32_t* pcc_off;
+    const uint32_t* pdc_k;
+    const uint32_t* pdc_off;
+    const uint32_t* lut_pw[2][3];  // [mode l / lr][profile]: [T][4][Nf] pilot | weight << 16
+    const float* lut_w[2][3];
+    uint32_t lut_n[2][3];
+    uint32_t lut_T[2];
+    float prof_snr[3];
+    const float2* Y;
+    rx_pkt_state* st;
+    const uint8_t* pcc_seq;
+    const uint8_t* const* pdc_seq;  // per packet (PDC phase)
+    int16_t* llr;                   // PCC: [n][196], PDC: [n][llr_stride]
+    uint32_t llr_stride;
+    uint32_t is_pdc;
+};
+hipError_t launch_rx_back(const rx_back_args& a, uint32_t n, hipStream_t st);
+
+}  // namespace dnrp::dev

@@ -1,0 +1,181 @@
+"""Python host binding of libdnrp.so (include/dnrp.h) — the MI355X DECT NR+ lower PHY.
+
+Mirrors the reference's per-worker PHY objects with batched calls:
+  Phy.tx_batch      <- tx_t::generate_tx_packet      (lib/src/phy/tx/tx.cpp:165-314)
+  Phy.rx_pcc_batch  <- rx_synced_t::demoddecod_rx_pcc (rx_synced.cpp:186-323)
+  Phy.rx_pdc_batch  <- rx_synced_t::demoddecod_rx_pdc (rx_synced.cpp:325-436)
+  Phy.add_network_id <- tx_rx_t::add_new_network_id (tx_rx.hpp:52)
+Device buffers are torch tensors on the context's device (torch is plumbing only: allocation
+and streams). Errors raise DnrpError carrying the C error code; the library must be present —
+there is no fallback path.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libdnrp.so")
+
+
+class DnrpError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"{what}: {code} ({strerror(code)})")
+        self.code = code
+
+
+class Cfg(C.Structure):
+    _fields_ = [("u_max", C.c_uint32), ("b_max", C.c_uint32), ("N_TX_max", C.c_uint32), ("os_min", C.c_uint32),
+                ("L", C.c_uint32), ("M", C.c_uint32), ("chestim_mode_lr", C.c_uint32),
+                ("chestim_lr_stride", C.c_uint32), ("max_batch", C.c_uint32), ("device", C.c_int32)]
+
+
+class PsDef(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("u", "b", "PacketLengthType", "PacketLength", "tm_mode_index",
+                                         "mcs_index", "Z")]
+
+
+PS_FIELDS = ["N_PACKET_symb", "N_DF_symb", "N_PDC_subc", "N_DRS_subc", "G", "N_PDC_bits", "N_TB_bits", "N_TB_byte",
+             "C", "N_samples_STF", "N_samples_STF_CP_only", "N_samples_DF", "N_samples_GI",
+             "N_samples_packet_no_GI", "N_samples_packet", "N_bps", "N_eff_TX", "N_SS", "N_TS", "N_TX", "N_b_DFT",
+             "N_b_OCC", "N_b_DFT_os", "N_samples_packet_no_GI_os_rs", "N_samples_packet_os_rs"]
+
+
+class PacketSizes(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in PS_FIELDS]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n in PS_FIELDS}
+
+
+class TxDesc(C.Structure):
+    _fields_ = [("codebook_index", C.c_uint32), ("network_id", C.c_uint32), ("plcf_type", C.c_uint32),
+                ("GI_percentage", C.c_uint32), ("DAC_scale", C.c_float), ("iq_phase_rad", C.c_float),
+                ("iq_phase_increment_s2s_post_resampling_rad", C.c_float), ("optimal_scaling_DAC", C.c_uint32)]
+
+
+class SyncReport(C.Structure):
+    _fields_ = [("fine_peak_time", C.c_int64), ("cfo_fractional_rad", C.c_float), ("cfo_integer_rad", C.c_float),
+                ("u", C.c_uint32), ("b", C.c_uint32), ("N_eff_TX", C.c_uint32)]
+
+
+class PccReport(C.Structure):
+    _fields_ = [("snr_dB", C.c_float), ("cfo_fractional_rad", C.c_float), ("sto_fractional", C.c_float),
+                ("rms", C.c_float * 8)]
+
+
+class PdcReport(C.Structure):
+    _fields_ = [("snr_dB", C.c_float)]
+
+
+class PdcReq(C.Structure):
+    _fields_ = [("network_id", C.c_uint32), ("plcf_type", C.c_uint32)]
+
+
+EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_get_packet_sizes", "dnrp_tx_batch",
+           "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_strerror"]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libdnrp.so not built at {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.dnrp_ctx_create.argtypes = [C.POINTER(Cfg), C.POINTER(P)]
+        L.dnrp_ctx_destroy.argtypes = [P]
+        L.dnrp_add_network_id.argtypes = [P, C.c_uint32]
+        L.dnrp_get_packet_sizes.argtypes = [P, C.POINTER(PsDef), C.POINTER(PacketSizes)]
+        L.dnrp_tx_batch.argtypes = [P, C.POINTER(PsDef), C.c_uint32, C.POINTER(TxDesc), P, P, C.c_uint32, P,
+                                    C.c_uint32, P]
+        L.dnrp_rx_pcc_batch.argtypes = [P, C.c_uint32, C.POINTER(SyncReport), P, C.c_uint32, P,
+                                        C.POINTER(PccReport), P]
+        L.dnrp_rx_pdc_batch.argtypes = [P, C.POINTER(PsDef), C.c_uint32, C.POINTER(PdcReq), P, C.c_uint32,
+                                        C.POINTER(PdcReport), P]
+        L.dnrp_sync.argtypes = [P, P]
+        L.dnrp_last_kernel_ms.argtypes = [P, C.c_char_p, C.POINTER(C.c_float)]
+        L.dnrp_strerror.argtypes = [C.c_int]
+        L.dnrp_strerror.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def strerror(code):
+    return lib().dnrp_strerror(int(code)).decode()
+
+
+def _chk(rc, what):
+    if rc != 0:
+        raise DnrpError(rc, what)
+
+
+def psdef(u, b, plt, pl, tm, mcs, Z=6144):
+    return PsDef(u, b, plt, pl, tm, mcs, Z)
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    return C.c_void_p(int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream))
+
+
+class Phy:
+    """One context = one submitting thread (like one worker_tx_rx_t)."""
+
+    def __init__(self, u_max, b_max, N_TX_max, os_min=1, L=10, M=9, chestim_mode_lr=True, stride=2, max_batch=64,
+                 device=0):
+        self.cfg = Cfg(u_max, b_max, N_TX_max, os_min, L, M, int(chestim_mode_lr), stride, max_batch, device)
+        self._ctx = C.c_void_p()
+        _chk(lib().dnrp_ctx_create(C.byref(self.cfg), C.byref(self._ctx)), "dnrp_ctx_create")
+
+    def close(self):
+        if self._ctx:
+            lib().dnrp_ctx_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_network_id(self, nid):
+        _chk(lib().dnrp_add_network_id(self._ctx, nid), "dnrp_add_network_id")
+
+    def packet_sizes(self, ps):
+        out = PacketSizes()
+        _chk(lib().dnrp_get_packet_sizes(self._ctx, C.byref(ps), C.byref(out)), "dnrp_get_packet_sizes")
+        return out.as_dict()
+
+    def tx_batch(self, ps, descs, pcc_d, pdc_d, iq_out, stream=None):
+        """pcc_d uint8 [n,25], pdc_d uint8 [n,stride], iq_out float32 [n,N_TX,S,2] (torch, device)."""
+        n = len(descs)
+        arr = (TxDesc * n)(*descs)
+        _chk(lib().dnrp_tx_batch(self._ctx, C.byref(ps), n, arr, C.c_void_p(pcc_d.data_ptr()),
+                                 C.c_void_p(pdc_d.data_ptr()), pdc_d.shape[1], C.c_void_p(iq_out.data_ptr()),
+                                 iq_out.shape[2], _stream_ptr(stream)), "dnrp_tx_batch")
+
+    def rx_pcc_batch(self, reports, iq_in, pcc_llr, want_report=False, stream=None):
+        n = len(reports)
+        arr = (SyncReport * n)(*reports)
+        rep = (PccReport * n)() if want_report else None
+        _chk(lib().dnrp_rx_pcc_batch(self._ctx, n, arr, C.c_void_p(iq_in.data_ptr()), iq_in.shape[2],
+                                     C.c_void_p(pcc_llr.data_ptr()), rep, _stream_ptr(stream)), "dnrp_rx_pcc_batch")
+        return rep
+
+    def rx_pdc_batch(self, ps, reqs, pdc_llr, want_report=False, stream=None):
+        n = len(reqs)
+        arr = (PdcReq * n)(*reqs)
+        rep = (PdcReport * n)() if want_report else None
+        _chk(lib().dnrp_rx_pdc_batch(self._ctx, C.byref(ps), n, arr, C.c_void_p(pdc_llr.data_ptr()),
+                                     pdc_llr.shape[1], rep, _stream_ptr(stream)), "dnrp_rx_pdc_batch")
+        return rep
+
+    def sync(self, stream=None):
+        _chk(lib().dnrp_sync(self._ctx, _stream_ptr(stream)), "dnrp_sync")
+
+    def last_kernel_ms(self, name):
+        ms = C.c_float()
+        _chk(lib().dnrp_last_kernel_ms(self._ctx, name.encode(), C.byref(ms)), "dnrp_last_kernel_ms")
+        return float(ms.value)

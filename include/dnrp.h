@@ -1,0 +1,169 @@
+/*
+ * dnrp.h — C-ABI of the MI355X-native DECT NR+ lower PHY (libdnrp.so).
+ *
+ * Drop-in boundary for the OFDM TX/RX hot path of maxpenner/DECT-NR-Plus-SDR. The reference has
+ * no FFI; its path is three C++ classes owned per worker thread. Each entry point below replaces
+ * one of them, batched over many independent packets (slots):
+ *
+ *   dnrp_ctx_create        <- tx_rx_t / tx_t / rx_synced_t constructors
+ *                             (lib/src/phy/tx_rx.cpp:38-129, tx/tx.cpp:48-141,
+ *                              rx/rx_synced/rx_synced.cpp:55-174)
+ *   dnrp_add_network_id    <- tx_rx_t::add_new_network_id (lib/include/dectnrp/phy/tx_rx.hpp:52,
+ *                             sections_part3/scrambling_pdc.cpp:36-57)
+ *   dnrp_get_packet_sizes  <- sp3::get_packet_sizes (sections_part3/derivative/packet_sizes.cpp:99)
+ *   dnrp_tx_batch          <- tx_t::generate_tx_packet (lib/include/dectnrp/phy/tx/tx.hpp:80-81,
+ *                             lib/src/phy/tx/tx.cpp:165-314), FEC boundary between rate matching
+ *                             and scrambling (pcc_enc.cpp:212, pdc_enc.cpp:218-221)
+ *   dnrp_rx_pcc_batch      <- rx_synced_t::demoddecod_rx_pcc up to the descrambled PCC d-bits
+ *                             (lib/include/dectnrp/phy/rx/rx_synced/rx_synced.hpp:93,
+ *                              rx_synced.cpp:186-302, pcc_enc.cpp:297)
+ *   dnrp_rx_pdc_batch      <- rx_synced_t::demoddecod_rx_pdc up to the descrambled PDC d-bits
+ *                             (rx_synced.hpp:103, rx_synced.cpp:325-436, pdc_enc.cpp:339-344)
+ *   dnrp_ctx_destroy       <- destructors
+ *
+ * Conventions (all functions):
+ *   - return 0 on success, a negative DNRP_E* code on argument/configuration error; never abort.
+ *   - bulk buffers (bits, IQ, LLRs) are DEVICE pointers on the context's HIP device; descriptor
+ *     and report arrays are HOST pointers. IQ is interleaved cf32, one contiguous stream per
+ *     antenna (radio/complex.hpp:28, buffer_tx.hpp, buffer_rx.hpp).
+ *   - work is stream-ordered on the caller's hipStream_t (passed as void*, NULL = default
+ *     stream); host report arrays are valid after dnrp_sync() or a stream synchronisation.
+ *   - one context per submitting host thread; contexts are not thread-safe (like the reference's
+ *     per-worker tx_t/rx_synced_t objects).
+ *   - LLRs are int16, positive means bit 1 (phy_config.hpp:39-41, fec/test/tb2pdc.cpp:173-176).
+ */
+#ifndef DNRP_H
+#define DNRP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DNRP_OK 0
+#define DNRP_EINVAL (-1)      /* bad argument / null pointer */
+#define DNRP_ECONFIG (-2)     /* packet configuration not valid (get_packet_sizes -> nullopt) */
+#define DNRP_EUNSUPPORTED (-3)/* valid DECT NR+ configuration the reference RX cannot demodulate */
+#define DNRP_ENOMEM (-4)      /* device allocation failed / batch larger than max_batch */
+#define DNRP_EDEVICE (-5)     /* HIP runtime error */
+#define DNRP_ENETID (-6)      /* network ID not registered with dnrp_add_network_id */
+#define DNRP_ESTATE (-7)      /* dnrp_rx_pdc_batch without a preceding dnrp_rx_pcc_batch */
+
+typedef struct dnrp_ctx dnrp_ctx;
+
+/* worker_pool_config_t subset (phy/worker_pool_config.hpp) */
+typedef struct {
+    uint32_t u_max, b_max;      /* radio device class maxima (sections_part3/radio_device_class.cpp) */
+    uint32_t N_TX_max;          /* physical antennas; RX uses N_RX = N_TX_max (rx_synced.hpp:120-126) */
+    uint32_t os_min;            /* minimum oversampling (phy.json os_min) */
+    uint32_t L, M;              /* hw/DECT resampling ratio L/M for TX, M/L for RX (phy_config.cpp:28-94) */
+    uint32_t chestim_mode_lr;   /* phy.json chestim_mode_lr_default */
+    uint32_t chestim_lr_stride; /* phy.json chestim_mode_lr_t_stride_default */
+    uint32_t max_batch;         /* packets per batch call */
+    int32_t device;             /* HIP device ordinal */
+} dnrp_cfg;
+
+/* sp3::packet_sizes_def_t */
+typedef struct {
+    uint32_t u, b, PacketLengthType, PacketLength, tm_mode_index, mcs_index, Z;
+} dnrp_psdef;
+
+/* sp3::packet_sizes_t + context-dependent hw-rate sizes */
+typedef struct {
+    uint32_t N_PACKET_symb, N_DF_symb, N_PDC_subc, N_DRS_subc, G, N_PDC_bits, N_TB_bits, N_TB_byte, C;
+    uint32_t N_samples_STF, N_samples_STF_CP_only, N_samples_DF, N_samples_GI;
+    uint32_t N_samples_packet_no_GI, N_samples_packet;
+    uint32_t N_bps, N_eff_TX, N_SS, N_TS, N_TX, N_b_DFT, N_b_OCC;
+    uint32_t N_b_DFT_os;                  /* FFT size used (tx.cpp:439) */
+    uint32_t N_samples_packet_no_GI_os_rs;/* hw samples carrying the packet (tx.cpp:527-529) */
+    uint32_t N_samples_packet_os_rs;      /* hw samples of the slot window incl. full GI */
+} dnrp_packet_sizes;
+
+/* tx_descriptor_t + tx_meta_t subset (phy/tx/tx_descriptor.hpp, phy/tx/tx_meta.hpp) */
+typedef struct {
+    uint32_t codebook_index;
+    uint32_t network_id;      /* must have been registered */
+    uint32_t plcf_type;       /* 1 or 2: selects the PDC scrambling sequence */
+    uint32_t GI_percentage;   /* share of the GI actually transmitted (zeros) */
+    float DAC_scale;
+    float iq_phase_rad;
+    float iq_phase_increment_s2s_post_resampling_rad;
+    uint32_t optimal_scaling_DAC; /* 0: standard W scaling (tx.cpp:582-592) */
+} dnrp_tx_desc;
+
+/* sync_report_t fields consumed by rx_synced_t (phy/rx/sync/sync_report.hpp) */
+typedef struct {
+    int64_t fine_peak_time;   /* hw-rate sample index of the packet start inside this packet's window */
+    float cfo_fractional_rad; /* per DECT-rate sample */
+    float cfo_integer_rad;
+    uint32_t u, b, N_eff_TX;
+} dnrp_sync_report;
+
+/* PHY part of pcc_report_t plus the sync_report_t values rx_synced_t refines (rx_synced.cpp:530-580) */
+typedef struct {
+    float snr_dB;             /* estimator_snr after STF + DRS of the PCC symbols */
+    float cfo_fractional_rad; /* sync value + STF re-estimate */
+    float sto_fractional;     /* samples, estimator_sto on the STF */
+    float rms[8];             /* per RX antenna, over the STF */
+} dnrp_pcc_report;
+
+/* PHY part of pdc_report_t (rx_synced.cpp:432-435) */
+typedef struct {
+    float snr_dB;
+} dnrp_pdc_report;
+
+/* per-packet PDC request = what maclow_phy_t / the HARQ process provide (interfaces/maclow_phy.hpp) */
+typedef struct {
+    uint32_t network_id;
+    uint32_t plcf_type;
+} dnrp_pdc_req;
+
+int dnrp_ctx_create(const dnrp_cfg* cfg, dnrp_ctx** out);
+int dnrp_ctx_destroy(dnrp_ctx* ctx);
+int dnrp_add_network_id(dnrp_ctx* ctx, uint32_t network_id);
+int dnrp_get_packet_sizes(const dnrp_ctx* ctx, const dnrp_psdef* psdef, dnrp_packet_sizes* out);
+
+/*
+ * TX: n packets of one configuration.
+ *   pcc_d   device [n][25] bytes: 196 rate-matched PCC bits, unscrambled, MSB first
+ *   pdc_d   device [n][pdc_stride] bytes: G rate-matched PDC bits, unscrambled, MSB first
+ *   iq_out  device [n][N_TX][S] cf32; samples [0, N_samples_packet_no_GI_os_rs) carry the packet,
+ *           the rest (GI and slot tail) are written as zeros. S >= N_samples_packet_os_rs.
+ */
+int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp_tx_desc* desc,
+                  const uint8_t* pcc_d, const uint8_t* pdc_d, uint32_t pdc_stride, float* iq_out,
+                  uint32_t S, void* stream);
+
+/*
+ * RX phase 1: synchronised PCC demodulation of n packets (same u, b, N_eff_TX).
+ *   iq_in    device [n][N_RX][S_in] cf32 slot windows, N_RX = cfg.N_TX_max
+ *   pcc_llr  device [n][196] int16, descrambled
+ *   rep      host [n] (optional)
+ * Device state for phase 2 is kept in the context until the next dnrp_rx_pcc_batch.
+ */
+int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, const float* iq_in,
+                      uint32_t S_in, int16_t* pcc_llr, dnrp_pcc_report* rep, void* stream);
+
+/*
+ * RX phase 2: PDC demodulation of the packets of the preceding dnrp_rx_pcc_batch (the MAC has
+ * decided from the decoded PLCF; psdef is the packet configuration the PLCF announced).
+ *   req      host [n] network ID / PLCF type per packet
+ *   pdc_llr  device [n][llr_stride] int16, G descrambled LLRs per packet
+ *   rep      host [n] (optional)
+ */
+int dnrp_rx_pdc_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp_pdc_req* req,
+                      int16_t* pdc_llr, uint32_t llr_stride, dnrp_pdc_report* rep, void* stream);
+
+int dnrp_sync(dnrp_ctx* ctx, void* stream);
+
+/* last kernel-level timing of the previous call (device ms via HIP events; diagnostics/bench) */
+int dnrp_last_kernel_ms(const dnrp_ctx* ctx, const char* name, float* ms);
+
+const char* dnrp_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DNRP_H */
