@@ -216,27 +216,36 @@ struct dnrp_ctx {
     uint32_t rx_n = 0, rx_S_in = 0, rx_nsym_cap = 0, rx_Nf_pad = 0;
     const float* rx_iq = nullptr;
     std::vector<dev::rx_pkt_in> rx_pin_host;
-    // timing
+    // timing: HIP events recorded on the caller's stream around every launch (DNRP_TIMING=1)
     bool timing = false;
-    std::map<std::string, std::pair<hipEvent_t, hipEvent_t>> ev;
+    struct ev_pool {
+        std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+        size_t used = 0;
+    };
+    std::map<std::string, ev_pool> ev;
     ~dnrp_ctx() {
-        for (auto& e : ev) {
-            (void)hipEventDestroy(e.second.first);
-            (void)hipEventDestroy(e.second.second);
-        }
+        for (auto& e : ev)
+            for (auto& p : e.second.ev) {
+                (void)hipEventDestroy(p.first);
+                (void)hipEventDestroy(p.second);
+            }
     }
     void tic(const char* name, hipStream_t s) {
         if (!timing) return;
-        auto& e = ev[name];
-        if (!e.first) {
-            (void)hipEventCreate(&e.first);
-            (void)hipEventCreate(&e.second);
+        auto& pool = ev[name];
+        if (pool.used == pool.ev.size()) {
+            std::pair<hipEvent_t, hipEvent_t> p{};
+            (void)hipEventCreate(&p.first);
+            (void)hipEventCreate(&p.second);
+            pool.ev.push_back(p);
         }
-        (void)hipEventRecord(e.first, s);
+        (void)hipEventRecord(pool.ev[pool.used].first, s);
     }
     void toc(const char* name, hipStream_t s) {
         if (!timing) return;
-        (void)hipEventRecord(ev[name].second, s);
+        auto& pool = ev[name];
+        (void)hipEventRecord(pool.ev[pool.used].second, s);
+        ++pool.used;
     }
 };
 
@@ -729,9 +738,28 @@ int dnrp_sync(dnrp_ctx* ctx, void* stream) {
 int dnrp_last_kernel_ms(const dnrp_ctx* ctx, const char* name, float* ms) {
     if (!ctx || !name || !ms) return DNRP_EINVAL;
     auto it = ctx->ev.find(name);
-    if (it == ctx->ev.end()) return DNRP_EINVAL;
-    if (hipEventSynchronize(it->second.second) != hipSuccess) return DNRP_EDEVICE;
-    return hipEventElapsedTime(ms, it->second.first, it->second.second) == hipSuccess ? DNRP_OK : DNRP_EDEVICE;
+    if (it == ctx->ev.end() || it->second.used == 0) return DNRP_EINVAL;
+    const auto& p = it->second.ev[it->second.used - 1];
+    if (hipEventSynchronize(p.second) != hipSuccess) return DNRP_EDEVICE;
+    return hipEventElapsedTime(ms, p.first, p.second) == hipSuccess ? DNRP_OK : DNRP_EDEVICE;
+}
+
+int dnrp_kernel_time_total(dnrp_ctx* ctx, const char* name, float* total_ms, uint32_t* count, int reset) {
+    if (!ctx || !name || !total_ms || !count) return DNRP_EINVAL;
+    *total_ms = 0.0f;
+    *count = 0;
+    auto it = ctx->ev.find(name);
+    if (it == ctx->ev.end()) return DNRP_OK;
+    auto& pool = it->second;
+    for (size_t i = 0; i < pool.used; ++i) {
+        float ms = 0.0f;
+        if (hipEventSynchronize(pool.ev[i].second) != hipSuccess) return DNRP_EDEVICE;
+        if (hipEventElapsedTime(&ms, pool.ev[i].first, pool.ev[i].second) != hipSuccess) return DNRP_EDEVICE;
+        *total_ms += ms;
+    }
+    *count = static_cast<uint32_t>(pool.used);
+    if (reset) pool.used = 0;
+    return DNRP_OK;
 }
 
 }  // extern "C"

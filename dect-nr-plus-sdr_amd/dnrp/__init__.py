@@ -12,6 +12,11 @@ there is no fallback path.
 import ctypes as C
 import os
 
+# torch ships its own HIP runtime (torch/lib/libamdhip64.so, SONAME libamdhip64.so.7). Loading it
+# first lets libdnrp.so bind to the same runtime instead of a second copy from /opt/rocm, so
+# device pointers and streams from torch tensors are valid inside the library.
+import torch  # noqa: F401
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "libdnrp.so")
 
@@ -71,7 +76,7 @@ class PdcReq(C.Structure):
 
 
 EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_get_packet_sizes", "dnrp_tx_batch",
-           "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_strerror"]
+           "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_kernel_time_total", "dnrp_strerror"]
 
 _lib = None
 
@@ -95,6 +100,7 @@ def lib():
                                         C.POINTER(PdcReport), P]
         L.dnrp_sync.argtypes = [P, P]
         L.dnrp_last_kernel_ms.argtypes = [P, C.c_char_p, C.POINTER(C.c_float)]
+        L.dnrp_kernel_time_total.argtypes = [P, C.c_char_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.c_int]
         L.dnrp_strerror.argtypes = [C.c_int]
         L.dnrp_strerror.restype = C.c_char_p
         _lib = L
@@ -174,6 +180,12 @@ class Phy:
 
     def sync(self, stream=None):
         _chk(lib().dnrp_sync(self._ctx, _stream_ptr(stream)), "dnrp_sync")
+
+    def kernel_time_total(self, name, reset=True):
+        ms, cnt = C.c_float(), C.c_uint32()
+        _chk(lib().dnrp_kernel_time_total(self._ctx, name.encode(), C.byref(ms), C.byref(cnt), int(reset)),
+             "dnrp_kernel_time_total")
+        return float(ms.value), int(cnt.value)
 
     def last_kernel_ms(self, name):
         ms = C.c_float()

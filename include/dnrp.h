@@ -157,8 +157,11 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const 
 
 int dnrp_sync(dnrp_ctx* ctx, void* stream);
 
-/* last kernel-level timing of the previous call (device ms via HIP events; diagnostics/bench) */
+/* Kernel timing (only when the environment has DNRP_TIMING=1 at dnrp_ctx_create): HIP events
+ * recorded on the caller's stream around each launch. Names: "tx", "rx_stf", "rx_fft_pcc",
+ * "rx_pcc", "rx_fft_pdc", "rx_pdc". */
 int dnrp_last_kernel_ms(const dnrp_ctx* ctx, const char* name, float* ms);
+int dnrp_kernel_time_total(dnrp_ctx* ctx, const char* name, float* total_ms, uint32_t* count, int reset);
 
 const char* dnrp_strerror(int code);
 

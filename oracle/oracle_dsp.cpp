@@ -7,7 +7,10 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <tuple>
+#include <mutex>
 #include <stdexcept>
+#include <type_traits>
 
 #include "oracle.hpp"
 #include "oracle_dsp.hpp"
@@ -125,6 +128,32 @@ static bool is_txdiv(uint32_t tm_index) { return tm_index == 1 || tm_index == 5 
 uint32_t pdc_c_init(uint32_t network_id, uint32_t plcf_type) {  // scrambling_pdc.cpp:41-48
     return plcf_type == 1 ? (network_id & 0xFFu) : (network_id >> 8);
 }
+
+// Mixer phasor for output sample m. double: exact phase. float (CPU baseline): VOLK-style
+// recursive rotator with periodic renormalisation (volk_32fc_s32fc_x2_rotator2_32fc).
+template <typename R>
+struct rotator_t {
+    double ph0, inc;
+    std::complex<float> cur, step;
+    uint64_t next = 0;
+    rotator_t(double p, double i) : ph0(p), inc(i), cur(std::cos(p), std::sin(p)), step(std::cos(i), std::sin(i)) {}
+    std::complex<R> at(uint64_t m) {
+        if constexpr (std::is_same_v<R, double>) {
+            const double phi = ph0 + static_cast<double>(m) * inc;
+            return {std::cos(phi), std::sin(phi)};
+        } else {
+            if (m != next) {  // random access: restart from the exact phase
+                const double phi = ph0 + static_cast<double>(m) * inc;
+                cur = {static_cast<float>(std::cos(phi)), static_cast<float>(std::sin(phi))};
+            }
+            const std::complex<float> r = cur;
+            cur *= step;
+            if ((m & 511u) == 511u) cur /= std::abs(cur);
+            next = m + 1;
+            return r;
+        }
+    }
+};
 
 // ================================================================= TX
 template <typename R>
@@ -248,24 +277,22 @@ void tx_packet(const cfg_t& cfg, const packet_sizes_t& ps, const tx_desc_t& d, c
     out.assign(tm.N_TX, std::vector<C>(S_slot, C(0, 0)));
     const uint32_t n_keep = std::min(dm.N_no_GI_os_rs, S_slot);
     const int64_t Nx = static_cast<int64_t>(x[0].size());
+    const bool mix = (ph0 != 0.0 || inc != 0.0);
     for (uint32_t a = 0; a < tm.N_TX; ++a) {
+        rotator_t<R> rot(ph0, inc);
         for (uint32_t m = 0; m < n_keep; ++m) {
-            std::complex<double> acc{0, 0};
+            C acc{0, 0};
             if (cfg.L == 1 && cfg.M == 1) {
-                acc = std::complex<double>(x[a][m].real(), x[a][m].imag());
+                acc = x[a][m];
             } else {
                 const uint64_t t = rs.delay + static_cast<uint64_t>(m) * rs.M;
                 const int64_t p = static_cast<int64_t>(t / rs.L);
                 const uint32_t ph = static_cast<uint32_t>(t % rs.L);
-                for (uint32_t dd = 0; dd <= rs.hl; ++dd) {
-                    const int64_t n = p - dd;
-                    if (n < 0 || n >= Nx) continue;
-                    acc += std::complex<double>(x[a][n].real(), x[a][n].imag()) *
-                           static_cast<double>(rs.h[ph + dd * rs.L]);
-                }
+                const uint32_t dmax = static_cast<uint32_t>(std::min<int64_t>(rs.hl, p));
+                const uint32_t dmin = p >= Nx ? static_cast<uint32_t>(p - Nx + 1) : 0u;
+                for (uint32_t dd = dmin; dd <= dmax; ++dd) acc += x[a][p - dd] * static_cast<R>(rs.h[ph + dd * rs.L]);
             }
-            const double phi = ph0 + static_cast<double>(m) * inc;
-            acc *= std::complex<double>(std::cos(phi), std::sin(phi));
+            if (mix) acc *= rot.at(m);
             out[a][m] = C(static_cast<R>(acc.real()), static_cast<R>(acc.imag()));
         }
     }
@@ -324,6 +351,17 @@ int16_t llr_to_i16(double v) {
 }
 
 namespace {
+// channel LUTs are init-time objects in the reference (rx_synced.cpp:147-157): build once
+const chest_lut_t& cached_lut(uint32_t Nsv, uint32_t b, uint32_t b_max, uint32_t u_max, int p, const chest_stats_t& st) {
+    static std::mutex mu;
+    static std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, int>, chest_lut_t> cache;
+    std::lock_guard<std::mutex> g(mu);
+    const auto key = std::make_tuple(Nsv, b, b_max, u_max, p);
+    auto it = cache.find(key);
+    if (it == cache.end()) it = cache.emplace(key, build_chest_lut(Nsv, b, b_max, st)).first;
+    return it->second;
+}
+
 template <typename R>
 struct rx_state_t {
     using C = std::complex<R>;
@@ -365,41 +403,46 @@ struct rx_state_t {
         const uint64_t need = dm.N_no_GI_os;
         y.assign(N_RX, std::vector<C>(need));
         for (uint32_t a = 0; a < N_RX; ++a) {
+            // input stream x[n] = iq[fine_peak + n] for n >= 0 (zero history before, zeros past the window)
             const float* src = in.iq + 2ull * a * in.S_in;
-            auto xs = [&](int64_t n) -> std::complex<double> {
+            const int64_t n_avail = std::max<int64_t>(0, static_cast<int64_t>(in.S_in) - in.fine_peak);
+            std::vector<C> xin(static_cast<size_t>(n_avail));
+            for (int64_t n = 0; n < n_avail; ++n) {
                 const int64_t idx = in.fine_peak + n;
-                if (n < 0 || idx < 0 || idx >= static_cast<int64_t>(in.S_in)) return {0, 0};
-                return {src[2 * idx], src[2 * idx + 1]};
-            };
+                xin[n] = idx >= 0 ? C(src[2 * idx], src[2 * idx + 1]) : C(0, 0);
+            }
             for (uint64_t m = 0; m < need; ++m) {
-                std::complex<double> acc{0, 0};
+                C acc{0, 0};
                 if (rs.L == 1 && rs.M == 1) {
-                    acc = xs(static_cast<int64_t>(m));
+                    if (static_cast<int64_t>(m) < n_avail) acc = xin[m];
                 } else {
                     const uint64_t t = rs.delay + m * rs.M;
                     const int64_t pp = static_cast<int64_t>(t / rs.L);
                     const uint32_t ph = static_cast<uint32_t>(t % rs.L);
-                    for (uint32_t dd = 0; dd <= rs.hl; ++dd)
-                        acc += xs(pp - dd) * static_cast<double>(rs.h[ph + dd * rs.L]);
+                    const uint32_t dmax = static_cast<uint32_t>(std::min<int64_t>(rs.hl, pp));
+                    const uint32_t dmin = pp >= n_avail ? static_cast<uint32_t>(std::min<int64_t>(pp - n_avail + 1, rs.hl + 1)) : 0u;
+                    for (uint32_t dd = dmin; dd <= dmax; ++dd) acc += xin[pp - dd] * static_cast<R>(rs.h[ph + dd * rs.L]);
                 }
-                y[a][m] = C(static_cast<R>(acc.real()), static_cast<R>(acc.imag()));
+                y[a][m] = acc;
             }
         }
     }
 
-    // mix one symbol of length len starting at rpos (mixer.cpp:41-65 closed form)
+    // mix one symbol of length len starting at rpos (mixer.cpp:41-65; phase continuous, the
+    // increment changes after the STF)
     std::vector<std::vector<C>> take_mixed(uint32_t len) {
         std::vector<std::vector<C>> s(N_RX, std::vector<C>(len));
-        for (uint32_t a = 0; a < N_RX; ++a)
+        const bool stf = rpos < n_stf;
+        const double ph0 = stf ? 0.0 : static_cast<double>(n_stf) * mix_inc0;
+        const double inc = stf ? mix_inc0 : mix_inc1;
+        const uint64_t m0 = stf ? 0 : n_stf;
+        for (uint32_t a = 0; a < N_RX; ++a) {
+            rotator_t<R> rot(ph0, inc);
             for (uint32_t i = 0; i < len; ++i) {
                 const uint64_t m = rpos + i;
-                const double phi = m < n_stf ? static_cast<double>(m) * mix_inc0
-                                             : static_cast<double>(n_stf) * mix_inc0 +
-                                                   static_cast<double>(m - n_stf) * mix_inc1;
-                const std::complex<double> v =
-                    std::complex<double>(y[a][m].real(), y[a][m].imag()) * std::complex<double>(std::cos(phi), std::sin(phi));
-                s[a][i] = C(static_cast<R>(v.real()), static_cast<R>(v.imag()));
+                s[a][i] = y[a][m] * rot.at(m - m0);
             }
+        }
         rpos += len;
         return s;
     }
@@ -644,8 +687,8 @@ struct rx_state_t {
         chest = zf;
         prof = chest_profiles(cfg.u_max);
         for (int i = 0; i < 3; ++i) {
-            lut0.push_back(build_chest_lut(0, ps.num.b, cfg.b_max, prof[i]));
-            lut_lr.push_back(build_chest_lut(N_step, ps.num.b, cfg.b_max, prof[i]));
+            lut0.push_back(cached_lut(0, ps.num.b, cfg.b_max, cfg.u_max, i, prof[i]));
+            lut_lr.push_back(cached_lut(N_step, ps.num.b, cfg.b_max, cfg.u_max, i, prof[i]));
         }
         drs = drs_schedule(N_eff_TX, ps.N_DF_symb);
         pcc_cells(ps.num.b, N_eff_TX, pcc_l, pcc_k);
