@@ -172,8 +172,9 @@ struct tx_tables {
     geo::dims_t dm{};
     dev::fft_plan plan{};
     geo::resampler_t rs;
-    dbuf code, stf, W, taps, tw, qam, qpsk;
+    dbuf code, stf, W, taps, tw, qam, qpsk, pdc_off;
     std::vector<float> wscale;  // per codebook
+    uint32_t stage_bytes = 0;
 };
 
 struct rx1_tables {  // per (u, b, N_eff_TX): STF/PCC phase
@@ -191,7 +192,7 @@ struct rx2_tables {  // per (psdef): PDC phase
     dnrp_packet_sizes q{};
     geo::maps_t maps;
     uint32_t n_pdc_ops = 0;
-    dbuf drs_l, drs_meta, pdc_k, pdc_off, pdc_ops;
+    dbuf drs_l, drs_meta, pdc_k, pdc_off, pdc_sym, pdc_ops;
 };
 
 struct netid_seq {
@@ -296,7 +297,15 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         for (const auto& w : geo::W_matrix(t->tm.N_TS, t->tm.N_TX, cb, &s)) W.push_back(make_float2(w.real(), w.imag()));
         t->wscale.push_back(s);
     }
-    if (!t->code.upload(m.code) || !t->stf.upload(stf) || !t->W.upload(W) || !t->taps.upload(t->rs.h) ||
+    // LDS staging of the per-symbol PDC source bytes (8 bytes per thread of a 256-thread WG)
+    uint32_t mx = 0;
+    for (uint32_t l = 1; l <= t->q.N_DF_symb; ++l) {
+        const uint64_t b0 = uint64_t(m.pdc_sym_off[l]) * t->tm.N_SS * t->q.N_bps / 8;
+        const uint64_t b1 = (uint64_t(m.pdc_sym_off[l + 1]) * t->tm.N_SS * t->q.N_bps + 7) / 8 + 1;
+        mx = std::max<uint32_t>(mx, static_cast<uint32_t>(b1 - b0));
+    }
+    t->stage_bytes = mx <= 8 * 256 ? (mx + 3) / 4 * 4 : 0;
+    if (!t->code.upload(m.code) || !t->stf.upload(stf) || !t->pdc_off.upload(m.pdc_sym_off) || !t->W.upload(W) || !t->taps.upload(t->rs.h) ||
         !t->tw.upload(twiddles(t->dm.Nd)) || !t->qam.upload(constellation(t->q.N_bps)) ||
         !t->qpsk.upload(constellation(2))) {
         *err = DNRP_ENOMEM;
@@ -392,8 +401,11 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         dl.push_back(x.l);
         dm.push_back(x.ts_first | (x.ts_last << 8) | (x.parity << 16));
     }
+    std::vector<uint16_t> csym(t->maps.pdc_k.size());
+    for (uint32_t l = 0; l <= t->q.N_DF_symb; ++l)
+        for (uint32_t j = t->maps.pdc_sym_off[l]; j < t->maps.pdc_sym_off[l + 1]; ++j) csym[j] = static_cast<uint16_t>(l);
     if (!t->drs_l.upload(dl) || !t->drs_meta.upload(dm) || !t->pdc_k.upload(t->maps.pdc_k) ||
-        !t->pdc_off.upload(t->maps.pdc_sym_off) || !t->pdc_ops.upload(pdc_ops)) {
+        !t->pdc_off.upload(t->maps.pdc_sym_off) || !t->pdc_sym.upload(csym) || !t->pdc_ops.upload(pdc_ops)) {
         *err = DNRP_ENOMEM;
         return nullptr;
     }
@@ -418,6 +430,9 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t) {
     a.M = t->rs.M;
     a.delay = t->rs.delay;
     a.hl = t->rs.hl;
+    a.m_star = 0;
+    while ((t->rs.delay + a.m_star * t->rs.M) % t->rs.L) ++a.m_star;
+    a.p_star = (t->rs.delay + a.m_star * t->rs.M) / t->rs.L;
     a.sym_per_block = 4;
     a.Nf_pad = ctx->rx_Nf_pad;
     a.n_sym_total = ctx->rx_nsym_cap + 1;
@@ -538,6 +553,7 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     tx_tables* t = get_tx(ctx, *psdef, &err);
     if (!t) return err;
     if (S < t->dm.N_packet_rs || pdc_stride < (t->q.G + 7) / 8) return DNRP_EINVAL;
+    if (t->q.N_b_OCC + 1 > 1024) return DNRP_EUNSUPPORTED;  // tx_kernel stages <= 4 code words per thread
     auto* pk = static_cast<dev::tx_pkt*>(ctx->st_tx.get(sizeof(dev::tx_pkt) * n));
     if (!pk) return DNRP_ENOMEM;
     for (uint32_t i = 0; i < n; ++i) {
@@ -583,8 +599,15 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     a.S = S;
     a.pdc_stride = pdc_stride;
     a.G = t->q.G;
-    a.xbuf_len = t->rs.hl + t->dm.STF_CP + t->dm.Nd + 16;
+    // the ring holds one symbol's FIR windows (reaching back hl + M inputs before the symbol) plus the
+    // next symbol's samples, so resampling needs no barrier before the next CP write
+    a.ring = (t->rs.hl + t->rs.M + 2 * std::max(t->dm.STF_CP, t->dm.CP) + 2 * t->dm.Nd + 64 + 63) / 64 * 64;
+    a.m_star = 0;
+    while ((t->rs.delay + a.m_star * t->rs.M) % t->rs.L) ++a.m_star;
+    a.p_star = (t->rs.delay + a.m_star * t->rs.M) / t->rs.L;
+    a.stage_bytes = t->stage_bytes;
     a.code = t->code.as<uint32_t>();
+    a.pdc_off = t->pdc_off.as<uint32_t>();
     a.stf = t->stf.as<float2>();
     a.W = t->W.as<float2>();
     a.taps = t->taps.as<float>();
@@ -713,6 +736,7 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const 
     ba.drs_meta = t2->drs_meta.as<uint32_t>();
     ba.pdc_k = t2->pdc_k.as<uint32_t>();
     ba.pdc_off = t2->pdc_off.as<uint32_t>();
+    ba.pdc_sym = t2->pdc_sym.as<uint16_t>();
     ba.N_bps = t2->q.N_bps;
     ba.pdc_seq = static_cast<const uint8_t* const*>(ctx->pdc_seq_ptrs.p);
     ba.llr = pdc_llr;

@@ -22,7 +22,7 @@ __device__ __forceinline__ float cnorm(float2 a) { return a.x * a.x + a.y * a.y;
 // exp(j*phi) for a double phase: exact range reduction in double, accurate sincos in float
 __device__ __forceinline__ float2 phasor(double phi) {
     const double twopi = 6.283185307179586476925286766559;
-    const double r = phi - twopi * rint(phi / twopi);
+    const double r = phi - twopi * rint(phi * 0.15915494309189533577);  // 1 / (2 pi)
     float s, c;
     sincosf(static_cast<float>(r), &s, &c);
     return make_float2(c, s);
@@ -48,16 +48,20 @@ __device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2&
 }
 
 // Stockham autosort passes on LDS ping-pong buffers; tw[j] = exp(-2*pi*i*j/N) (forward table).
+// nb transforms stored back to back (x[b*N .. b*N+N)) run in the same passes.
 // Returns the buffer holding the result. Whole workgroup participates; ends with a barrier.
 template <int SIGN>
-__device__ float2* fft_lds(float2* x, float2* y, const float2* __restrict__ tw, const fft_plan& p) {
+__device__ float2* fft_lds(float2* x_, float2* y_, const float2* __restrict__ tw, const fft_plan& p, uint32_t nb = 1) {
     const uint32_t N = p.N;
     uint32_t Ns = 1;
     for (uint32_t s = 0; s < p.nr; ++s) {
         const uint32_t R = p.radix[s];
         const uint32_t NR = N / R;
         const uint32_t tstep = N / (Ns * R);
-        for (uint32_t j = threadIdx.x; j < NR; j += blockDim.x) {
+        for (uint32_t jb = threadIdx.x; jb < nb * NR; jb += blockDim.x) {
+            const uint32_t b = jb / NR, j = jb - b * NR;
+            const float2* x = x_ + b * N;
+            float2* y = y_ + b * N;
             const uint32_t k = j % Ns;
             const uint32_t od = (j / Ns) * Ns * R + k;
             if (R == 4) {
@@ -111,12 +115,82 @@ __device__ float2* fft_lds(float2* x, float2* y, const float2* __restrict__ tw, 
             }
         }
         __syncthreads();
-        float2* t = x;
-        x = y;
-        y = t;
+        float2* t = x_;
+        x_ = y_;
+        y_ = t;
         Ns *= R;
     }
-    return x;
+    return x_;
+}
+
+// Power-of-two sizes (every u>=2 / b in {1,2,4,8,16} FFT of tx_rx.hpp:67-69): radix-4 Stockham
+// passes with shift/mask index arithmetic (no integer division) + one radix-2 pass for odd log2.
+// tw: forward twiddle table of N entries (LDS or global), tw[j] = exp(-2 pi i j / N).
+template <int SIGN>
+__device__ float2* fft_pow2(float2* x_, float2* y_, const float2* tw, uint32_t log2N, uint32_t nb = 1) {
+    const uint32_t N = 1u << log2N;
+    uint32_t s = 0;  // log2(Ns)
+    for (; s + 2 <= log2N; s += 2) {
+        const uint32_t NR = N >> 2, kmask = (1u << s) - 1u, tsh = log2N - s - 2;
+        for (uint32_t jb = threadIdx.x; jb < nb * NR; jb += blockDim.x) {
+            const uint32_t j = jb & (NR - 1u), bo = (jb >> (log2N - 2)) << log2N;
+            const float2* x = x_ + bo;
+            float2* y = y_ + bo;
+            const uint32_t k = j & kmask;
+            const uint32_t od = ((j - k) << 2) + k;
+            float2 a0 = x[j], a1 = x[j + NR], a2 = x[j + 2 * NR], a3 = x[j + 3 * NR];
+            if (s) {
+                const uint32_t e = k << tsh;
+                float2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
+                if (SIGN > 0) {
+                    w1 = cconj(w1);
+                    w2 = cconj(w2);
+                    w3 = cconj(w3);
+                }
+                a1 = cmul(a1, w1);
+                a2 = cmul(a2, w2);
+                a3 = cmul(a3, w3);
+            }
+            dft4<SIGN>(a0, a1, a2, a3);
+            y[od] = a0;
+            y[od + (1u << s)] = a1;
+            y[od + (2u << s)] = a2;
+            y[od + (3u << s)] = a3;
+        }
+        __syncthreads();
+        float2* t = x_;
+        x_ = y_;
+        y_ = t;
+    }
+    if (s < log2N) {  // final radix-2 pass, Ns = N/2
+        const uint32_t NR = N >> 1, kmask = (1u << s) - 1u;
+        for (uint32_t jb = threadIdx.x; jb < nb * NR; jb += blockDim.x) {
+            const uint32_t j = jb & (NR - 1u), bo = (jb >> (log2N - 1)) << log2N;
+            const float2* x = x_ + bo;
+            float2* y = y_ + bo;
+            const uint32_t k = j & kmask;
+            const uint32_t od = ((j - k) << 1) + k;
+            const float2 a0 = x[j];
+            float2 a1 = x[j + NR];
+            float2 w = tw[k];
+            if (SIGN > 0) w = cconj(w);
+            a1 = cmul(a1, w);
+            y[od] = cadd(a0, a1);
+            y[od + (1u << s)] = csub(a0, a1);
+        }
+        __syncthreads();
+        float2* t = x_;
+        x_ = y_;
+        y_ = t;
+    }
+    return x_;
+}
+
+// dispatch: power-of-two fast path, generic mixed radix otherwise
+template <int SIGN>
+__device__ __forceinline__ float2* fft_any(float2* x, float2* y, const float2* tw, const fft_plan& p, uint32_t nb = 1) {
+    if ((p.N & (p.N - 1)) == 0) return fft_pow2<SIGN>(x, y, tw, 31u - __clz(p.N), nb);
+    return fft_lds<SIGN>(x, y, tw, p, nb);
 }
 
 // block-wide sum of a double, result valid in all threads (blockDim.x multiple of 64, <= 1024)

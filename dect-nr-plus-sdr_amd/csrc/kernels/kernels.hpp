@@ -28,9 +28,13 @@ struct tx_pkt {
 struct tx_args {
     fft_plan plan;  // IFFT size N_b_DFT_os
     uint32_t N_occ, off_lower, CP, STF_CP, N_DF, N_TS, N_TX, N_SS, N_bps, txdiv, mod, pattern_len;
-    uint32_t L, M, delay, hl, n_keep, S, pdc_stride, G, xbuf_len;
-    uint32_t pair[12];  // transmit diversity TS pairs, A | B << 4
+    uint32_t L, M, delay, hl, n_keep, S, pdc_stride, G;
+    uint32_t ring;            // resampler input ring length (samples)
+    uint32_t m_star, p_star;  // first phase-0 output (delay + m_star*M = p_star*L), polyphase.hpp
+    uint32_t stage_bytes;  // max PDC source bytes of one symbol staged in LDS (0: read global)
+    uint32_t pair[12];     // transmit diversity TS pairs, A | B << 4
     const uint32_t* code;
+    const uint32_t* pdc_off;  // [N_DF+2] first PDC cell of each symbol
     const float2* stf;
     const float2* W;     // [codebooks][N_TX][N_TS]
     const float* taps;   // [(hl+1)*L]
@@ -66,6 +70,7 @@ struct rx_front_args {
     fft_plan plan;
     uint32_t N_occ, off_lower, CP, STF_CP, N_RX, S_in, n_pattern, pattern_len, b;
     uint32_t L, M, delay, hl;  // RX resampler (L and M already swapped)
+    uint32_t m_star, p_star;   // first phase-0 output (delay + m_star*M = p_star*L), polyphase.hpp
     uint32_t sym_first, sym_count, sym_per_block, Nf_pad, n_sym_total;
     float amp_scale;           // sqrt(N_b_OCC) / N_b_DFT_os
     const float* taps;
@@ -95,6 +100,7 @@ struct rx_back_args {
     const uint32_t* pcc_off;
     const uint32_t* pdc_k;
     const uint32_t* pdc_off;
+    const uint16_t* pdc_sym;    // per PDC cell: OFDM symbol index
     const uint32_t* lut_pw[2][3];  // [mode l / lr][profile]: [T][4][Nf] pilot | weight << 16
     const float* lut_w[2][3];
     uint32_t lut_n[2][3];

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Kernel-trace stats + PMC passes for the C4 bench (run on the GPU box from the repo root).
+# Usage: tools/profile_r01.sh <tag> [bench args...]
+set -e
+tag=$1; shift
+out=gpurun_out/prof_$tag
+mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- \
+    python3 bench.py --no-cpu-baseline "$@" > $out/trace.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
+    --output-format csv -d $out/pmc_sq -o run -- python3 bench.py --no-cpu-baseline "$@" > $out/pmc_sq.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_fetch -o run -- \
+    python3 bench.py --no-cpu-baseline "$@" > $out/pmc_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o run -- \
+    python3 bench.py --no-cpu-baseline "$@" > $out/pmc_write.log 2>&1
