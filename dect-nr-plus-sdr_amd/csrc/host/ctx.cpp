@@ -177,22 +177,36 @@ struct tx_tables {
     uint32_t stage_bytes = 0;
 };
 
+// device copy of a geo::rx_plan_t
+struct rx_plan_dev {
+    uint32_t n_dops = 0, n_epochs = 0;
+    dbuf dl, dmeta, segs, epochs;
+    bool upload(const geo::rx_plan_t& p) {
+        static_assert(sizeof(geo::rx_seg_t) == sizeof(dev::rx_seg), "rx_seg layout");
+        static_assert(sizeof(geo::rx_epoch_t) == sizeof(dev::rx_epoch), "rx_epoch layout");
+        n_dops = static_cast<uint32_t>(p.dl.size());
+        n_epochs = static_cast<uint32_t>(p.epochs.size());
+        return dl.upload(p.dl) && dmeta.upload(p.dmeta) && segs.upload(p.segs) && epochs.upload(p.epochs);
+    }
+};
+
 struct rx1_tables {  // per (u, b, N_eff_TX): STF/PCC phase
     uint32_t u, b, N_eff_TX, Nd, N_occ, off_lower, CP, STF_CP, n_pattern, pattern_len;
     dev::fft_plan plan{};
     geo::resampler_t rs;
     geo::maps_t maps;
-    uint32_t pcc_max = 0, n_pcc_ops = 0;
-    dbuf stf, tw, taps, drs_l, drs_meta, drs_k, drs_v, pcc_k, pcc_off, pcc_ops;
-    dbuf lut_pw[2][3], lut_w[2][3];
+    uint32_t pcc_max = 0;
+    dbuf stf, tw, taps, drs_k, drs_v, pcc_k;
+    rx_plan_dev bplan;  // PCC phase back end
+    dbuf lut_pw[2][3], lut_w[2][3], luts;
     uint32_t lut_n[2][3] = {}, lut_T[2] = {};
 };
 
 struct rx2_tables {  // per (psdef): PDC phase
     dnrp_packet_sizes q{};
     geo::maps_t maps;
-    uint32_t n_pdc_ops = 0;
-    dbuf drs_l, drs_meta, pdc_k, pdc_off, pdc_sym, pdc_ops;
+    dbuf pdc_k, pdc_sym;
+    rx_plan_dev bplan;  // PDC phase back end
 };
 
 struct netid_seq {
@@ -210,7 +224,7 @@ struct dnrp_ctx {
     std::map<uint32_t, std::unique_ptr<netid_seq>> netid;
     dbuf pcc_seq;
     // batch scratch
-    dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs;
+    dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d;
     pinned st_tx, st_rxin, st_seq, st_rep;
     // retained RX phase-1 state
     rx1_tables* rx1_last = nullptr;
@@ -348,17 +362,12 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
     std::vector<geo::op_t> pcc_ops, dummy;
     geo::build_rx_ops(t->maps, N_eff_TX, 20, c.chestim_mode_lr != 0, std::max(1u, c.chestim_lr_stride), pcc_ops, dummy,
                       t->pcc_max);
-    t->n_pcc_ops = static_cast<uint32_t>(pcc_ops.size());
     std::vector<float2> stfv(t->maps.Nf);
     for (uint32_t k = 0; k < t->maps.Nf; ++k) stfv[k] = make_float2(t->maps.stf[k].real(), t->maps.stf[k].imag());
-    std::vector<uint32_t> dl, dm;
-    for (const auto& d : t->maps.drs) {
-        dl.push_back(d.l);
-        dm.push_back(d.ts_first | (d.ts_last << 8) | (d.parity << 16));
-    }
-    bool ok = t->stf.upload(stfv) && t->tw.upload(twiddles(t->Nd)) && t->taps.upload(t->rs.h) && t->drs_l.upload(dl) &&
-              t->drs_meta.upload(dm) && t->drs_k.upload(t->maps.drs_k) && t->drs_v.upload(t->maps.drs_v) &&
-              t->pcc_k.upload(t->maps.pcc_k) && t->pcc_off.upload(t->maps.pcc_sym_off) && t->pcc_ops.upload(pcc_ops);
+    const auto plan = geo::build_rx_plan(t->maps, pcc_ops, N_eff_TX);
+    bool ok = t->stf.upload(stfv) && t->tw.upload(twiddles(t->Nd)) && t->taps.upload(t->rs.h) &&
+              t->drs_k.upload(t->maps.drs_k) && t->drs_v.upload(t->maps.drs_v) && t->pcc_k.upload(t->maps.pcc_k) &&
+              t->bplan.upload(plan);
     const uint32_t Nsv = N_eff_TX <= 2 ? 5 : 10;
     for (uint32_t mode = 0; mode < 2 && ok; ++mode)
         for (uint32_t p = 0; p < 3 && ok; ++p) {
@@ -367,7 +376,11 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
             t->lut_n[mode][p] = L.n;
             t->lut_T[mode] = L.T;
         }
-    if (!ok) {
+    std::vector<dev::rx_lut> luts(6);
+    for (uint32_t mode = 0; mode < 2; ++mode)
+        for (uint32_t p = 0; p < 3; ++p)
+            luts[mode * 3 + p] = {t->lut_pw[mode][p].as<uint32_t>(), t->lut_w[mode][p].as<float>(), t->lut_n[mode][p], 0};
+    if (!ok || !t->luts.upload(luts)) {
         *err = DNRP_ENOMEM;
         return nullptr;
     }
@@ -395,17 +408,11 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
     uint32_t pm;
     geo::build_rx_ops(t->maps, tm.N_eff_TX, t->q.N_DF_symb, ctx->cfg.chestim_mode_lr != 0,
                       std::max(1u, ctx->cfg.chestim_lr_stride), pcc_ops, pdc_ops, pm);
-    t->n_pdc_ops = static_cast<uint32_t>(pdc_ops.size());
-    std::vector<uint32_t> dl, dm;
-    for (const auto& x : t->maps.drs) {
-        dl.push_back(x.l);
-        dm.push_back(x.ts_first | (x.ts_last << 8) | (x.parity << 16));
-    }
+    const auto plan = geo::build_rx_plan(t->maps, pdc_ops, tm.N_eff_TX);
     std::vector<uint16_t> csym(t->maps.pdc_k.size());
     for (uint32_t l = 0; l <= t->q.N_DF_symb; ++l)
         for (uint32_t j = t->maps.pdc_sym_off[l]; j < t->maps.pdc_sym_off[l + 1]; ++j) csym[j] = static_cast<uint16_t>(l);
-    if (!t->drs_l.upload(dl) || !t->drs_meta.upload(dm) || !t->pdc_k.upload(t->maps.pdc_k) ||
-        !t->pdc_off.upload(t->maps.pdc_sym_off) || !t->pdc_sym.upload(csym) || !t->pdc_ops.upload(pdc_ops)) {
+    if (!t->pdc_k.upload(t->maps.pdc_k) || !t->pdc_sym.upload(csym) || !t->bplan.upload(plan)) {
         *err = DNRP_ENOMEM;
         return nullptr;
     }
@@ -447,33 +454,58 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t) {
     return a;
 }
 
-dev::rx_back_args back_args(dnrp_ctx* ctx, rx1_tables* t) {
-    dev::rx_back_args a{};
-    a.N_occ = t->N_occ;
-    a.N_RX = ctx->cfg.N_TX_max;
-    a.N_eff_TX = t->N_eff_TX;
-    a.Nf_pad = ctx->rx_Nf_pad;
-    a.n_sym_total = ctx->rx_nsym_cap + 1;
-    a.n_drs = t->N_occ / 4;
-    fill_pairs(t->N_eff_TX, a.pair, a.mod);
-    a.txdiv = t->N_eff_TX > 1;
-    a.drs_k = t->drs_k.as<uint32_t>();
-    a.drs_v = t->drs_v.as<float>();
-    a.pcc_k = t->pcc_k.as<uint32_t>();
-    a.pcc_off = t->pcc_off.as<uint32_t>();
-    for (int m = 0; m < 2; ++m) {
-        a.lut_T[m] = t->lut_T[m];
-        for (int p = 0; p < 3; ++p) {
-            a.lut_pw[m][p] = t->lut_pw[m][p].as<uint32_t>();
-            a.lut_w[m][p] = t->lut_w[m][p].as<float>();
-            a.lut_n[m][p] = t->lut_n[m][p];
-        }
-    }
-    for (int p = 0; p < 3; ++p) a.prof_snr[p] = geo::lut_profile_snr_db(p);
-    a.Y = ctx->Y.as<float2>();
-    a.st = ctx->rx_st.as<dev::rx_pkt_state>();
-    a.pcc_seq = ctx->pcc_seq.as<uint8_t>();
-    return a;
+// back-end launches of one phase: SNR chain, then cells (rx_back.hip)
+int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t n, bool pdc, uint32_t N_bps,
+                const uint32_t* kk, const uint16_t* pdc_sym, int16_t* llr, uint32_t llr_stride, hipStream_t st) {
+    const char* name = pdc ? "rx_pdc" : "rx_pcc";
+    if (!ctx->lut_d.ensure(size_t(ctx->cfg.max_batch) * std::max(plan.n_dops, 1u))) return DNRP_ENOMEM;
+    dev::rx_snr_args s{};
+    s.N_RX = ctx->cfg.N_TX_max;
+    s.Nf_pad = ctx->rx_Nf_pad;
+    s.n_sym_total = ctx->rx_nsym_cap + 1;
+    s.n_drs = t->N_occ / 4;
+    s.n_dops = plan.n_dops;
+    s.is_pdc = pdc;
+    s.dl = plan.dl.as<uint32_t>();
+    s.dmeta = plan.dmeta.as<uint32_t>();
+    s.drs_k = t->drs_k.as<uint32_t>();
+    s.drs_v = t->drs_v.as<float>();
+    for (int p = 0; p < 3; ++p) s.prof_snr[p] = geo::lut_profile_snr_db(p);
+    s.Y = ctx->Y.as<float2>();
+    s.st = ctx->rx_st.as<dev::rx_pkt_state>();
+    s.lut_d = ctx->lut_d.as<uint8_t>();
+    dev::rx_cells_args c{};
+    c.N_occ = t->N_occ;
+    c.N_RX = ctx->cfg.N_TX_max;
+    c.NT = t->N_eff_TX;
+    c.Nf_pad = ctx->rx_Nf_pad;
+    c.n_sym_total = ctx->rx_nsym_cap + 1;
+    c.n_drs = t->N_occ / 4;
+    c.n_dops = plan.n_dops;
+    c.n_epochs = plan.n_epochs;
+    c.N_bps = N_bps;
+    fill_pairs(t->N_eff_TX, c.pair, c.mod);
+    c.is_pdc = pdc;
+    c.epochs = plan.epochs.as<dev::rx_epoch>();
+    c.segs = plan.segs.as<dev::rx_seg>();
+    c.dl = s.dl;
+    c.dmeta = s.dmeta;
+    c.drs_k = s.drs_k;
+    c.drs_v = s.drs_v;
+    c.kk = kk;
+    c.pdc_sym = pdc_sym;
+    c.luts = t->luts.as<dev::rx_lut>();
+    c.Y = s.Y;
+    c.lut_d = s.lut_d;
+    c.pcc_seq = ctx->pcc_seq.as<uint8_t>();
+    c.pdc_seq = static_cast<const uint8_t* const*>(ctx->pdc_seq_ptrs.p);
+    c.llr = llr;
+    c.llr_stride = llr_stride;
+    ctx->tic(name, st);
+    if (dev::launch_rx_snr(s, n, st) != hipSuccess) return DNRP_EDEVICE;
+    if (plan.n_epochs && dev::launch_rx_cells(c, n, st) != hipSuccess) return DNRP_EDEVICE;
+    ctx->toc(name, st);
+    return DNRP_OK;
 }
 
 }  // namespace
@@ -669,18 +701,8 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
     ctx->tic("rx_fft_pcc", st);
     if (dev::launch_rx_fft(fa, n, st) != hipSuccess) return DNRP_EDEVICE;
     ctx->toc("rx_fft_pcc", st);
-    auto ba = back_args(ctx, t);
-    ba.ops = t->pcc_ops.as<dev::rx_op>();
-    ba.n_ops = t->n_pcc_ops;
-    ba.drs_l = t->drs_l.as<uint32_t>();
-    ba.drs_meta = t->drs_meta.as<uint32_t>();
-    ba.N_bps = 2;
-    ba.llr = pcc_llr;
-    ba.llr_stride = 196;
-    ba.is_pdc = 0;
-    ctx->tic("rx_pcc", st);
-    if (dev::launch_rx_back(ba, n, st) != hipSuccess) return DNRP_EDEVICE;
-    ctx->toc("rx_pcc", st);
+    if ((err = launch_back(ctx, t, t->bplan, n, false, 2, t->pcc_k.as<uint32_t>(), nullptr, pcc_llr, 196, st)) != DNRP_OK)
+        return err;
     ctx->rx1_last = t;
     if (rep) {
         std::vector<dev::rx_pkt_state> S(n);
@@ -729,22 +751,9 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const 
         if (dev::launch_rx_fft(fa, n, st) != hipSuccess) return DNRP_EDEVICE;
         ctx->toc("rx_fft_pdc", st);
     }
-    auto ba = back_args(ctx, t);
-    ba.ops = t2->pdc_ops.as<dev::rx_op>();
-    ba.n_ops = t2->n_pdc_ops;
-    ba.drs_l = t2->drs_l.as<uint32_t>();
-    ba.drs_meta = t2->drs_meta.as<uint32_t>();
-    ba.pdc_k = t2->pdc_k.as<uint32_t>();
-    ba.pdc_off = t2->pdc_off.as<uint32_t>();
-    ba.pdc_sym = t2->pdc_sym.as<uint16_t>();
-    ba.N_bps = t2->q.N_bps;
-    ba.pdc_seq = static_cast<const uint8_t* const*>(ctx->pdc_seq_ptrs.p);
-    ba.llr = pdc_llr;
-    ba.llr_stride = llr_stride;
-    ba.is_pdc = 1;
-    ctx->tic("rx_pdc", st);
-    if (dev::launch_rx_back(ba, n, st) != hipSuccess) return DNRP_EDEVICE;
-    ctx->toc("rx_pdc", st);
+    if ((err = launch_back(ctx, t, t2->bplan, n, true, t2->q.N_bps, t2->pdc_k.as<uint32_t>(), t2->pdc_sym.as<uint16_t>(),
+                           pdc_llr, llr_stride, st)) != DNRP_OK)
+        return err;
     if (rep) {
         std::vector<dev::rx_pkt_state> S(n);
         HIPCHK(hipMemcpyAsync(S.data(), ctx->rx_st.p, sizeof(dev::rx_pkt_state) * n, hipMemcpyDeviceToHost, st));

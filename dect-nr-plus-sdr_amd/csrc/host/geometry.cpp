@@ -2,6 +2,8 @@
 // file it restates (paths relative to maxpenner/DECT-NR-Plus-SDR).
 #include "geometry.hpp"
 
+#include <cstring>
+
 #include <algorithm>
 #include <cmath>
 #include <stdexcept>
@@ -659,6 +661,80 @@ void build_rx_ops(const maps_t& m, uint32_t N_eff_TX, uint32_t N_DF, bool mode_l
             rel = 0;
         }
     }
+}
+
+rx_plan_t build_rx_plan(const maps_t& m, const std::vector<op_t>& ops, uint32_t NT) {
+    rx_plan_t p;
+    uint16_t src[4][2];
+    for (auto& r : src) r[0] = r[1] = RX_SRC_NONE;
+    uint32_t drs_off = 0, drs_cnt = 0;
+    bool dirty = true;
+    rx_seg_t ev{};
+    auto units = [&](const rx_seg_t& s) { return NT == 1 ? s.j1 - s.j0 : (s.j1 - s.j0) / 2; };
+    auto add = [&](rx_seg_t s) {
+        if (s.j1 <= s.j0) return;
+        if (dirty || p.epochs.empty()) {
+            rx_epoch_t e{};
+            std::memcpy(e.src, src, sizeof(src));
+            e.seg0 = e.seg1 = static_cast<uint32_t>(p.segs.size());
+            p.epochs.push_back(e);
+            dirty = false;
+        }
+        auto& e = p.epochs.back();
+        if (s.kind == OP_PDC && e.seg1 > e.seg0) {  // extend a run of PDC symbols on the same event
+            auto& b = p.segs.back();
+            if (b.kind == OP_PDC && b.j1 == s.j0 && b.mode == s.mode && b.rel == s.rel && b.swap == s.swap &&
+                b.off == s.off && b.drs_cnt == s.drs_cnt) {
+                e.units -= units(b);
+                b.j1 = s.j1;
+                e.units += units(b);
+                return;
+            }
+        }
+        s.u0 = e.units;
+        e.units += units(s);
+        p.segs.push_back(s);
+        e.seg1 = static_cast<uint32_t>(p.segs.size());
+    };
+    for (const auto& op : ops) {
+        if (op.kind == OP_DRS) {
+            const auto& d = m.drs[op.b];
+            const uint32_t dop = static_cast<uint32_t>(p.dl.size());
+            p.dl.push_back(d.l);
+            p.dmeta.push_back(d.ts_first | (d.ts_last << 8) | (d.parity << 16));
+            drs_off = 0;
+            for (uint32_t t = d.ts_first; t <= d.ts_last; ++t) {  // channel_antenna.hpp:38-63 write offsets
+                const uint32_t rel = op.c, ps = op.d;
+                const bool lhs = rel <= 1, hi = (t & 3u) >= 2;
+                const uint32_t off = (ps % 2 == 0) ? (lhs ? hi : !hi) : (lhs ? !hi : hi);
+                drs_off |= off << t;
+                src[t][off] = static_cast<uint16_t>(dop);
+            }
+            ++drs_cnt;
+            dirty = true;
+        } else if (op.kind == OP_EVENT) {
+            ev.mode = op.a;
+            ev.rel = op.b;
+            ev.swap = (op.c & 1u) ? 2u : 0u;
+            ev.off = drs_off;
+            ev.drs_cnt = drs_cnt;
+        } else if (op.kind == OP_PCC) {
+            rx_seg_t s = ev;
+            s.kind = OP_PCC;
+            s.l = op.a;
+            s.j0 = m.pcc_sym_off[op.b];
+            s.j1 = m.pcc_sym_off[op.b + 1];
+            add(s);
+        } else if (op.kind == OP_PDC) {
+            rx_seg_t s = ev;
+            s.kind = OP_PDC;
+            s.l = op.a;
+            s.j0 = m.pdc_sym_off[op.a];
+            s.j1 = m.pdc_sym_off[op.a + 1];
+            add(s);
+        }
+    }
+    return p;
 }
 
 }  // namespace dnrp::geo

@@ -94,4 +94,29 @@ struct op_t {
 void build_rx_ops(const maps_t& m, uint32_t N_eff_TX, uint32_t N_DF, bool mode_lr, uint32_t stride,
                   std::vector<op_t>& pcc_ops, std::vector<op_t>& pdc_ops, uint32_t& pcc_max_symbol);
 
+// RX back-end plan derived from one op list. The DRS symbols in processing order feed the
+// sequential SNR / LUT-pick chain (one WG per packet); the cell work is grouped into epochs of
+// constant pilot-buffer content, each a list of segments sharing one interpolation event (one WG
+// per packet x epoch). src[t][o]: DRS op whose zero-forced pilots sit at interlace offset o of
+// stream t in the epoch's pilot buffer (channel_antenna.hpp:38-63), RX_SRC_NONE if never written.
+constexpr uint16_t RX_SRC_NONE = 0xFFFF;
+struct rx_seg_t {
+    uint32_t kind;     // OP_PCC / OP_PDC
+    uint32_t l;        // PCC: OFDM symbol
+    uint32_t j0, j1;   // cell range (pcc_k / pdc_k indices)
+    uint32_t mode, rel, swap, off;  // event: LUT mode, row, TS swap (0/2), write offsets of the latest DRS
+    uint32_t drs_cnt;  // DRS ops processed before the event (selects the LUT profile pick)
+    uint32_t u0;       // first work unit (cell or SFBC pair) of the segment within its epoch
+};
+struct rx_epoch_t {
+    uint16_t src[4][2];
+    uint32_t seg0, seg1, units;
+};
+struct rx_plan_t {
+    std::vector<uint32_t> dl, dmeta;  // per DRS op: symbol; ts_first | ts_last << 8 | parity << 16
+    std::vector<rx_seg_t> segs;
+    std::vector<rx_epoch_t> epochs;
+};
+rx_plan_t build_rx_plan(const maps_t& m, const std::vector<op_t>& ops, uint32_t N_eff_TX);
+
 }  // namespace dnrp::geo

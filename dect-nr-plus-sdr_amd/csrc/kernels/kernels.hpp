@@ -84,36 +84,53 @@ struct rx_front_args {
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);
 hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st);
 
-struct rx_op {
-    uint32_t kind, a, b, c, d;
+// back end, see geometry.hpp rx_plan_t (identical layouts)
+struct rx_seg {
+    uint32_t kind, l, j0, j1, mode, rel, swap, off, drs_cnt, u0;
+};
+struct rx_epoch {
+    uint16_t src[4][2];
+    uint32_t seg0, seg1, units;
 };
 
-struct rx_back_args {
-    uint32_t N_occ, N_RX, N_eff_TX, Nf_pad, n_sym_total, n_drs, N_bps, mod, n_ops, txdiv;
-    uint32_t pair[12];
-    const rx_op* ops;
-    const uint32_t* drs_l;      // per DRS index: symbol
-    const uint32_t* drs_meta;   // per DRS index: ts_first | ts_last << 8 | parity << 16
-    const uint32_t* drs_k;      // [2][4][n_drs]
-    const float* drs_v;         // [8][n_drs]
-    const uint32_t* pcc_k;
-    const uint32_t* pcc_off;
-    const uint32_t* pdc_k;
-    const uint32_t* pdc_off;
-    const uint16_t* pdc_sym;    // per PDC cell: OFDM symbol index
-    const uint32_t* lut_pw[2][3];  // [mode l / lr][profile]: [T][4][Nf] pilot | weight << 16
-    const float* lut_w[2][3];
-    uint32_t lut_n[2][3];
-    uint32_t lut_T[2];
+struct rx_snr_args {        // DRS zero-forcing SNR chain + LUT profile picks, one WG per packet
+    uint32_t N_RX, Nf_pad, n_sym_total, n_drs, n_dops, is_pdc;
+    const uint32_t* dl;     // per DRS op: symbol
+    const uint32_t* dmeta;  // per DRS op: ts_first | ts_last << 8 | parity << 16
+    const uint32_t* drs_k;  // [2][4][n_drs]
+    const float* drs_v;     // [8][n_drs]
     float prof_snr[3];
     const float2* Y;
     rx_pkt_state* st;
+    uint8_t* lut_d;         // [n][n_dops]: profile picked after each DRS op
+};
+hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st);
+
+struct rx_lut {             // one Wiener LUT: [T][4][Nf] pilot | weight << 16, weights [n_vec][n]
+    const uint32_t* pw;
+    const float* w;
+    uint32_t n, pad;
+};
+
+struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epoch)
+    uint32_t N_occ, N_RX, NT, Nf_pad, n_sym_total, n_drs, n_dops, n_epochs, N_bps, mod, is_pdc;
+    uint32_t pair[12];
+    const rx_epoch* epochs;
+    const rx_seg* segs;
+    const uint32_t* dl;
+    const uint32_t* dmeta;
+    const uint32_t* drs_k;
+    const float* drs_v;
+    const uint32_t* kk;        // pcc_k (PCC phase) or pdc_k (PDC phase)
+    const uint16_t* pdc_sym;   // per PDC cell: OFDM symbol
+    const rx_lut* luts;        // [mode l / lr][profile] (device table: no dynamic kernel-argument indexing)
+    const float2* Y;
+    const uint8_t* lut_d;
     const uint8_t* pcc_seq;
     const uint8_t* const* pdc_seq;  // per packet (PDC phase)
     int16_t* llr;                   // PCC: [n][196], PDC: [n][llr_stride]
     uint32_t llr_stride;
-    uint32_t is_pdc;
 };
-hipError_t launch_rx_back(const rx_back_args& a, uint32_t n, hipStream_t st);
+hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st);
 
 }  // namespace dnrp::dev

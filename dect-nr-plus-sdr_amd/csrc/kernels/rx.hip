@@ -7,10 +7,7 @@
 //  rx_fft_kernel   one WG per (packet, antenna, symbol block): resampling + phase-continuous mixer
 //                  + CP removal + FFT + bin extraction + amplitude scaling + STO derotation
 //                  (rx_synced.cpp:711-771) into the frequency-domain grid Y in HBM.
-//  rx_back_kernel  one WG per packet: interprets the host-built schedule of DRS zero-forcing,
-//                  SNR-driven Wiener LUT choice, interpolation events and PCC/PDC cell
-//                  combining (MRC / SFBC), int16 soft demapping and descrambling
-//                  (rx_synced.cpp:773-1392, pcc_enc.cpp:297, pdc_enc.cpp:339-344).
+// The back end (channel estimation, equalisation, demapping) is in rx_back.hip.
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
@@ -324,226 +321,6 @@ hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
         hipLaunchKernelGGL((rx_fft_kernel<9, 10, 4>), g, b, lds, st, a);
     else
         hipLaunchKernelGGL((rx_fft_kernel<0, 0, 0>), g, b, lds, st, a);
-    return hipGetLastError();
-}
-
-// ===================================================================== back end
-__device__ __forceinline__ int16_t q16(float v) {
-    const float r = rintf(v);
-    return static_cast<int16_t>(fminf(32767.f, fmaxf(-32768.f, r)));
-}
-
-// srsRAN demod_soft restatement: LTE max-log per axis with int16 scale constants
-__device__ __forceinline__ void demap(float2 y, uint32_t N_bps, float* L) {
-    switch (N_bps) {
-        case 1:
-            L[0] = -100.f * (y.x + y.y);
-            break;
-        case 2:
-            L[0] = -100.f * y.x;
-            L[1] = -100.f * y.y;
-            break;
-        case 4: {
-            const float S = 400.f, yr = S * y.x, yi = S * y.y, o = 2.f * S * 0.31622776601683794f;
-            L[0] = -yr;
-            L[1] = -yi;
-            L[2] = fabsf(yr) - o;
-            L[3] = fabsf(yi) - o;
-            break;
-        }
-        case 6: {
-            const float S = 700.f, yr = S * y.x, yi = S * y.y, q = S * 0.15430334996209191f;
-            L[0] = -yr;
-            L[1] = -yi;
-            L[2] = fabsf(yr) - 4.f * q;
-            L[3] = fabsf(yi) - 4.f * q;
-            L[4] = fabsf(L[2]) - 2.f * q;
-            L[5] = fabsf(L[3]) - 2.f * q;
-            break;
-        }
-        default: {
-            const float S = 1000.f, yr = S * y.x, yi = S * y.y, q = S * 0.07669649888473704f;
-            L[0] = -yr;
-            L[1] = -yi;
-            L[2] = fabsf(yr) - 8.f * q;
-            L[3] = fabsf(yi) - 8.f * q;
-            L[4] = fabsf(L[2]) - 4.f * q;
-            L[5] = fabsf(L[3]) - 4.f * q;
-            L[6] = fabsf(L[4]) - 2.f * q;
-            L[7] = fabsf(L[5]) - 2.f * q;
-            break;
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t seq_bit(const uint8_t* __restrict__ s, uint32_t i) {
-    return (s[i >> 3] >> (7u - (i & 7u))) & 1u;
-}
-
-__global__ void __launch_bounds__(256) rx_back_kernel(rx_back_args A) {
-    extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    __shared__ double red[16];
-    const uint32_t pkt = blockIdx.x;
-    const uint32_t N = A.N_occ, Nf = N + 1, nd = A.n_drs;
-    const uint32_t NT = A.N_eff_TX;  // <= 4
-    // Interlaced pilot buffer [N_RX][4][2 nd] (channel_antenna.hpp:38-63). The non-interlaced
-    // per-DRS-symbol estimates of the reference are the entries at each stream's write offset.
-    float2* zfi = smem;
-    rx_pkt_state S = A.st[pkt];
-    double sn = S.snr_SN, nn = S.snr_N;
-    uint32_t sn_cnt = S.snr_SN_cnt, nn_cnt = S.snr_N_cnt;
-    uint32_t lut_pick = 0;
-    uint32_t ev_mode = 0, ev_rel = 0, ev_swap = 0, ev_lut = 0;
-    uint32_t drs_off = 0, ev_off = 0;  // bit t: write offset of stream t in the latest DRS symbol
-    const float2* Yp = A.Y + size_t(pkt) * A.N_RX * A.n_sym_total * A.Nf_pad;
-    const uint8_t* pdc_seq = A.is_pdc ? A.pdc_seq[pkt] : nullptr;
-    int16_t* llr = A.llr + size_t(pkt) * A.llr_stride;
-    auto Yat = [&](uint32_t a, uint32_t l, uint32_t k) { return Yp[(size_t(a) * A.n_sym_total + l) * A.Nf_pad + k]; };
-    auto snr_db = [&]() -> float {
-        if (sn <= 0.0 || nn <= 0.0) return 0.f;
-        const float Sa = static_cast<float>((sn - nn) / sn_cnt), Na = static_cast<float>(nn / nn_cnt);
-        return 10.f * log10f(Sa / Na);
-    };
-    // on-the-fly Wiener interpolation at subcarrier k (rx_synced.cpp:932-946)
-    auto chest = [&](uint32_t a, uint32_t t, uint32_t k) {
-        const uint32_t tl = (t & 3u) ^ ev_swap;
-        const uint32_t pw = A.lut_pw[ev_mode][ev_lut][(size_t(ev_rel) * 4 + tl) * Nf + k];
-        const uint32_t nI = A.lut_n[ev_mode][ev_lut];
-        const float* __restrict__ w = A.lut_w[ev_mode][ev_lut] + size_t(pw >> 16) * nI;
-        const float2* z = zfi + (size_t(a) * 4 + t) * 2 * nd;
-        uint32_t pos = pw & 0xFFFFu, step = 1;
-        if (!ev_mode) {  // non-interlaced pilots of the latest DRS symbol
-            pos = 2 * pos + ((ev_off >> t) & 1u);
-            step = 2;
-        }
-        float ar = 0.f, ai = 0.f;
-        for (uint32_t i = 0; i < nI; ++i) {
-            const float2 v = z[pos + i * step];
-            ar = fmaf(v.x, w[i], ar);
-            ai = fmaf(v.y, w[i], ai);
-        }
-        return make_float2(ar, ai);
-    };
-    // combining + demapping + descrambling of cells [j0, j1); sym(j) gives the OFDM symbol
-    auto cells = [&](const uint32_t* kk, uint32_t j0, uint32_t j1, uint32_t N_bps, const uint8_t* seq, auto sym) {
-        const uint32_t cnt = j1 - j0;
-        const uint32_t units = NT == 1 ? cnt : cnt / 2;
-        for (uint32_t u = threadIdx.x; u < units; u += blockDim.x) {
-            float2 x0, x1 = make_float2(0.f, 0.f);
-            const uint32_t jj = j0 + (NT == 1 ? u : 2 * u);
-            const uint32_t l = sym(jj);
-            if (NT == 1) {  // MRC (rx_synced.cpp:1204-1306)
-                const uint32_t k = kk[jj];
-                float2 num = make_float2(0.f, 0.f);
-                float den = 0.f;
-                for (uint32_t a = 0; a < A.N_RX; ++a) {
-                    const float2 h = chest(a, 0, k);
-                    num = cadd(num, cmulc(Yat(a, l, k), h));
-                    den += cnorm(h);
-                }
-                x0 = cscale(num, 1.0f / den);
-            } else {  // SFBC pair (rx_synced.cpp:1335-1392)
-                const uint32_t k0 = kk[jj], k1 = kk[jj + 1];
-                const uint32_t pr = A.pair[(jj >> 1) % A.mod];
-                const uint32_t tA = pr & 0xFu, tB = pr >> 4;
-                float2 n0 = make_float2(0.f, 0.f), n1 = make_float2(0.f, 0.f);
-                float den = 0.f;
-                for (uint32_t a = 0; a < A.N_RX; ++a) {
-                    const float2 h0 = cscale(cadd(chest(a, tA, k0), chest(a, tA, k1)), 0.5f);
-                    const float2 h1 = cscale(cadd(chest(a, tB, k0), chest(a, tB, k1)), 0.5f);
-                    const float2 r0 = Yat(a, l, k0), r1 = Yat(a, l, k1);
-                    n0 = cadd(n0, cadd(cmul(cconj(h0), r0), cmul(h1, cconj(r1))));
-                    n1 = cadd(n1, cadd(cmul(make_float2(-h1.x, -h1.y), cconj(r0)), cmul(cconj(h0), r1)));
-                    den += cnorm(h0) + cnorm(h1);
-                }
-                x0 = cscale(n0, 1.0f / den);
-                x1 = cscale(n1, 1.0f / den);
-            }
-            for (uint32_t q = 0; q < (NT == 1 ? 1u : 2u); ++q) {
-                float L[8];
-                demap(q ? x1 : x0, N_bps, L);
-                const uint32_t base = (jj + q) * N_bps;
-                for (uint32_t b = 0; b < N_bps; ++b) {
-                    const float v = seq_bit(seq, base + b) ? -L[b] : L[b];
-                    llr[base + b] = q16(v);
-                }
-            }
-        }
-    };
-
-    for (uint32_t o = 0; o < A.n_ops; ++o) {
-        const rx_op op = A.ops[o];
-        if (op.kind == 1) {  // OP_DRS: zero-forcing (rx_synced.cpp:773-861)
-            const uint32_t meta = A.drs_meta[op.b];
-            const uint32_t tf = meta & 0xFFu, tlst = (meta >> 8) & 0xFFu, par = (meta >> 16) & 0xFFu;
-            const uint32_t l = op.a, rel = op.c, ps = op.d;
-            const uint32_t nts = tlst - tf + 1;
-            drs_off = 0;
-            for (uint32_t t = tf; t <= tlst; ++t) {  // channel_antenna.hpp:38-63 write offsets
-                const bool lhs = rel <= 1, hi = (t & 3u) >= 2;
-                const uint32_t off = (ps % 2 == 0) ? (lhs ? hi : !hi) : (lhs ? !hi : hi);
-                drs_off |= off << t;
-            }
-            for (uint32_t e = threadIdx.x; e < A.N_RX * nts * nd; e += blockDim.x) {
-                const uint32_t i = e % nd, t = tf + (e / nd) % nts, a = e / (nd * nts);
-                const uint32_t k = A.drs_k[((par * 4) + (t & 3u)) * nd + i];
-                const float2 v = cscale(Yat(a, l, k), A.drs_v[t * nd + i]);
-                zfi[(a * 4 + t) * 2 * nd + 2 * i + ((drs_off >> t) & 1u)] = v;
-            }
-            __syncthreads();
-            double s1 = 0.0, s2 = 0.0;  // estimator_snr.cpp:104-146
-            for (uint32_t e = threadIdx.x; e < A.N_RX * nts * nd; e += blockDim.x) {
-                const uint32_t i = e % nd, t = tf + (e / nd) % nts, a = e / (nd * nts);
-                const float2* z = zfi + (a * 4 + t) * 2 * nd + ((drs_off >> t) & 1u);
-                const float2 v = z[2 * i];
-                s1 += cnorm(v);
-                if (i + 1 < nd) s2 += cnorm(csub(v, z[2 * i + 2]));
-            }
-            sn += block_sum(s1, red);
-            nn += block_sum(s2, red) / 2.0;
-            sn_cnt += A.N_RX * nts * nd;
-            nn_cnt += A.N_RX * nts * (nd - 1);
-            // LUT pick: nearest profile SNR, ties to the later profile (rx_synced.cpp:863-891)
-            const float s = snr_db();
-            float best = fabsf(s - A.prof_snr[0]);
-            lut_pick = 0;
-            for (uint32_t i = 1; i < 3; ++i) {
-                const float d = fabsf(s - A.prof_snr[i]);
-                if (d <= best) {
-                    best = d;
-                    lut_pick = i;
-                }
-            }
-        } else if (op.kind == 2) {  // OP_EVENT
-            ev_mode = op.a;
-            ev_rel = op.b;
-            ev_swap = (op.c & 1u) ? 2u : 0u;
-            ev_lut = lut_pick;
-            ev_off = drs_off;
-        } else if (op.kind == 3) {  // OP_PCC
-            const uint32_t l = op.a;
-            cells(A.pcc_k, A.pcc_off[op.b], A.pcc_off[op.b + 1], 2, A.pcc_seq, [&](uint32_t) { return l; });
-        } else if (op.kind == 4) {  // OP_PDC: merge the run of PDC symbols sharing the current estimate
-            uint32_t o2 = o;
-            while (o2 + 1 < A.n_ops && A.ops[o2 + 1].kind == 4) ++o2;
-            const uint32_t l0 = op.a, l1 = A.ops[o2].a;
-            cells(A.pdc_k, A.pdc_off[l0], A.pdc_off[l1 + 1], A.N_bps, pdc_seq,
-                  [&](uint32_t j) { return static_cast<uint32_t>(A.pdc_sym[j]); });
-            o = o2;
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        if (A.is_pdc)
-            A.st[pkt].snr_pdc = snr_db();
-        else
-            A.st[pkt].snr_pcc = snr_db();
-    }
-}
-
-hipError_t launch_rx_back(const rx_back_args& a, uint32_t n, hipStream_t st) {
-    const size_t lds = size_t(a.N_RX) * 4 * a.n_drs * 2 * sizeof(float2);
-    hipLaunchKernelGGL(rx_back_kernel, dim3(n), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 

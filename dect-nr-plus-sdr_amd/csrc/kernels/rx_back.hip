@@ -1,0 +1,333 @@
+// RX back end of the synchronised receiver: channel estimation, equalisation, soft demapping.
+//
+//  rx_snr_kernel    one WG per packet: zero-forcing of every DRS symbol of the phase, SNR
+//                   accumulation (estimator_snr.cpp:104-146) and the SNR-driven Wiener LUT profile
+//                   pick after each DRS symbol (rx_synced.cpp:863-891). One wavefront per DRS
+//                   symbol; the accumulation itself is a short serial prefix.
+//  rx_cells_kernel  one WG per (packet, epoch): an epoch is a run of cell work over which the
+//                   interlaced pilot buffer (channel_antenna.hpp:38-63) does not change. The WG
+//                   rebuilds that buffer in LDS from the zero-forced DRS cells of Y, then every
+//                   thread takes whole work units (a cell for MRC, an SFBC pair for transmit
+//                   diversity): Wiener interpolation of the channel at the unit's subcarriers
+//                   (rx_synced.cpp:932-946), MRC (1204-1306) or SFBC combining (1335-1392),
+//                   srsRAN-style int16 soft demapping and descrambling (pcc_enc.cpp:297,
+//                   pdc_enc.cpp:339-344).
+// Y layout: [packet][N_RX][n_sym_total][Nf_pad] float2 (rx_fft_kernel).
+#include "device_common.hpp"
+#include "kernels.hpp"
+
+namespace dnrp::dev {
+
+__device__ __forceinline__ int16_t q16(float v) {
+    const float r = rintf(v);
+    return static_cast<int16_t>(fminf(32767.f, fmaxf(-32768.f, r)));
+}
+
+// srsRAN demod_soft restatement: LTE max-log per axis with int16 scale constants
+__device__ __forceinline__ void demap(float2 y, uint32_t N_bps, float* L) {
+    switch (N_bps) {
+        case 1:
+            L[0] = -100.f * (y.x + y.y);
+            break;
+        case 2:
+            L[0] = -100.f * y.x;
+            L[1] = -100.f * y.y;
+            break;
+        case 4: {
+            const float S = 400.f, yr = S * y.x, yi = S * y.y, o = 2.f * S * 0.31622776601683794f;
+            L[0] = -yr;
+            L[1] = -yi;
+            L[2] = fabsf(yr) - o;
+            L[3] = fabsf(yi) - o;
+            break;
+        }
+        case 6: {
+            const float S = 700.f, yr = S * y.x, yi = S * y.y, q = S * 0.15430334996209191f;
+            L[0] = -yr;
+            L[1] = -yi;
+            L[2] = fabsf(yr) - 4.f * q;
+            L[3] = fabsf(yi) - 4.f * q;
+            L[4] = fabsf(L[2]) - 2.f * q;
+            L[5] = fabsf(L[3]) - 2.f * q;
+            break;
+        }
+        default: {
+            const float S = 1000.f, yr = S * y.x, yi = S * y.y, q = S * 0.07669649888473704f;
+            L[0] = -yr;
+            L[1] = -yi;
+            L[2] = fabsf(yr) - 8.f * q;
+            L[3] = fabsf(yi) - 8.f * q;
+            L[4] = fabsf(L[2]) - 4.f * q;
+            L[5] = fabsf(L[3]) - 4.f * q;
+            L[6] = fabsf(L[4]) - 2.f * q;
+            L[7] = fabsf(L[5]) - 2.f * q;
+            break;
+        }
+    }
+}
+
+// demap + descramble + int16 of cell j (LLRs j*N_bps .. j*N_bps+N_bps-1)
+__device__ __forceinline__ void emit_cell(float2 x, uint32_t j, uint32_t N_bps, const uint8_t* __restrict__ seq,
+                                          int16_t* __restrict__ llr) {
+    float L[8];
+    demap(x, N_bps, L);
+    const uint32_t base = j * N_bps;
+    if (N_bps == 8) {  // one scrambling byte, one 16-B store
+        const uint32_t sb = seq[j];
+        uint32_t w[4];
+#pragma unroll
+        for (int b = 0; b < 8; b += 2) {
+            const float v0 = ((sb >> (7 - b)) & 1u) ? -L[b] : L[b];
+            const float v1 = ((sb >> (6 - b)) & 1u) ? -L[b + 1] : L[b + 1];
+            w[b / 2] = static_cast<uint16_t>(q16(v0)) | (static_cast<uint32_t>(static_cast<uint16_t>(q16(v1))) << 16);
+        }
+        int16_t* dst = llr + base;
+        if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+            *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                dst[2 * b] = static_cast<int16_t>(w[b] & 0xFFFFu);
+                dst[2 * b + 1] = static_cast<int16_t>(w[b] >> 16);
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) {
+        if (b < N_bps) {
+            const uint32_t i = base + b;
+            const uint32_t sbit = (seq[i >> 3] >> (7u - (i & 7u))) & 1u;
+            llr[i] = q16(sbit ? -L[b] : L[b]);
+        }
+    }
+}
+
+// ===================================================================== SNR chain
+constexpr uint32_t SNR_THREADS = 256, MAX_DOPS = 64;
+
+__global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
+    __shared__ double s1s[MAX_DOPS], s2s[MAX_DOPS];
+    const uint32_t pkt = blockIdx.x, nd = A.n_drs;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u, nw = SNR_THREADS / 64;
+    const float2* Yp = A.Y + size_t(pkt) * A.N_RX * A.n_sym_total * A.Nf_pad;
+    for (uint32_t d = wave; d < A.n_dops; d += nw) {
+        const uint32_t meta = A.dmeta[d], l = A.dl[d];
+        const uint32_t tf = meta & 0xFFu, tl = (meta >> 8) & 0xFFu, par = (meta >> 16) & 0xFFu, nts = tl - tf + 1;
+        double s1 = 0.0, s2 = 0.0;
+        for (uint32_t e = lane; e < A.N_RX * nts * nd; e += 64) {
+            const uint32_t i = e % nd, t = tf + (e / nd) % nts, a = e / (nd * nts);
+            const uint32_t* kb = A.drs_k + (par * 4 + (t & 3u)) * nd;
+            const float* vv = A.drs_v + t * nd;
+            const float2* row = Yp + (size_t(a) * A.n_sym_total + l) * A.Nf_pad;
+            const float2 v = cscale(row[kb[i]], vv[i]);
+            s1 += cnorm(v);
+            if (i + 1 < nd) s2 += cnorm(csub(v, cscale(row[kb[i + 1]], vv[i + 1])));
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            s1 += __shfl_xor(s1, o);
+            s2 += __shfl_xor(s2, o);
+        }
+        if (lane == 0) {
+            s1s[d] = s1;
+            s2s[d] = s2;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    rx_pkt_state* st = A.st + pkt;
+    double sn = st->snr_SN, nn = st->snr_N;
+    uint32_t sn_cnt = st->snr_SN_cnt, nn_cnt = st->snr_N_cnt;
+    auto snr_db = [&]() -> float {
+        if (sn <= 0.0 || nn <= 0.0) return 0.f;
+        const float Sa = static_cast<float>((sn - nn) / sn_cnt), Na = static_cast<float>(nn / nn_cnt);
+        return 10.f * log10f(Sa / Na);
+    };
+    for (uint32_t d = 0; d < A.n_dops; ++d) {
+        const uint32_t meta = A.dmeta[d];
+        const uint32_t nts = ((meta >> 8) & 0xFFu) - (meta & 0xFFu) + 1;
+        sn += s1s[d];
+        nn += s2s[d] / 2.0;
+        sn_cnt += A.N_RX * nts * nd;
+        nn_cnt += A.N_RX * nts * (nd - 1);
+        // nearest profile SNR, ties to the later profile (rx_synced.cpp:863-891)
+        const float s = snr_db();
+        float best = fabsf(s - A.prof_snr[0]);
+        uint32_t pick = 0;
+        for (uint32_t i = 1; i < 3; ++i) {
+            const float dd = fabsf(s - A.prof_snr[i]);
+            if (dd <= best) {
+                best = dd;
+                pick = i;
+            }
+        }
+        A.lut_d[size_t(pkt) * A.n_dops + d] = static_cast<uint8_t>(pick);
+    }
+    if (A.is_pdc)
+        st->snr_pdc = snr_db();
+    else
+        st->snr_pcc = snr_db();
+}
+
+hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st) {
+    if (a.n_dops > MAX_DOPS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rx_snr_kernel, dim3(n), dim3(SNR_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+// ===================================================================== cells
+constexpr uint32_t CELL_THREADS = 512;
+
+template <int NRX, int NT>
+__global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 zfi[];  // [NRX][NT][2 nd]
+    const uint32_t pkt = blockIdx.x / A.n_epochs, ep = blockIdx.x % A.n_epochs;
+    const rx_epoch E = A.epochs[ep];
+    const uint32_t nd = A.n_drs, Nf = A.N_occ + 1, nd2 = 2 * nd;
+    const float2* Yp = A.Y + size_t(pkt) * NRX * A.n_sym_total * A.Nf_pad;
+    auto Yat = [&](uint32_t a, uint32_t l, uint32_t k) { return Yp[(size_t(a) * A.n_sym_total + l) * A.Nf_pad + k]; };
+    // ---- pilot buffer of the epoch: zero-forced DRS cells at their interlace slots
+    for (uint32_t e = threadIdx.x; e < NRX * NT * nd2; e += CELL_THREADS) {
+        const uint32_t i = e % nd, o = (e / nd) & 1u, t = (e / nd2) % NT, a = e / (nd2 * NT);
+        const uint32_t src = A.epochs[ep].src[t][o];  // global: no dynamic register-array index
+        float2 v = make_float2(0.f, 0.f);
+        if (src != 0xFFFFu) {
+            const uint32_t par = (A.dmeta[src] >> 16) & 0xFFu;
+            const uint32_t k = A.drs_k[(par * 4 + (t & 3u)) * nd + i];
+            v = cscale(Yat(a, A.dl[src], k), A.drs_v[t * nd + i]);
+        }
+        zfi[(a * NT + t) * nd2 + 2 * i + o] = v;
+    }
+    __syncthreads();
+    const uint8_t* __restrict__ seq = A.is_pdc ? A.pdc_seq[pkt] : A.pcc_seq;
+    int16_t* __restrict__ llr = A.llr + size_t(pkt) * A.llr_stride;
+    const uint8_t* lutp = A.lut_d + size_t(pkt) * A.n_dops;
+    if (E.units == 0) return;
+    uint32_t si = E.seg0;
+    rx_seg S = A.segs[si];
+    uint32_t seg_end = si + 1 < E.seg1 ? A.segs[si + 1].u0 : E.units;
+    for (uint32_t u = threadIdx.x; u < E.units; u += CELL_THREADS) {
+        while (u >= seg_end) {
+            ++si;
+            S = A.segs[si];
+            seg_end = si + 1 < E.seg1 ? A.segs[si + 1].u0 : E.units;
+        }
+        const uint32_t lut = S.drs_cnt ? lutp[S.drs_cnt - 1] : 0u;
+        const uint32_t mode = S.mode;
+        const rx_lut LT = A.luts[mode * 3 + lut];
+        const uint32_t* __restrict__ pwt = LT.pw + size_t(S.rel) * 4 * Nf;
+        const float* __restrict__ wt = LT.w;
+        const uint32_t nI = LT.n;
+        const uint32_t step = mode ? 1u : 2u;
+        // interpolation weights and pilot start for stream t at subcarrier k
+        auto locate = [&](uint32_t t, uint32_t k, const float*& w, uint32_t& pos) {
+            const uint32_t pw = pwt[((t & 3u) ^ S.swap) * Nf + k];
+            w = wt + size_t(pw >> 16) * nI;
+            pos = pw & 0xFFFFu;
+            if (!mode) pos = 2 * pos + ((S.off >> t) & 1u);  // non-interlaced: latest DRS symbol only
+            pos += t * nd2;
+        };
+        if constexpr (NT == 1) {
+            const uint32_t jj = S.j0 + (u - S.u0);
+            const uint32_t k = A.kk[jj];
+            const uint32_t l = A.is_pdc ? static_cast<uint32_t>(A.pdc_sym[jj]) : S.l;
+            float2 r[NRX];
+#pragma unroll
+            for (int a = 0; a < NRX; ++a) r[a] = Yat(a, l, k);
+            const float* w;
+            uint32_t pos;
+            locate(0, k, w, pos);
+            float2 h[NRX];
+#pragma unroll
+            for (int a = 0; a < NRX; ++a) h[a] = make_float2(0.f, 0.f);
+            for (uint32_t i = 0; i < nI; ++i) {
+                const float wi = w[i];
+#pragma unroll
+                for (int a = 0; a < NRX; ++a) {
+                    const float2 z = zfi[a * NT * nd2 + pos + i * step];
+                    h[a].x = fmaf(z.x, wi, h[a].x);
+                    h[a].y = fmaf(z.y, wi, h[a].y);
+                }
+            }
+            float2 num = make_float2(0.f, 0.f);
+            float den = 0.f;
+#pragma unroll
+            for (int a = 0; a < NRX; ++a) {  // MRC (rx_synced.cpp:1204-1306)
+                num = cadd(num, cmulc(r[a], h[a]));
+                den += cnorm(h[a]);
+            }
+            emit_cell(cscale(num, 1.0f / den), jj, A.N_bps, seq, llr);
+        } else {
+            const uint32_t jj = S.j0 + 2 * (u - S.u0);
+            const uint32_t k0 = A.kk[jj], k1 = A.kk[jj + 1];
+            const uint32_t l = A.is_pdc ? static_cast<uint32_t>(A.pdc_sym[jj]) : S.l;
+            const uint32_t pr = A.pair[(jj >> 1) % A.mod];
+            const uint32_t tA = pr & 0xFu, tB = pr >> 4;
+            float2 r0[NRX], r1[NRX];
+#pragma unroll
+            for (int a = 0; a < NRX; ++a) {
+                r0[a] = Yat(a, l, k0);
+                r1[a] = Yat(a, l, k1);
+            }
+            const float* w[4];
+            uint32_t pos[4];
+            locate(tA, k0, w[0], pos[0]);
+            locate(tA, k1, w[1], pos[1]);
+            locate(tB, k0, w[2], pos[2]);
+            locate(tB, k1, w[3], pos[3]);
+            float2 h[NRX][4];
+#pragma unroll
+            for (int a = 0; a < NRX; ++a)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) h[a][c] = make_float2(0.f, 0.f);
+            for (uint32_t i = 0; i < nI; ++i) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float wi = w[c][i];
+                    const uint32_t p = pos[c] + i * step;
+#pragma unroll
+                    for (int a = 0; a < NRX; ++a) {
+                        const float2 z = zfi[a * NT * nd2 + p];
+                        h[a][c].x = fmaf(z.x, wi, h[a][c].x);
+                        h[a][c].y = fmaf(z.y, wi, h[a][c].y);
+                    }
+                }
+            }
+            float2 n0 = make_float2(0.f, 0.f), n1 = make_float2(0.f, 0.f);
+            float den = 0.f;
+#pragma unroll
+            for (int a = 0; a < NRX; ++a) {  // SFBC pair (rx_synced.cpp:1335-1392)
+                const float2 h0 = cscale(cadd(h[a][0], h[a][1]), 0.5f);
+                const float2 h1 = cscale(cadd(h[a][2], h[a][3]), 0.5f);
+                n0 = cadd(n0, cadd(cmul(cconj(h0), r0[a]), cmul(h1, cconj(r1[a]))));
+                n1 = cadd(n1, cadd(cmul(make_float2(-h1.x, -h1.y), cconj(r0[a])), cmul(cconj(h0), r1[a])));
+                den += cnorm(h0) + cnorm(h1);
+            }
+            emit_cell(cscale(n0, 1.0f / den), jj, A.N_bps, seq, llr);
+            emit_cell(cscale(n1, 1.0f / den), jj + 1, A.N_bps, seq, llr);
+        }
+    }
+}
+
+hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st) {
+    const size_t lds = size_t(a.N_RX) * a.NT * 2 * a.n_drs * sizeof(float2);
+    const dim3 g(n * a.n_epochs), b(CELL_THREADS);
+#define DNRP_CELLS(R, T)                                                                 \
+    if (a.N_RX == R && a.NT == T) {                                                      \
+        hipLaunchKernelGGL((rx_cells_kernel<R, T>), g, b, lds, st, a);                   \
+        return hipGetLastError();                                                        \
+    }
+    DNRP_CELLS(1, 1)
+    DNRP_CELLS(2, 1)
+    DNRP_CELLS(4, 1)
+    DNRP_CELLS(8, 1)
+    DNRP_CELLS(2, 2)
+    DNRP_CELLS(4, 2)
+    DNRP_CELLS(8, 2)
+    DNRP_CELLS(4, 4)
+    DNRP_CELLS(8, 4)
+#undef DNRP_CELLS
+    return hipErrorInvalidValue;
+}
+
+}  // namespace dnrp::dev
