@@ -142,6 +142,21 @@ std::vector<float2> constellation(uint32_t N_bps) {  // 3GPP TS 36.211 §7.1, in
     return t;
 }
 
+// input-major block taps for the register-blocked resampler (polyphase.hpp): rows i = 0..W-1 of
+// LP = 4*ceil(L/4) floats, g[i][k] = h[ph_k + (hl + o_k - i) * L] inside output k's FIR span
+std::vector<float> taps_polyphase(const geo::resampler_t& rs, uint32_t* count) {
+    const uint32_t L = rs.L, M = rs.M, hl = rs.hl;
+    const uint32_t W = hl + 1 + ((L - 1) * M) / L, lp = (L + 3) / 4 * 4;
+    std::vector<float> g(size_t(W) * lp, 0.0f);
+    for (uint32_t i = 0; i < W; ++i)
+        for (uint32_t k = 0; k < L; ++k) {
+            const int d = static_cast<int>(hl + (k * M) / L) - static_cast<int>(i);
+            if (d >= 0 && d <= static_cast<int>(hl)) g[i * lp + k] = rs.h[(k * M) % L + d * L];
+        }
+    *count = static_cast<uint32_t>(g.size());
+    return g;
+}
+
 double phasor_arg(double rad) {  // mixer_t::set_phase* builds float phasors (mixer.cpp:27-33)
     const float c = std::cos(static_cast<float>(rad)), s = std::sin(static_cast<float>(rad));
     return std::atan2(static_cast<double>(s), static_cast<double>(c));
@@ -172,9 +187,10 @@ struct tx_tables {
     geo::dims_t dm{};
     dev::fft_plan plan{};
     geo::resampler_t rs;
-    dbuf code, stf, W, taps, tw, qam, qpsk, pdc_off;
+    dbuf code, stf, W, taps, taps_pp, tw, qam, qpsk, pdc_off;
+    uint32_t npp = 0;  // floats in taps_pp
     std::vector<float> wscale;  // per codebook
-    uint32_t stage_bytes = 0;
+    std::vector<uint32_t> pdc_off_h;  // host copy of maps.pdc_sym_off
 };
 
 // device copy of a geo::rx_plan_t
@@ -196,7 +212,8 @@ struct rx1_tables {  // per (u, b, N_eff_TX): STF/PCC phase
     geo::resampler_t rs;
     geo::maps_t maps;
     uint32_t pcc_max = 0;
-    dbuf stf, tw, taps, drs_k, drs_v, pcc_k;
+    dbuf stf, tw, taps, taps_pp, drs_k, drs_v, pcc_k;
+    uint32_t npp = 0;  // floats in taps_pp
     rx_plan_dev bplan;  // PCC phase back end
     dbuf lut_pw[2][3], lut_w[2][3], luts;
     uint32_t lut_n[2][3] = {}, lut_T[2] = {};
@@ -311,15 +328,8 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         for (const auto& w : geo::W_matrix(t->tm.N_TS, t->tm.N_TX, cb, &s)) W.push_back(make_float2(w.real(), w.imag()));
         t->wscale.push_back(s);
     }
-    // LDS staging of the per-symbol PDC source bytes (8 bytes per thread of a 256-thread WG)
-    uint32_t mx = 0;
-    for (uint32_t l = 1; l <= t->q.N_DF_symb; ++l) {
-        const uint64_t b0 = uint64_t(m.pdc_sym_off[l]) * t->tm.N_SS * t->q.N_bps / 8;
-        const uint64_t b1 = (uint64_t(m.pdc_sym_off[l + 1]) * t->tm.N_SS * t->q.N_bps + 7) / 8 + 1;
-        mx = std::max<uint32_t>(mx, static_cast<uint32_t>(b1 - b0));
-    }
-    t->stage_bytes = mx <= 8 * 256 ? (mx + 3) / 4 * 4 : 0;
-    if (!t->code.upload(m.code) || !t->stf.upload(stf) || !t->pdc_off.upload(m.pdc_sym_off) || !t->W.upload(W) || !t->taps.upload(t->rs.h) ||
+    t->pdc_off_h = m.pdc_sym_off;
+    if (!t->code.upload(m.code) || !t->stf.upload(stf) || !t->pdc_off.upload(m.pdc_sym_off) || !t->W.upload(W) || !t->taps.upload(t->rs.h) || !t->taps_pp.upload(taps_polyphase(t->rs, &t->npp)) ||
         !t->tw.upload(twiddles(t->dm.Nd)) || !t->qam.upload(constellation(t->q.N_bps)) ||
         !t->qpsk.upload(constellation(2))) {
         *err = DNRP_ENOMEM;
@@ -365,7 +375,7 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
     std::vector<float2> stfv(t->maps.Nf);
     for (uint32_t k = 0; k < t->maps.Nf; ++k) stfv[k] = make_float2(t->maps.stf[k].real(), t->maps.stf[k].imag());
     const auto plan = geo::build_rx_plan(t->maps, pcc_ops, N_eff_TX);
-    bool ok = t->stf.upload(stfv) && t->tw.upload(twiddles(t->Nd)) && t->taps.upload(t->rs.h) &&
+    bool ok = t->stf.upload(stfv) && t->tw.upload(twiddles(t->Nd)) && t->taps.upload(t->rs.h) && t->taps_pp.upload(taps_polyphase(t->rs, &t->npp)) &&
               t->drs_k.upload(t->maps.drs_k) && t->drs_v.upload(t->maps.drs_v) && t->pcc_k.upload(t->maps.pcc_k) &&
               t->bplan.upload(plan);
     const uint32_t Nsv = N_eff_TX <= 2 ? 5 : 10;
@@ -445,6 +455,8 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t) {
     a.n_sym_total = ctx->rx_nsym_cap + 1;
     a.amp_scale = std::sqrt(static_cast<float>(t->N_occ)) / static_cast<float>(t->Nd);
     a.taps = t->taps.as<float>();
+    a.taps_pp = t->taps_pp.as<float>();
+    a.npp = t->npp;
     a.tw = t->tw.as<float2>();
     a.stf = t->stf.as<float2>();
     a.iq = reinterpret_cast<const float2*>(ctx->rx_iq);
@@ -631,18 +643,44 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     a.S = S;
     a.pdc_stride = pdc_stride;
     a.G = t->q.G;
-    // the ring holds one symbol's FIR windows (reaching back hl + M inputs before the symbol) plus the
-    // next symbol's samples, so resampling needs no barrier before the next CP write
-    a.ring = (t->rs.hl + t->rs.M + 2 * std::max(t->dm.STF_CP, t->dm.CP) + 2 * t->dm.Nd + 64 + 63) / 64 * 64;
+    // symbol runs (tx.hip): K symbols per WG plus the preceding symbol as resampler history
+    static const uint32_t K = [] {
+        const char* e = std::getenv("DNRP_TX_RUN");
+        const int k = e ? std::atoi(e) : 2;
+        return static_cast<uint32_t>(k >= 1 && k <= 3 ? k : 2);
+    }();
+    a.K = K;
+    a.dbg = std::getenv("DNRP_TX_DBG") ? static_cast<uint32_t>(std::atoi(std::getenv("DNRP_TX_DBG"))) : 0u;
+    a.n_runs = (t->q.N_DF_symb + 1 + K - 1) / K;
     a.m_star = 0;
     while ((t->rs.delay + a.m_star * t->rs.M) % t->rs.L) ++a.m_star;
     a.p_star = (t->rs.delay + a.m_star * t->rs.M) / t->rs.L;
-    a.stage_bytes = t->stage_bytes;
+    a.HP = 2 * (t->rs.hl + t->rs.M + 1);
+    {
+        const uint32_t len0 = t->dm.STF_CP + t->dm.Nd, lenD = t->dm.CP + t->dm.Nd;
+        auto bsym = [&](uint32_t l) { return l == 0 ? 0u : len0 + (l - 1) * lenD; };
+        const uint32_t bpc = t->tm.N_SS * t->q.N_bps;
+        uint32_t mx = 0, span = 0;
+        for (uint32_t r = 0; r < a.n_runs; ++r) {
+            const uint32_t lf = r * K, ll = std::min(lf + K, t->q.N_DF_symb + 1) - 1, s0 = std::max(lf, 1u) - 1;
+            span = std::max(span, bsym(ll + 1) - bsym(s0));
+            const uint64_t b0 = (uint64_t(t->pdc_off_h[std::max(s0, 1u)]) * bpc) >> 3;
+            const uint64_t b1 = ((uint64_t(t->pdc_off_h[ll + 1]) * bpc + 7) >> 3) + 1;
+            if (b1 > b0) mx = std::max<uint32_t>(mx, static_cast<uint32_t>(b1 - b0));
+        }
+        a.stage_bytes = mx <= 8192 ? (mx + 3) / 4 * 4 : 0;
+        a.lin_len = std::max(2 * a.HP + span, (K + 1) * t->dm.Nd);
+        // output staging reuses bufB + twiddles + constellation: size bufB for the longest run
+        const uint32_t max_out = static_cast<uint32_t>((uint64_t(span + t->rs.hl) * t->rs.L + t->rs.M - 1) / t->rs.M) + t->rs.L;
+        a.bufB_len = std::max((K + 1) * t->dm.Nd, max_out > t->dm.Nd + 256 ? max_out - t->dm.Nd - 256 : 0u);
+    }
     a.code = t->code.as<uint32_t>();
     a.pdc_off = t->pdc_off.as<uint32_t>();
     a.stf = t->stf.as<float2>();
     a.W = t->W.as<float2>();
     a.taps = t->taps.as<float>();
+    a.taps_pp = t->taps_pp.as<float>();
+    a.npp = t->npp;
     a.tw = t->tw.as<float2>();
     a.qam = t->qam.as<float2>();
     a.qpsk = t->qpsk.as<float2>();

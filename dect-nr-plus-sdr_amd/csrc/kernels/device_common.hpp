@@ -19,13 +19,13 @@ __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 __device__ __forceinline__ float cnorm(float2 a) { return a.x * a.x + a.y * a.y; }
 
-// exp(j*phi) for a double phase: exact range reduction in double, accurate sincos in float
+// exp(j*phi) for a double phase: exact reduction to revolutions in [-1/2, 1/2] in double, then the
+// hardware sin/cos (v_sin_f32 / v_cos_f32 take revolutions; ~1e-6 absolute error). No slow
+// large-argument path, so no register-hungry Payne-Hanek code next to the hot loops.
 __device__ __forceinline__ float2 phasor(double phi) {
-    const double twopi = 6.283185307179586476925286766559;
-    const double r = phi - twopi * rint(phi * 0.15915494309189533577);  // 1 / (2 pi)
-    float s, c;
-    sincosf(static_cast<float>(r), &s, &c);
-    return make_float2(c, s);
+    const double rev = phi * 0.15915494309189533577;  // 1 / (2 pi)
+    const float r = static_cast<float>(rev - rint(rev));
+    return make_float2(__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r));
 }
 
 // FFT plan passed by value: radix sequence (each 2, 3 or 4), product = N
@@ -191,6 +191,161 @@ template <int SIGN>
 __device__ __forceinline__ float2* fft_any(float2* x, float2* y, const float2* tw, const fft_plan& p, uint32_t nb = 1) {
     if ((p.N & (p.N - 1)) == 0) return fft_pow2<SIGN>(x, y, tw, 31u - __clz(p.N), nb);
     return fft_lds<SIGN>(x, y, tw, p, nb);
+}
+
+// Batched FFT whose last pass hands its outputs to store(b, n, v) (transform b, output index n)
+// instead of writing the ping-pong buffer, e.g. straight into a cyclic-prefixed time-domain layout.
+// The input must be in x; pass i reads x when i is even, so with fft_num_passes() = P the last pass
+// reads x iff P is odd: the caller places the input so that the store target is never read.
+__host__ __device__ inline uint32_t fft_num_passes(const fft_plan& p) {
+    if ((p.N & (p.N - 1)) == 0) {
+        uint32_t lg = 0;
+        while ((1u << lg) < p.N) ++lg;
+        return (lg + 1) / 2;
+    }
+    return p.nr;
+}
+
+template <int SIGN, class Store>
+__device__ void fft_store(float2* x_, float2* y_, const float2* tw, const fft_plan& p, uint32_t nb, Store store) {
+    const uint32_t N = p.N;
+    if ((N & (N - 1)) == 0) {
+        const uint32_t log2N = 31u - __clz(N);
+        uint32_t s = 0;
+        for (; s + 2 <= log2N; s += 2) {
+            const bool last = (s + 2 == log2N);
+            const uint32_t NR = N >> 2, kmask = (1u << s) - 1u, tsh = log2N - s - 2;
+            for (uint32_t jb = threadIdx.x; jb < nb * NR; jb += blockDim.x) {
+                const uint32_t j = jb & (NR - 1u), b = jb >> (log2N - 2), bo = b << log2N;
+                const float2* x = x_ + bo;
+                const uint32_t k = j & kmask;
+                const uint32_t od = ((j - k) << 2) + k;
+                float2 a0 = x[j], a1 = x[j + NR], a2 = x[j + 2 * NR], a3 = x[j + 3 * NR];
+                if (s) {
+                    const uint32_t e = k << tsh;
+                    float2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
+                    if (SIGN > 0) {
+                        w1 = cconj(w1);
+                        w2 = cconj(w2);
+                        w3 = cconj(w3);
+                    }
+                    a1 = cmul(a1, w1);
+                    a2 = cmul(a2, w2);
+                    a3 = cmul(a3, w3);
+                }
+                dft4<SIGN>(a0, a1, a2, a3);
+                if (last) {
+                    store(b, od, a0);
+                    store(b, od + (1u << s), a1);
+                    store(b, od + (2u << s), a2);
+                    store(b, od + (3u << s), a3);
+                } else {
+                    float2* y = y_ + bo;
+                    y[od] = a0;
+                    y[od + (1u << s)] = a1;
+                    y[od + (2u << s)] = a2;
+                    y[od + (3u << s)] = a3;
+                }
+            }
+            __syncthreads();
+            float2* t = x_;
+            x_ = y_;
+            y_ = t;
+        }
+        if (s < log2N) {  // final radix-2 pass
+            const uint32_t NR = N >> 1, kmask = (1u << s) - 1u;
+            for (uint32_t jb = threadIdx.x; jb < nb * NR; jb += blockDim.x) {
+                const uint32_t j = jb & (NR - 1u), b = jb >> (log2N - 1), bo = b << log2N;
+                const float2* x = x_ + bo;
+                const uint32_t k = j & kmask;
+                const uint32_t od = ((j - k) << 1) + k;
+                const float2 a0 = x[j];
+                float2 w = tw[k];
+                if (SIGN > 0) w = cconj(w);
+                const float2 a1 = cmul(x[j + NR], w);
+                store(b, od, cadd(a0, a1));
+                store(b, od + (1u << s), csub(a0, a1));
+            }
+            __syncthreads();
+        }
+        return;
+    }
+    uint32_t Ns = 1;
+    for (uint32_t s = 0; s < p.nr; ++s) {
+        const bool last = (s + 1 == p.nr);
+        const uint32_t R = p.radix[s];
+        const uint32_t NR = N / R;
+        const uint32_t tstep = N / (Ns * R);
+        for (uint32_t jb = threadIdx.x; jb < nb * NR; jb += blockDim.x) {
+            const uint32_t b = jb / NR, j = jb - b * NR;
+            const float2* x = x_ + b * N;
+            float2* y = y_ + b * N;
+            const uint32_t k = j % Ns;
+            const uint32_t od = (j / Ns) * Ns * R + k;
+            float2 o[4];
+            if (R == 4) {
+                float2 a0 = x[j], a1 = x[j + NR], a2 = x[j + 2 * NR], a3 = x[j + 3 * NR];
+                if (Ns > 1) {
+                    const uint32_t e = k * tstep;
+                    float2 w1 = tw[e % N], w2 = tw[(2 * e) % N], w3 = tw[(3 * e) % N];
+                    if (SIGN > 0) {
+                        w1 = cconj(w1);
+                        w2 = cconj(w2);
+                        w3 = cconj(w3);
+                    }
+                    a1 = cmul(a1, w1);
+                    a2 = cmul(a2, w2);
+                    a3 = cmul(a3, w3);
+                }
+                dft4<SIGN>(a0, a1, a2, a3);
+                o[0] = a0;
+                o[1] = a1;
+                o[2] = a2;
+                o[3] = a3;
+            } else if (R == 2) {
+                float2 a0 = x[j], a1 = x[j + NR];
+                if (Ns > 1) {
+                    float2 w1 = tw[(k * tstep) % N];
+                    if (SIGN > 0) w1 = cconj(w1);
+                    a1 = cmul(a1, w1);
+                }
+                o[0] = cadd(a0, a1);
+                o[1] = csub(a0, a1);
+            } else {
+                float2 a0 = x[j], a1 = x[j + NR], a2 = x[j + 2 * NR];
+                if (Ns > 1) {
+                    const uint32_t e = k * tstep;
+                    float2 w1 = tw[e % N], w2 = tw[(2 * e) % N];
+                    if (SIGN > 0) {
+                        w1 = cconj(w1);
+                        w2 = cconj(w2);
+                    }
+                    a1 = cmul(a1, w1);
+                    a2 = cmul(a2, w2);
+                }
+                const float c3 = -0.5f, s3 = SIGN * 0.86602540378443864676f;
+                const float2 sm = cadd(a1, a2), d = csub(a1, a2);
+                const float2 m = make_float2(a0.x + c3 * sm.x, a0.y + c3 * sm.y);
+                const float2 jd = make_float2(-s3 * d.y, s3 * d.x);
+                o[0] = cadd(a0, sm);
+                o[1] = cadd(m, jd);
+                o[2] = csub(m, jd);
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) {
+                if (r >= R) break;
+                if (last)
+                    store(b, od + r * Ns, o[r]);
+                else
+                    y[od + r * Ns] = o[r];
+            }
+        }
+        __syncthreads();
+        float2* t = x_;
+        x_ = y_;
+        y_ = t;
+        Ns *= R;
+    }
 }
 
 // block-wide sum of a double, result valid in all threads (blockDim.x multiple of 64, <= 1024)

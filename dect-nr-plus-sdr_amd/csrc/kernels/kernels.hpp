@@ -29,17 +29,22 @@ struct tx_args {
     fft_plan plan;  // IFFT size N_b_DFT_os
     uint32_t N_occ, off_lower, CP, STF_CP, N_DF, N_TS, N_TX, N_SS, N_bps, txdiv, mod, pattern_len;
     uint32_t L, M, delay, hl, n_keep, S, pdc_stride, G;
-    uint32_t ring;            // resampler input ring length (samples)
     uint32_t m_star, p_star;  // first phase-0 output (delay + m_star*M = p_star*L), polyphase.hpp
-    uint32_t stage_bytes;  // max PDC source bytes of one symbol staged in LDS (0: read global)
+    // symbol runs: WG (packet, antenna, run) synthesises symbols [run*K, run*K+K) plus the symbol
+    // before them (resampler history) into a linear cyclic-prefixed buffer of lin_len samples
+    uint32_t K, n_runs, HP, lin_len, bufB_len;
+    uint32_t stage_bytes;  // PDC source bytes of one run staged in LDS (0: read HBM directly)
+    uint32_t dbg;          // TEMP: section-skip mask for profiling
     uint32_t pair[12];     // transmit diversity TS pairs, A | B << 4
     const uint32_t* code;
     const uint32_t* pdc_off;  // [N_DF+2] first PDC cell of each symbol
     const float2* stf;
     const float2* W;     // [codebooks][N_TX][N_TS]
-    const float* taps;   // [(hl+1)*L]
-    const float2* tw;    // forward twiddles exp(-2 pi i j / N)
-    const float2* qam;   // constellation for N_bps
+    const float* taps;     // [(hl+1)*L]
+    const float* taps_pp;  // input-major block taps [W][LP] (polyphase.hpp)
+    uint32_t npp;          // floats in taps_pp
+    const float2* tw;      // forward twiddles exp(-2 pi i j / N)
+    const float2* qam;     // constellation for N_bps
     const float2* qpsk;  // QPSK table for the PCC
     const uint8_t* pcc_seq;
     const uint8_t* pcc_d;
@@ -74,6 +79,8 @@ struct rx_front_args {
     uint32_t sym_first, sym_count, sym_per_block, Nf_pad, n_sym_total;
     float amp_scale;           // sqrt(N_b_OCC) / N_b_DFT_os
     const float* taps;
+    const float* taps_pp;      // input-major block taps [W][LP] (polyphase.hpp)
+    uint32_t npp;              // floats in taps_pp
     const float2* tw;
     const float2* stf;         // STF values for (b, N_eff_TX)
     const float2* iq;          // [n][N_RX][S_in]

@@ -3,40 +3,45 @@
 // Output m of an L/M resampler with group delay D reads inputs p(m) - d, d = 0..HL, weighted by
 // h[ph(m) + d*L], where t = D + m*M, p = t / L, ph = t % L. For an "aligned" output m_b with
 // ph(m_b) = 0 the L outputs m_b .. m_b+L-1 have the compile-time phases (k*M) % L and newest inputs
-// p(m_b) + (k*M) / L. One thread therefore computes a whole block of L outputs from
-// W = HL + 1 + ((L-1)*M)/L inputs held in registers, with every tap index a compile-time constant:
-// the taps are uniform across the wavefront and are read once per block through the scalar
-// (constant) cache instead of per output through LDS. Aligned outputs are m_b = m_star + L*q,
-// whose newest input is p_star + M*q (no integer division on the device).
+// p(m_b) + (k*M) / L, so one thread computes a whole block of L outputs from the
+// W = HL + 1 + ((L-1)*M)/L window inputs starting at p(m_b) - HL.
+//
+// The loop runs input-major: window input i (one LDS read) updates all L accumulators with the
+// taps g[i][k] = h[ph_k + (HL + o_k - i) * L] (zero outside output k's FIR span), a [W][LP] table
+// in LDS that every lane reads at the same address (16-B broadcasts, LP = 4*ceil(L/4)). Live state
+// is L accumulators plus one input and one tap row, the loop is not unrolled across inputs, and
+// nothing can be hoisted into registers: small VGPR footprint whatever the filter length.
+// Aligned outputs are m_b = m_star + L*q, whose newest input is p_star + M*q.
 #pragma once
 
 #include "device_common.hpp"
 
 namespace dnrp::dev {
 
-typedef const __attribute__((address_space(4))) float* const_taps_t;
-
-__device__ __forceinline__ const_taps_t as_const_taps(const float* p) {
-    return (const_taps_t)(p);
-}
+typedef float v4f __attribute__((ext_vector_type(4)));
 
 template <int L, int M, int HL>
 struct pp_block {
-    static constexpr int W = HL + 1 + ((L - 1) * M) / L;  // inputs per block
+    static constexpr int W = HL + 1 + ((L - 1) * M) / L;  // window inputs per block
+    static constexpr int LP = (L + 3) / 4 * 4;             // padded tap row length
 
-    // x[i] = input p_b - HL + i; y[k] = output m_b + k (unmixed)
-    __device__ static __forceinline__ void run(const float2 (&x)[W], const_taps_t h, float2 (&y)[L]) {
+    // xw: LDS window (xw[i] = input p_b - HL + i); g: LDS taps [W][LP]; y[k] = output m_b + k
+    __device__ static __forceinline__ void run(const float2* xw, const float* g, float2 (&y)[L]) {
 #pragma unroll
-        for (int k = 0; k < L; ++k) {
-            const int ph = (k * M) % L, o = (k * M) / L;
-            float ar = 0.f, ai = 0.f;
+        for (int k = 0; k < L; ++k) y[k] = make_float2(0.f, 0.f);
+        const v4f* rows = reinterpret_cast<const v4f*>(g);
+#pragma unroll 2
+        for (int i = 0; i < W; ++i) {
+            const float2 xv = xw[i];
+            v4f t[LP / 4];
 #pragma unroll
-            for (int d = 0; d <= HL; ++d) {
-                const float t = h[ph + d * L];
-                ar = fmaf(x[HL + o - d].x, t, ar);
-                ai = fmaf(x[HL + o - d].y, t, ai);
+            for (int c = 0; c < LP / 4; ++c) t[c] = rows[i * (LP / 4) + c];
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const float tv = t[k / 4][k % 4];
+                y[k].x = fmaf(xv.x, tv, y[k].x);
+                y[k].y = fmaf(xv.y, tv, y[k].y);
             }
-            y[k] = make_float2(ar, ai);
         }
     }
 };

@@ -181,24 +181,15 @@ __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
 // ===================================================================== data-symbol FFTs
 // One WG per (packet, antenna, run of sym_per_block symbols); the symbols are processed in pairs
 // (RX_SYM_PASS): resampling of both into LDS, one batched FFT, bin extraction + STO derotation.
-// Register-blocked path (LR > 0): thread (s, j) computes the L outputs of aligned block j of symbol s
-// straight from HBM (its W-sample window, 16-B loads), taps on the scalar path (polyphase.hpp).
+// Register-blocked path (LR > 0): the hw-rate input span of the symbol pair is staged in LDS with
+// coalesced loads, then thread j computes the L outputs of aligned block j (polyphase.hpp).
 constexpr uint32_t RX_THREADS = 256;
-
-// xv[i] = src[i] with 16-B loads; OFF = 1 when src is 8 mod 16 (then src[-1] is read too)
-template <int W, int OFF>
-__device__ __forceinline__ void load_window(const float2* src, float2 (&xv)[W]) {
-    const float4* v4 = reinterpret_cast<const float4*>(src - OFF);
-    float4 t4[(W + OFF + 1) / 2];
-#pragma unroll
-    for (int i = 0; i < (W + OFF + 1) / 2; ++i) t4[i] = v4[i];
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        const int e = i + OFF;
-        xv[i] = (e & 1) ? make_float2(t4[e >> 1].z, t4[e >> 1].w) : make_float2(t4[e >> 1].x, t4[e >> 1].y);
-    }
-}
 constexpr uint32_t RX_SYM_PASS = 2;
+
+// LDS samples for one pass's input span (host and device agree on this bound)
+__host__ __device__ inline uint32_t rx_in_cap(uint32_t Nd, uint32_t CP, uint32_t L, uint32_t M, uint32_t W) {
+    return ((RX_SYM_PASS * (Nd + CP)) * M + L - 1) / L + W + 2 * M + 2 * L;
+}
 
 template <int LR, int MR, int HLR>
 __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
@@ -208,15 +199,19 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
     const uint32_t blk = blockIdx.x % nblk;
     const uint32_t a = (blockIdx.x / nblk) % A.N_RX;
     const uint32_t pkt = blockIdx.x / (nblk * A.N_RX);
+    using PB = pp_block<(LR > 0 ? LR : 1), (LR > 0 ? MR : 1), (LR > 0 ? HLR : 0)>;
     float2* fa = smem;                         // [RX_SYM_PASS][Nd]
     float2* fb = fa + RX_SYM_PASS * Nd;        // [RX_SYM_PASS][Nd]
     float2* twl = fb + RX_SYM_PASS * Nd;       // Nd
     float2* rot = twl + Nd;                    // Nf: STO derotation per subcarrier
-    float2* inbuf = rot + Nf;                  // generic path only
-    float* taps = reinterpret_cast<float*>(inbuf + (LR > 0 ? 0u : (Nd * A.M) / A.L + A.hl + 4));
+    float2* inbuf = rot + Nf;                  // input span of a pass
+    const uint32_t in_cap = LR > 0 ? rx_in_cap(Nd, A.CP, LR, MR, PB::W) : (Nd * A.M) / A.L + A.hl + 4;
+    float* taps = reinterpret_cast<float*>(inbuf + in_cap);
     for (uint32_t i = threadIdx.x; i < Nd; i += RX_THREADS) twl[i] = A.tw[i];
     if (LR == 0)
         for (uint32_t i = threadIdx.x; i < (A.hl + 1) * A.L; i += RX_THREADS) taps[i] = A.taps[i];
+    else
+        for (uint32_t i = threadIdx.x; i < A.npp; i += RX_THREADS) taps[i] = A.taps_pp[i];
     const rx_pkt_in in = A.pin[pkt];
     const rx_pkt_state S = A.st[pkt];
     const uint32_t n_stf = A.STF_CP + Nd;
@@ -228,48 +223,37 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
     const uint32_t l0 = A.sym_first + blk * A.sym_per_block;
     const uint32_t l1 = min(A.sym_first + A.sym_count, l0 + A.sym_per_block);
     // valid input window relative to the fine peak: history is zero before it (rx_synced.cpp:711-740)
-    const int64_t q_lo = 0, q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak;
+    const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak;
+    auto m_first = [&](uint32_t l) { return static_cast<int>(n_stf + (l - 1) * (A.CP + Nd) + A.CP); };
     for (uint32_t lp = l0; lp < l1; lp += RX_SYM_PASS) {
         const uint32_t ns = min(RX_SYM_PASS, l1 - lp);
         if constexpr (LR > 0) {
-            using PB = pp_block<LR, MR, HLR>;
-            const const_taps_t h = as_const_taps(A.taps);
-            constexpr uint32_t TPS = RX_THREADS / RX_SYM_PASS;  // threads per symbol
-            const uint32_t s = threadIdx.x / TPS;
-            if (s < ns) {
-                const uint32_t l = lp + s;
-                const int m0 = static_cast<int>(n_stf + (l - 1) * (A.CP + Nd) + A.CP);  // first output of symbol l
-                const int qb0 = (m0 - static_cast<int>(A.m_star)) / LR;                 // m0 >= m_star
-                const int qb1 = (m0 + static_cast<int>(Nd) - static_cast<int>(A.m_star) + LR - 1) / LR;
-                for (int q = qb0 + static_cast<int>(threadIdx.x % TPS); q < qb1; q += TPS) {
-                    const int mb = static_cast<int>(A.m_star) + LR * q;
-                    const int64_t qs = static_cast<int64_t>(A.p_star) + int64_t(MR) * q - HLR;  // first input
-                    float2 xv[PB::W];
-                    const float2* src = x + in.fine_peak + qs;
-                    if (qs - 1 >= q_lo && qs + PB::W + 1 <= q_hi) {
-                        if (reinterpret_cast<uintptr_t>(src) & 15u)
-                            load_window<PB::W, 1>(src, xv);
-                        else
-                            load_window<PB::W, 0>(src, xv);
-                    } else {
+            const int m_a = m_first(lp), m_b = m_first(lp + ns - 1) + static_cast<int>(Nd);
+            const int qb0 = (m_a - static_cast<int>(A.m_star)) / LR;  // m_a >= m_star
+            const int qb1 = (m_b - static_cast<int>(A.m_star) + LR - 1) / LR;
+            const int64_t in0 = static_cast<int64_t>(A.p_star) + int64_t(MR) * qb0 - HLR;
+            const uint32_t n_in = static_cast<uint32_t>(MR * (qb1 - 1 - qb0) + PB::W);
+            const float2* src = x + in.fine_peak + in0;
+            for (uint32_t i = threadIdx.x; i < n_in; i += RX_THREADS) {
+                const int64_t qi = in0 + i;
+                inbuf[i] = (qi >= 0 && qi < q_hi) ? src[i] : make_float2(0.f, 0.f);
+            }
+            __syncthreads();
+            for (int q = qb0 + static_cast<int>(threadIdx.x); q < qb1; q += RX_THREADS) {
+                const int mb = static_cast<int>(A.m_star) + LR * q;
+                // the symbol this block feeds (blocks in the CP gap feed none)
+                const uint32_t s = (ns > 1 && mb + LR > m_first(lp + 1)) ? 1u : 0u;
+                const int m0 = m_first(lp + s);
+                if (mb + LR <= m0 || mb >= m0 + static_cast<int>(Nd)) continue;
+                float2 y[LR];
+                PB::run(inbuf + MR * (q - qb0), taps, y);
+                float2 r = phasor(phi_stf + static_cast<double>(mb - static_cast<int>(n_stf)) * S.inc1);
+                float2* dst = fa + s * Nd;
 #pragma unroll
-                        for (int i = 0; i < PB::W; ++i) {
-                            const int64_t qi = qs + i;
-                            xv[i] = (qi >= q_lo && qi < q_hi) ? src[i] : make_float2(0.f, 0.f);
-                        }
-                    }
-                    float2 y[LR];
-                    const_taps_t hq = h;
-                    asm volatile("" : "+s"(hq));  // keep the tap loads inside the loop (SGPR budget)
-                    PB::run(xv, hq, y);
-                    float2 r = phasor(phi_stf + static_cast<double>(mb - static_cast<int>(n_stf)) * S.inc1);
-                    float2* dst = fa + s * Nd;
-#pragma unroll
-                    for (int k = 0; k < LR; ++k) {
-                        const uint32_t idx = static_cast<uint32_t>(mb + k - m0);
-                        if (idx < Nd) dst[idx] = cmul(y[k], r);
-                        r = cmul(r, step1);
-                    }
+                for (int k = 0; k < LR; ++k) {
+                    const uint32_t idx = static_cast<uint32_t>(mb + k - m0);
+                    if (idx < Nd) dst[idx] = cmul(y[k], r);
+                    r = cmul(r, step1);
                 }
             }
             __syncthreads();
@@ -312,15 +296,19 @@ hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
     const uint32_t Nd = a.plan.N;
     const uint32_t nblk = (a.sym_count + a.sym_per_block - 1) / a.sym_per_block;
     const dim3 g(n * a.N_RX * nblk), b(RX_THREADS);
-    const bool fast9 = a.L == 9 && a.M == 10 && (a.hl == 24 || a.hl == 4);
-    const size_t lds = ((2 * RX_SYM_PASS + 1) * size_t(Nd) + a.N_occ + 1) * sizeof(float2) +
-                       (fast9 ? 0 : ((Nd * a.M) / a.L + a.hl + 4) * sizeof(float2) + (a.hl + 1) * a.L * sizeof(float));
+    const size_t base = ((2 * RX_SYM_PASS + 1) * size_t(Nd) + a.N_occ + 1) * sizeof(float2);
+    auto fast = [&](auto kern, uint32_t W) {
+        const size_t lds = base + rx_in_cap(Nd, a.CP, a.L, a.M, W) * sizeof(float2) + a.npp * sizeof(float);
+        hipLaunchKernelGGL(kern, g, b, lds, st, a);
+    };
     if (a.L == 9 && a.M == 10 && a.hl == 24)  // os_min 1 (225 taps)
-        hipLaunchKernelGGL((rx_fft_kernel<9, 10, 24>), g, b, lds, st, a);
+        fast(rx_fft_kernel<9, 10, 24>, pp_block<9, 10, 24>::W);
     else if (a.L == 9 && a.M == 10 && a.hl == 4)  // os_min 2
-        hipLaunchKernelGGL((rx_fft_kernel<9, 10, 4>), g, b, lds, st, a);
+        fast(rx_fft_kernel<9, 10, 4>, pp_block<9, 10, 4>::W);
     else
-        hipLaunchKernelGGL((rx_fft_kernel<0, 0, 0>), g, b, lds, st, a);
+        hipLaunchKernelGGL((rx_fft_kernel<0, 0, 0>), g, b,
+                           base + ((Nd * a.M) / a.L + a.hl + 4) * sizeof(float2) + (a.hl + 1) * a.L * sizeof(float), st,
+                           a);
     return hipGetLastError();
 }
 
