@@ -587,6 +587,23 @@ int dnrp_get_packet_sizes(const dnrp_ctx* ctx, const dnrp_psdef* d, dnrp_packet_
     return DNRP_OK;
 }
 
+int dnrp_compute_packet_sizes(const dnrp_cfg* cfg, const dnrp_psdef* d, dnrp_packet_sizes* out) {
+    if (!d || !out) return DNRP_EINVAL;
+    dnrp_packet_sizes q;
+    if (!geo::packet_sizes(*d, q)) return DNRP_ECONFIG;
+    q.N_b_DFT_os = q.N_samples_packet_no_GI_os_rs = q.N_samples_packet_os_rs = 0;
+    if (cfg) {
+        if (cfg->L == 0 || cfg->M == 0 || cfg->os_min == 0 || d->u > cfg->u_max || d->b > cfg->b_max)
+            return DNRP_EINVAL;
+        const auto dm = geo::make_dims(*cfg, *d, q);
+        q.N_b_DFT_os = dm.Nd;
+        q.N_samples_packet_no_GI_os_rs = dm.N_no_GI_rs;
+        q.N_samples_packet_os_rs = dm.N_packet_rs;
+    }
+    *out = q;
+    return DNRP_OK;
+}
+
 int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp_tx_desc* desc, const uint8_t* pcc_d,
                   const uint8_t* pdc_d, uint32_t pdc_stride, float* iq_out, uint32_t S, void* stream) {
     if (!ctx || !psdef || (n > 0 && (!desc || !pcc_d || !pdc_d || !iq_out))) return DNRP_EINVAL;

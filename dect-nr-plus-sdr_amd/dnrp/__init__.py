@@ -75,7 +75,8 @@ class PdcReq(C.Structure):
     _fields_ = [("network_id", C.c_uint32), ("plcf_type", C.c_uint32)]
 
 
-EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_get_packet_sizes", "dnrp_tx_batch",
+EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_get_packet_sizes",
+           "dnrp_compute_packet_sizes", "dnrp_tx_batch",
            "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_kernel_time_total", "dnrp_strerror"]
 
 _lib = None
@@ -92,6 +93,7 @@ def lib():
         L.dnrp_ctx_destroy.argtypes = [P]
         L.dnrp_add_network_id.argtypes = [P, C.c_uint32]
         L.dnrp_get_packet_sizes.argtypes = [P, C.POINTER(PsDef), C.POINTER(PacketSizes)]
+        L.dnrp_compute_packet_sizes.argtypes = [C.POINTER(Cfg), C.POINTER(PsDef), C.POINTER(PacketSizes)]
         L.dnrp_tx_batch.argtypes = [P, C.POINTER(PsDef), C.c_uint32, C.POINTER(TxDesc), P, P, C.c_uint32, P,
                                     C.c_uint32, P]
         L.dnrp_rx_pcc_batch.argtypes = [P, C.c_uint32, C.POINTER(SyncReport), P, C.c_uint32, P,
@@ -118,6 +120,16 @@ def _chk(rc, what):
 
 def psdef(u, b, plt, pl, tm, mcs, Z=6144):
     return PsDef(u, b, plt, pl, tm, mcs, Z)
+
+
+def compute_packet_sizes(ps, u_max=None, b_max=None, os_min=1, L=10, M=9):
+    """Context-free packet geometry (host only). With u_max/b_max the oversampled fields are set."""
+    out = PacketSizes()
+    cfg = Cfg(u_max, b_max, 1, os_min, L, M, 1, 2, 1, 0) if u_max else None
+    rc = lib().dnrp_compute_packet_sizes(C.byref(cfg) if cfg else None, C.byref(ps), C.byref(out))
+    if rc != 0:
+        raise DnrpError(rc, "dnrp_compute_packet_sizes")
+    return out.as_dict()
 
 
 def _stream_ptr(stream):

@@ -11,6 +11,7 @@
  *   dnrp_add_network_id    <- tx_rx_t::add_new_network_id (lib/include/dectnrp/phy/tx_rx.hpp:52,
  *                             sections_part3/scrambling_pdc.cpp:36-57)
  *   dnrp_get_packet_sizes  <- sp3::get_packet_sizes (sections_part3/derivative/packet_sizes.cpp:99)
+ *   dnrp_compute_packet_sizes  (same, context-free and host-only)
  *   dnrp_tx_batch          <- tx_t::generate_tx_packet (lib/include/dectnrp/phy/tx/tx.hpp:80-81,
  *                             lib/src/phy/tx/tx.cpp:165-314), FEC boundary between rate matching
  *                             and scrambling (pcc_enc.cpp:212, pdc_enc.cpp:218-221)
@@ -123,6 +124,11 @@ int dnrp_ctx_create(const dnrp_cfg* cfg, dnrp_ctx** out);
 int dnrp_ctx_destroy(dnrp_ctx* ctx);
 int dnrp_add_network_id(dnrp_ctx* ctx, uint32_t network_id);
 int dnrp_get_packet_sizes(const dnrp_ctx* ctx, const dnrp_psdef* psdef, dnrp_packet_sizes* out);
+/* Same as dnrp_get_packet_sizes without a context or device: the reference's static
+ * sp3::get_packet_sizes (sections_part3/derivative/packet_sizes.cpp:99-236). The oversampled /
+ * resampled fields (N_b_DFT_os, N_samples_packet_*_os_rs) are filled from cfg when cfg is not
+ * NULL (tx.cpp:429-600 geometry), else 0. Host-only: safe on machines without a GPU. */
+int dnrp_compute_packet_sizes(const dnrp_cfg* cfg, const dnrp_psdef* psdef, dnrp_packet_sizes* out);
 
 /*
  * TX: n packets of one configuration.

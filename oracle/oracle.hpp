@@ -62,6 +62,7 @@ mcs_t get_mcs(uint32_t index);
 uint32_t get_N_TB_bits(uint32_t N_SS, uint32_t N_PDC_subc, uint32_t N_bps, uint32_t Rn,
                        uint32_t Rd, uint32_t Z);
 bool get_packet_sizes(const psdef_t& d, packet_sizes_t& q);
+void special_values(float z, float* out5);
 
 // ---------------------------------------------------------------- geometry tables
 // Transmit-stream vector index i in [0, N_b_OCC] maps to subcarrier k = i - N_b_OCC/2.

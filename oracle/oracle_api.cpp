@@ -44,6 +44,60 @@ int oracle_packet_sizes(const uint32_t* psdef, uint32_t* out) {
     }
 }
 
+// ---- table pins against tests/golden/ref_tables.json (reference-compiled fixture)
+// out: u, b, delta_u_f, N_SLOT_u_symb, N_SLOT_u_subslot, N_b_DFT, N_b_CP, N_b_OCC, N_guards_top,
+//      N_guards_bottom; T_u_symb in *T
+int oracle_numerology(uint32_t u, uint32_t b, uint32_t* out, double* T) {
+    try {
+        const auto q = get_numerology(u, b);
+        const uint32_t v[] = {q.u, q.b, q.delta_u_f, q.N_SLOT_u_symb, q.N_SLOT_u_subslot, q.N_b_DFT, q.N_b_CP,
+                              q.N_b_OCC, q.N_guards_top, q.N_guards_bottom};
+        std::memcpy(out, v, sizeof(v));
+        *T = q.T_u_symb;
+        return 0;
+    } catch (...) {
+        return -2;
+    }
+}
+
+// out: index, N_eff_TX, N_SS, cl, N_TS, N_TX
+int oracle_tm_mode(uint32_t index, uint32_t* out) {
+    try {
+        const auto t = get_tm_mode(index);
+        const uint32_t v[] = {t.index, t.N_eff_TX, t.N_SS, t.cl ? 1u : 0u, t.N_TS, t.N_TX};
+        std::memcpy(out, v, sizeof(v));
+        return 0;
+    } catch (...) {
+        return -2;
+    }
+}
+
+// out: index, N_bps, R_numerator, R_denominator
+int oracle_mcs(uint32_t index, uint32_t* out) {
+    try {
+        const auto m = get_mcs(index);
+        const uint32_t v[] = {m.index, m.N_bps, m.R_num, m.R_den};
+        std::memcpy(out, v, sizeof(v));
+        return 0;
+    } catch (...) {
+        return -2;
+    }
+}
+
+uint32_t oracle_tbs(uint32_t N_SS, uint32_t N_PDC_subc, uint32_t mcs, uint32_t Z) {
+    const auto m = get_mcs(mcs);
+    return get_N_TB_bits(N_SS, N_PDC_subc, m.N_bps, m.R_num, m.R_den, Z);
+}
+
+int oracle_k_b_occ(uint32_t b, int32_t* out, uint32_t cap) {
+    const auto k = k_b_OCC(b);
+    if (k.size() > cap) return -1;
+    for (size_t i = 0; i < k.size(); ++i) out[i] = k[i];
+    return static_cast<int>(k.size());
+}
+
+void oracle_special(float z, float* out5) { special_values(z, out5); }
+
 // out: N_b_DFT_os, off_lower, CP_os, STF_CP_os, N_no_GI_os, N_no_GI_os_rs, N_packet_os_rs
 int oracle_dims(const uint32_t* cfg, const uint32_t* psdef, uint32_t* out) {
     try {

@@ -555,6 +555,16 @@ static float sinc_f(float n) {
     return (n == 0.0f) ? 1.0f : static_cast<float>(std::sin(M_PI * n) / (M_PI * n));
 }
 
+// J0(z), I0(z), sinc(z - 2), r_f_uni(1 us, z * 27 kHz), r_t_jakes(500 Hz, z * 5.2083 us): the sample
+// points of tests/golden/ref_tables.json "special" (channel_statistics.cpp:27-33 in float)
+void special_values(float z, float* out) {
+    out[0] = bessel_J0(z);
+    out[1] = bessel_I0(z);
+    out[2] = sinc_f(z - 2.0f);
+    out[3] = sinc_f(static_cast<float>(M_PI) * 1.0e-6f * (z * 27000.0f));
+    out[4] = bessel_J0(2.0f * static_cast<float>(M_PI) * 500.0f * (z * 5.2083e-6f));
+}
+
 std::vector<float> kaiser(float f_pass, float f_stop, float ripple_dB, float att_dB, float fs,
                           bool force_odd) {
     const float d0 = std::pow(10.0f, -att_dB / 20.0f);

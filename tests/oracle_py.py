@@ -47,6 +47,14 @@ def lib():
                                 C.c_uint32, I16P, I16P, C.c_void_p, C.c_void_p, F32P, C.c_int]
         L.oracle_loopback_timed.argtypes = [U32P, U32P, C.c_uint32, C.c_uint32, C.c_uint64]
         L.oracle_loopback_timed.restype = C.c_double
+        L.oracle_numerology.argtypes = [C.c_uint32, C.c_uint32, U32P, C.POINTER(C.c_double)]
+        L.oracle_tm_mode.argtypes = [C.c_uint32, U32P]
+        L.oracle_mcs.argtypes = [C.c_uint32, U32P]
+        L.oracle_tbs.argtypes = [C.c_uint32] * 4
+        L.oracle_tbs.restype = C.c_uint32
+        L.oracle_k_b_occ.argtypes = [C.c_uint32, np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS"),
+                                     C.c_uint32]
+        L.oracle_special.argtypes = [C.c_float, F32P]
         _lib = L
     return _lib
 
@@ -120,3 +128,46 @@ def loopback_timed(cf, ps, n_packets, n_threads, seed=0xDEC7):
 
 def pack_bits(bits):
     return np.packbits(np.asarray(bits, dtype=np.uint8))
+
+
+# ---- reference-table restatements (pinned by tests/golden/ref_tables.json)
+def numerology(u, b):
+    out = np.zeros(10, np.uint32)
+    T = C.c_double()
+    if lib().oracle_numerology(u, b, out, C.byref(T)) != 0:
+        raise ValueError((u, b))
+    keys = ["u", "b", "delta_u_f", "N_SLOT_u_symb", "N_SLOT_u_subslot", "N_b_DFT", "N_b_CP", "N_b_OCC",
+            "N_guards_top", "N_guards_bottom"]
+    d = {k: int(v) for k, v in zip(keys, out)}
+    d["T_u_symb"] = T.value
+    return d
+
+
+def tm_mode(i):
+    out = np.zeros(6, np.uint32)
+    if lib().oracle_tm_mode(i, out) != 0:
+        raise ValueError(i)
+    return dict(zip(["index", "N_eff_TX", "N_SS", "cl", "N_TS", "N_TX"], map(int, out)))
+
+
+def mcs(i):
+    out = np.zeros(4, np.uint32)
+    if lib().oracle_mcs(i, out) != 0:
+        raise ValueError(i)
+    return dict(zip(["index", "N_bps", "R_num", "R_den"], map(int, out)))
+
+
+def tbs(N_SS, N_PDC, mcs_index, Z):
+    return int(lib().oracle_tbs(N_SS, N_PDC, mcs_index, Z))
+
+
+def k_b_occ(b):
+    out = np.zeros(1024, np.int32)
+    n = lib().oracle_k_b_occ(b, out, out.size)
+    return out[:n].tolist()
+
+
+def special(z):
+    out = np.zeros(5, np.float32)
+    lib().oracle_special(np.float32(z), out)
+    return out
