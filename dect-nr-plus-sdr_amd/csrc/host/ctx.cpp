@@ -329,7 +329,27 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         t->wscale.push_back(s);
     }
     t->pdc_off_h = m.pdc_sym_off;
-    if (!t->code.upload(m.code) || !t->stf.upload(stf) || !t->pdc_off.upload(m.pdc_sym_off) || !t->W.upload(W) || !t->taps.upload(t->rs.h) || !t->taps_pp.upload(taps_polyphase(t->rs, &t->npp)) ||
+    // transmit diversity pair index per PCC/PDC cell into the code words (kernels.hpp CODE_*)
+    std::vector<uint32_t> code = m.code;
+    {
+        uint32_t pair[12], mod = 1;
+        fill_pairs(t->tm.N_TS, pair, mod);
+        for (auto& c : code) {
+            const uint32_t ty = c & dev::CODE_MASK;
+            if (ty != dev::CODE_PCC && ty != dev::CODE_PDC) continue;
+            const uint32_t j = c & ~dev::CODE_MASK;
+            if (j > dev::CODE_J_MASK) {
+                *err = DNRP_EUNSUPPORTED;
+                return nullptr;
+            }
+            c = ty | j | (((j >> 1) % mod) << dev::CODE_PAIR_SHIFT);
+        }
+    }
+    if (uint64_t(t->dm.N_packet_rs + 2 * t->rs.hl) * t->rs.L >= (1ull << 32)) {  // 32-bit output indexing
+        *err = DNRP_EUNSUPPORTED;
+        return nullptr;
+    }
+    if (!t->code.upload(code) || !t->stf.upload(stf) || !t->pdc_off.upload(m.pdc_sym_off) || !t->W.upload(W) || !t->taps.upload(t->rs.h) || !t->taps_pp.upload(taps_polyphase(t->rs, &t->npp)) ||
         !t->tw.upload(twiddles(t->dm.Nd)) || !t->qam.upload(constellation(t->q.N_bps)) ||
         !t->qpsk.upload(constellation(2))) {
         *err = DNRP_ENOMEM;
@@ -661,11 +681,12 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     a.pdc_stride = pdc_stride;
     a.G = t->q.G;
     // symbol runs (tx.hip): K symbols per WG plus the preceding symbol as resampler history
-    static const uint32_t K = [] {
+    // 1024-point symbols: one wavefront per symbol, 3 symbols + history fill the 4-wave workgroup
+    static const int K_env = [] {
         const char* e = std::getenv("DNRP_TX_RUN");
-        const int k = e ? std::atoi(e) : 2;
-        return static_cast<uint32_t>(k >= 1 && k <= 3 ? k : 2);
+        return e ? std::atoi(e) : 0;
     }();
+    const uint32_t K = (K_env >= 1 && K_env <= 3) ? static_cast<uint32_t>(K_env) : (t->dm.Nd == 1024 ? 3u : 2u);
     a.K = K;
     a.dbg = std::getenv("DNRP_TX_DBG") ? static_cast<uint32_t>(std::atoi(std::getenv("DNRP_TX_DBG"))) : 0u;
     a.n_runs = (t->q.N_DF_symb + 1 + K - 1) / K;

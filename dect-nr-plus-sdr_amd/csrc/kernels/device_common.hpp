@@ -348,6 +348,97 @@ __device__ void fft_store(float2* x_, float2* y_, const float2* tw, const fft_pl
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// One-wavefront 1024-point FFT (N_b_DFT_os = 1024: u,b = 8,16 / 4,16 / ... at os 1).
+// Lane t holds v[m] = x[t + 64 m] on entry and v[m] = X[t + 64 m] on exit. Stockham passes
+// radix 16 (Ns = 1), radix 16 (Ns = 16) and radix 4 (Ns = 256, four butterflies per lane): the
+// first pass starts from registers, two exchanges go through the wave's own LDS buffer xb
+// (>= 1088 float2, index padded i + i/16: conflict-free b64 writes, <= 2-way reads), no workgroup
+// barrier. tw: forward twiddles exp(-2 pi i j / 1024) (LDS or global).
+constexpr uint32_t WFFT_XB = 1024 + 64;
+
+__device__ __forceinline__ uint32_t wfft_pad(uint32_t i) { return i + (i >> 4); }
+
+template <int SIGN>
+__device__ __forceinline__ float2 wfft_tw(const float2* tw, uint32_t e) {
+    const float2 w = tw[e];
+    return SIGN > 0 ? cconj(w) : w;
+}
+
+// X[k1 + 4 k2] = sum_r x[r] W16^(r k), r = c + 4 a (decimation in time, twiddles W16^(c k1))
+template <int SIGN>
+__device__ __forceinline__ void dft16(float2 (&v)[16]) {
+    constexpr float C1 = 0.92387953251128675613f, S1 = 0.38268343236508977173f, R2 = 0.70710678118654752440f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dft4<SIGN>(v[c], v[c + 4], v[c + 8], v[c + 12]);  // A[c][k1] at v[c + 4 k1]
+    // W16^(c k1), SIGN-signed angle 2 pi c k1 / 16
+    auto rot = [](float2 a, float cs, float sn) {  // a * (cs + SIGN*j*sn)
+        const float s = SIGN * sn;
+        return make_float2(a.x * cs - a.y * s, a.x * s + a.y * cs);
+    };
+    v[1 + 4 * 1] = rot(v[1 + 4 * 1], C1, S1);
+    v[1 + 4 * 2] = rot(v[1 + 4 * 2], R2, R2);
+    v[1 + 4 * 3] = rot(v[1 + 4 * 3], S1, C1);
+    v[2 + 4 * 1] = rot(v[2 + 4 * 1], R2, R2);
+    v[2 + 4 * 2] = rot(v[2 + 4 * 2], 0.f, 1.f);
+    v[2 + 4 * 3] = rot(v[2 + 4 * 3], -R2, R2);
+    v[3 + 4 * 1] = rot(v[3 + 4 * 1], S1, C1);
+    v[3 + 4 * 2] = rot(v[3 + 4 * 2], -R2, R2);
+    v[3 + 4 * 3] = rot(v[3 + 4 * 3], -C1, -S1);
+    float2 o[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+        float2 a0 = v[4 * k1], a1 = v[4 * k1 + 1], a2 = v[4 * k1 + 2], a3 = v[4 * k1 + 3];
+        dft4<SIGN>(a0, a1, a2, a3);  // over c -> k2
+        o[k1] = a0;
+        o[k1 + 4] = a1;
+        o[k1 + 8] = a2;
+        o[k1 + 12] = a3;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = o[k];
+}
+
+template <int SIGN>
+__device__ __forceinline__ void wave_fft1024(float2 (&v)[16], float2* xb, const float2* tw, uint32_t lane) {
+    // pass 1: radix 16, Ns = 1, butterfly j = lane on x[j + 64 r] -> y[16 j + k]
+    dft16<SIGN>(v);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xb[wfft_pad(16 * lane + k)] = v[k];
+    __builtin_amdgcn_wave_barrier();
+    // pass 2: radix 16, Ns = 16: reads y[j + 64 r], twiddle W256^(r kk), writes z[(j/16) 256 + kk + 16 k]
+    const uint32_t kk = lane & 15u;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = xb[wfft_pad(lane + 64 * r)];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], wfft_tw<SIGN>(tw, 4 * r * kk));
+    dft16<SIGN>(v);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t zb = (lane >> 4) * 256 + kk;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xb[wfft_pad(zb + 16 * k)] = v[k];
+    __builtin_amdgcn_wave_barrier();
+    // pass 3: radix 4, Ns = 256: butterflies j = lane + 64 b read z[j + 256 r], twiddle W1024^(r j),
+    // write X[j + 256 r] = X[lane + 64 (b + 4 r)] -> v[b + 4 r]
+    float2 o[16];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t j = lane + 64 * b;
+        float2 a0 = xb[wfft_pad(j)], a1 = xb[wfft_pad(j + 256)], a2 = xb[wfft_pad(j + 512)], a3 = xb[wfft_pad(j + 768)];
+        a1 = cmul(a1, wfft_tw<SIGN>(tw, j));
+        a2 = cmul(a2, wfft_tw<SIGN>(tw, 2 * j));
+        a3 = cmul(a3, wfft_tw<SIGN>(tw, 3 * j));
+        dft4<SIGN>(a0, a1, a2, a3);
+        o[b] = a0;
+        o[b + 4] = a1;
+        o[b + 8] = a2;
+        o[b + 12] = a3;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = o[m];
+}
+
 // block-wide sum of a double, result valid in all threads (blockDim.x multiple of 64, <= 1024)
 __device__ __forceinline__ double block_sum(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

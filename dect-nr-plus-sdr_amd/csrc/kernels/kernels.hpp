@@ -9,7 +9,11 @@
 
 namespace dnrp::dev {
 
+// TX cell codes: type in bits 29-31; PCC/PDC: cell index j in bits 0-19 and the transmit
+// diversity pair index ((j >> 1) % mod) in bits 20-23 (host-precomputed); DRS: stream | sign << 3
 enum : uint32_t {
+    CODE_J_MASK = 0xFFFFFu,
+    CODE_PAIR_SHIFT = 20,
     CODE_PCC = 1u << 29,
     CODE_PDC = 2u << 29,
     CODE_DRS = 3u << 29,
