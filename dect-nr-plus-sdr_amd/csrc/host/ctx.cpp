@@ -681,12 +681,12 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     a.pdc_stride = pdc_stride;
     a.G = t->q.G;
     // symbol runs (tx.hip): K symbols per WG plus the preceding symbol as resampler history
-    // 1024-point symbols: one wavefront per symbol, 3 symbols + history fill the 4-wave workgroup
+    // K = 2 symbols + history per workgroup (measured faster than 3 + history on the 4-wave groups)
     static const int K_env = [] {
         const char* e = std::getenv("DNRP_TX_RUN");
         return e ? std::atoi(e) : 0;
     }();
-    const uint32_t K = (K_env >= 1 && K_env <= 3) ? static_cast<uint32_t>(K_env) : (t->dm.Nd == 1024 ? 3u : 2u);
+    const uint32_t K = (K_env >= 1 && K_env <= 3) ? static_cast<uint32_t>(K_env) : 2u;
     a.K = K;
     a.dbg = std::getenv("DNRP_TX_DBG") ? static_cast<uint32_t>(std::atoi(std::getenv("DNRP_TX_DBG"))) : 0u;
     a.n_runs = (t->q.N_DF_symb + 1 + K - 1) / K;

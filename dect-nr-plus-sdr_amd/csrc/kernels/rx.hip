@@ -292,6 +292,112 @@ hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ---- N_b_DFT_os = 1024: one wavefront per symbol, no workgroup barrier after the table load.
+// The wave stages its symbol's hw-rate input span in its own LDS region, resamples it with the
+// register-blocked polyphase blocks (outputs kept in registers), writes the 1024 outputs back into
+// the same region as FFT input, runs wave_fft1024 there, and stores the occupied bins, amplitude
+// scaled and STO-derotated, straight to Y.
+constexpr uint32_t RXW_SYMS = 4;  // symbols (= wavefronts) per workgroup
+
+__host__ __device__ inline uint32_t rxw_region(uint32_t L, uint32_t M, uint32_t W) {
+    const uint32_t n_in = ((1024 + 2 * L) * M) / L + W + M;  // one symbol's input span, upper bound
+    const uint32_t r = n_in > WFFT_XB ? n_in : WFFT_XB;
+    return (r + 15) / 16 * 16;
+}
+
+template <int LR, int MR, int HLR>
+__global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    using PB = pp_block<LR, MR, HLR>;
+    constexpr uint32_t Nd = 1024;
+    constexpr int BR = (Nd + 2 * LR) / LR / 64 + 1;  // block rounds per lane
+    const uint32_t N = A.N_occ;
+    const uint32_t nblk = (A.sym_count + RXW_SYMS - 1) / RXW_SYMS;
+    const uint32_t blk = blockIdx.x % nblk;
+    const uint32_t a = (blockIdx.x / nblk) % A.N_RX;
+    const uint32_t pkt = blockIdx.x / (nblk * A.N_RX);
+    const uint32_t region = rxw_region(LR, MR, PB::W);
+    float2* twl = smem;                                  // Nd
+    float* taps = reinterpret_cast<float*>(twl + Nd);    // npp
+    float2* reg0 = twl + Nd + (A.npp + 1) / 2;           // RXW_SYMS regions
+    for (uint32_t i = threadIdx.x; i < Nd; i += RX_THREADS) twl[i] = A.tw[i];
+    for (uint32_t i = threadIdx.x; i < A.npp; i += RX_THREADS) taps[i] = A.taps_pp[i];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t l = A.sym_first + blk * RXW_SYMS + w;
+    const bool active = l < A.sym_first + A.sym_count;
+    const rx_pkt_in in = A.pin[pkt];
+    const rx_pkt_state S = A.st[pkt];
+    const uint32_t n_stf = A.STF_CP + Nd;
+    const int m0 = static_cast<int>(n_stf + (l - 1) * (A.CP + Nd) + A.CP);  // first output of symbol l
+    const int qb0 = (m0 - static_cast<int>(A.m_star)) / LR;                  // m0 >= m_star
+    const int qb1 = (m0 + static_cast<int>(Nd) - static_cast<int>(A.m_star) + LR - 1) / LR;
+    const int64_t in0 = static_cast<int64_t>(A.p_star) + int64_t(MR) * qb0 - HLR;
+    const uint32_t n_in = static_cast<uint32_t>(MR * (qb1 - 1 - qb0) + PB::W);
+    float2* R = reg0 + w * region;
+    // valid input window relative to the fine peak: history is zero before it (rx_synced.cpp:711-740)
+    const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak;
+    const float2* src = A.iq + (size_t(pkt) * A.N_RX + a) * A.S_in + in.fine_peak + in0;
+    if (active)
+        for (uint32_t i = lane; i < n_in; i += 64) {
+            const int64_t qi = in0 + i;
+            R[i] = (qi >= 0 && qi < q_hi) ? src[i] : make_float2(0.f, 0.f);
+        }
+    __syncthreads();  // twiddles / taps (and this wave's own staging)
+    if (!active) return;
+    // resampling + phase-continuous mixer, outputs in registers
+    const double phi_stf = static_cast<double>(n_stf) * in.inc0;  // mixer phase at the first data sample
+    const float2 step1 = phasor(S.inc1);
+    float2 ys[BR][LR];
+#pragma unroll
+    for (int rd = 0; rd < BR; ++rd) {
+        const int q = qb0 + static_cast<int>(lane) + 64 * rd;
+        if (q < qb1) {
+            PB::run(R + MR * (q - qb0), taps, ys[rd]);
+            const int mb = static_cast<int>(A.m_star) + LR * q;
+            float2 r = phasor(phi_stf + static_cast<double>(mb - static_cast<int>(n_stf)) * S.inc1);
+#pragma unroll
+            for (int k = 0; k < LR; ++k) {
+                ys[rd][k] = cmul(ys[rd][k], r);
+                r = cmul(r, step1);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int rd = 0; rd < BR; ++rd) {
+        const int q = qb0 + static_cast<int>(lane) + 64 * rd;
+        if (q < qb1) {
+            const int mb = static_cast<int>(A.m_star) + LR * q;
+#pragma unroll
+            for (int k = 0; k < LR; ++k) {
+                const uint32_t idx = static_cast<uint32_t>(mb + k - m0);
+                if (idx < Nd) R[idx] = ys[rd][k];
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    float2 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = R[lane + 64 * m];
+    __builtin_amdgcn_wave_barrier();
+    wave_fft1024<-1>(v, R, twl, lane);
+    // occupied bins: FFT bin n -> subcarrier index k (extract_bins), amplitude, STO derotation
+    float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const uint32_t n = lane + 64 * m;
+        uint32_t k = 0xFFFFFFFFu;
+        if (n <= N / 2)
+            k = n + N / 2;
+        else if (n >= A.off_lower && n < A.off_lower + N / 2)
+            k = n - A.off_lower;
+        if (k != 0xFFFFFFFFu) {
+            const float2 rot = phasor(S.sto_inc * (static_cast<double>(k) - static_cast<double>(N / 2)));
+            Yrow[k] = cmul(cscale(v[m], A.amp_scale), rot);
+        }
+    }
+}
+
 hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
     const uint32_t Nd = a.plan.N;
     const uint32_t nblk = (a.sym_count + a.sym_per_block - 1) / a.sym_per_block;
@@ -301,7 +407,11 @@ hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
         const size_t lds = base + rx_in_cap(Nd, a.CP, a.L, a.M, W) * sizeof(float2) + a.npp * sizeof(float);
         hipLaunchKernelGGL(kern, g, b, lds, st, a);
     };
-    if (a.L == 9 && a.M == 10 && a.hl == 24)  // os_min 1 (225 taps)
+    if (Nd == 1024 && a.L == 9 && a.M == 10 && a.hl == 24 && a.sym_per_block == RXW_SYMS) {  // os_min 1
+        const uint32_t W = pp_block<9, 10, 24>::W;
+        const size_t lds = (Nd + (a.npp + 1) / 2 + RXW_SYMS * size_t(rxw_region(9, 10, W))) * sizeof(float2);
+        hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24>), g, b, lds, st, a);
+    } else if (a.L == 9 && a.M == 10 && a.hl == 24)  // os_min 1 (225 taps)
         fast(rx_fft_kernel<9, 10, 24>, pp_block<9, 10, 24>::W);
     else if (a.L == 9 && a.M == 10 && a.hl == 4)  // os_min 2
         fast(rx_fft_kernel<9, 10, 4>, pp_block<9, 10, 4>::W);
