@@ -12,70 +12,13 @@
 #include <tuple>
 #include <vector>
 
-#include "../kernels/kernels.hpp"
-#include "dnrp.h"
-#include "geometry.hpp"
+#include "ctx_internal.hpp"
 
 using namespace dnrp;
+using namespace dnrp::host;
 
-namespace {
+namespace dnrp::host {
 
-#define HIPCHK(x)                                  \
-    do {                                           \
-        if ((x) != hipSuccess) return DNRP_EDEVICE; \
-    } while (0)
-
-// device buffer owning wrapper
-struct dbuf {
-    void* p = nullptr;
-    size_t n = 0;
-    dbuf() = default;
-    dbuf(const dbuf&) = delete;
-    dbuf& operator=(const dbuf&) = delete;
-    ~dbuf() {
-        if (p) (void)hipFree(p);
-    }
-    bool ensure(size_t bytes) {
-        if (bytes <= n) return true;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-        if (hipMalloc(&p, bytes) != hipSuccess) return false;
-        n = bytes;
-        return true;
-    }
-    template <typename T>
-    bool upload(const std::vector<T>& v) {
-        if (!ensure(std::max<size_t>(v.size() * sizeof(T), 16))) return false;
-        return hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
-    }
-    template <typename T>
-    T* as() const {
-        return static_cast<T*>(p);
-    }
-};
-
-struct pinned {
-    void* p = nullptr;
-    size_t n = 0;
-    hipEvent_t ev = nullptr;
-    ~pinned() {
-        if (p) (void)hipHostFree(p);
-        if (ev) (void)hipEventDestroy(ev);
-    }
-    void* get(size_t bytes) {
-        if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        (void)hipEventSynchronize(ev);  // previous async copy out of this buffer is done
-        if (bytes > n) {
-            if (p) (void)hipHostFree(p);
-            p = nullptr;
-            n = 0;
-            if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
-            n = bytes;
-        }
-        return p;
-    }
-};
 
 dev::fft_plan make_plan(uint32_t N) {
     dev::fft_plan p{};
@@ -181,105 +124,8 @@ void fill_pairs(uint32_t N_TS, uint32_t* pair, uint32_t& mod) {  // transmit_div
     }
 }
 
-struct tx_tables {
-    dnrp_packet_sizes q{};
-    geo::tm_t tm{};
-    geo::dims_t dm{};
-    dev::fft_plan plan{};
-    geo::resampler_t rs;
-    dbuf code, stf, W, taps, taps_pp, tw, qam, qpsk, pdc_off;
-    uint32_t npp = 0;  // floats in taps_pp
-    std::vector<float> wscale;  // per codebook
-    std::vector<uint32_t> pdc_off_h;  // host copy of maps.pdc_sym_off
-};
 
-// device copy of a geo::rx_plan_t
-struct rx_plan_dev {
-    uint32_t n_dops = 0, n_epochs = 0;
-    dbuf dl, dmeta, segs, epochs;
-    bool upload(const geo::rx_plan_t& p) {
-        static_assert(sizeof(geo::rx_seg_t) == sizeof(dev::rx_seg), "rx_seg layout");
-        static_assert(sizeof(geo::rx_epoch_t) == sizeof(dev::rx_epoch), "rx_epoch layout");
-        n_dops = static_cast<uint32_t>(p.dl.size());
-        n_epochs = static_cast<uint32_t>(p.epochs.size());
-        return dl.upload(p.dl) && dmeta.upload(p.dmeta) && segs.upload(p.segs) && epochs.upload(p.epochs);
-    }
-};
-
-struct rx1_tables {  // per (u, b, N_eff_TX): STF/PCC phase
-    uint32_t u, b, N_eff_TX, Nd, N_occ, off_lower, CP, STF_CP, n_pattern, pattern_len;
-    dev::fft_plan plan{};
-    geo::resampler_t rs;
-    geo::maps_t maps;
-    uint32_t pcc_max = 0;
-    dbuf stf, tw, taps, taps_pp, drs_k, drs_v, pcc_k;
-    uint32_t npp = 0;  // floats in taps_pp
-    rx_plan_dev bplan;  // PCC phase back end
-    dbuf lut_pw[2][3], lut_w[2][3], luts;
-    uint32_t lut_n[2][3] = {}, lut_T[2] = {};
-};
-
-struct rx2_tables {  // per (psdef): PDC phase
-    dnrp_packet_sizes q{};
-    geo::maps_t maps;
-    dbuf pdc_k, pdc_sym;
-    rx_plan_dev bplan;  // PDC phase back end
-};
-
-struct netid_seq {
-    uint32_t nbits = 0;
-    dbuf t1, t2;
-};
-
-}  // namespace
-
-struct dnrp_ctx {
-    dnrp_cfg cfg{};
-    std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, std::unique_ptr<tx_tables>> txt;
-    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::unique_ptr<rx1_tables>> rx1t;
-    std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, std::unique_ptr<rx2_tables>> rx2t;
-    std::map<uint32_t, std::unique_ptr<netid_seq>> netid;
-    dbuf pcc_seq;
-    // batch scratch
-    dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d;
-    pinned st_tx, st_rxin, st_seq, st_rep;
-    // retained RX phase-1 state
-    rx1_tables* rx1_last = nullptr;
-    uint32_t rx_n = 0, rx_S_in = 0, rx_nsym_cap = 0, rx_Nf_pad = 0;
-    const float* rx_iq = nullptr;
-    std::vector<dev::rx_pkt_in> rx_pin_host;
-    // timing: HIP events recorded on the caller's stream around every launch (DNRP_TIMING=1)
-    bool timing = false;
-    struct ev_pool {
-        std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
-        size_t used = 0;
-    };
-    std::map<std::string, ev_pool> ev;
-    ~dnrp_ctx() {
-        for (auto& e : ev)
-            for (auto& p : e.second.ev) {
-                (void)hipEventDestroy(p.first);
-                (void)hipEventDestroy(p.second);
-            }
-    }
-    void tic(const char* name, hipStream_t s) {
-        if (!timing) return;
-        auto& pool = ev[name];
-        if (pool.used == pool.ev.size()) {
-            std::pair<hipEvent_t, hipEvent_t> p{};
-            (void)hipEventCreate(&p.first);
-            (void)hipEventCreate(&p.second);
-            pool.ev.push_back(p);
-        }
-        (void)hipEventRecord(pool.ev[pool.used].first, s);
-    }
-    void toc(const char* name, hipStream_t s) {
-        if (!timing) return;
-        auto& pool = ev[name];
-        (void)hipEventRecord(pool.ev[pool.used].second, s);
-        ++pool.used;
-    }
-};
+}  // namespace dnrp::host
 
 namespace {
 

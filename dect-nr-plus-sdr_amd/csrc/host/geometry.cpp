@@ -238,6 +238,21 @@ static std::vector<uint32_t> pcc_linear(uint32_t b, uint32_t N_TS) {  // pcc.cpp
     return out;
 }
 
+std::vector<cf32> stf_values(uint32_t b, uint32_t N_eff_TX) {  // stf.cpp:171-183, 185-285
+    const uint32_t N = 56 * b;
+    const auto pol = stf_polarity(b);
+    uint32_t lg = 0;
+    while ((1u << lg) < N_eff_TX) ++lg;
+    const cf32 fac = cf32(1.0f, 0.0f) * cf32(static_cast<float>(std::cos(M_PI / 4.0)), static_cast<float>(std::sin(M_PI / 4.0)));
+    std::vector<cf32> v(N + 1, cf32(0, 0));
+    for (uint32_t i = 0; i < N / 4; ++i) {
+        const uint32_t occ = i < N / 8 ? 4 * i : N / 2 + 3 + 4 * (i - N / 8);
+        const uint32_t k = static_cast<uint32_t>(kocc(N, occ) + static_cast<int>(N / 2));
+        v[k] = cf32(static_cast<float>(pol[(i + 2 * lg) % (N / 4)]), 0.0f) * fac;
+    }
+    return v;
+}
+
 maps_t build_maps(uint32_t b, uint32_t N_TS, uint32_t N_eff_TX, uint32_t N_DF) {
     maps_t m;
     const uint32_t Nb = 64 * b, N = 56 * b, Nf = N + 1, gb = 4 * b;
@@ -247,17 +262,9 @@ maps_t build_maps(uint32_t b, uint32_t N_TS, uint32_t N_eff_TX, uint32_t N_DF) {
     m.Nf = Nf;
     m.code.assign((N_DF + 1) * Nf, CODE_NONE);
     // STF (stf.cpp:171-183, 185-285), scale 1.0 as built in tx_rx.cpp:71
-    const auto pol = stf_polarity(b);
-    uint32_t lg = 0;
-    while ((1u << lg) < N_eff_TX) ++lg;
-    const cf32 fac = cf32(1.0f, 0.0f) * cf32(static_cast<float>(std::cos(M_PI / 4.0)), static_cast<float>(std::sin(M_PI / 4.0)));
-    m.stf.assign(Nf, cf32(0, 0));
-    for (uint32_t i = 0; i < N / 4; ++i) {
-        const uint32_t occ = i < N / 8 ? 4 * i : N / 2 + 3 + 4 * (i - N / 8);
-        const uint32_t k = static_cast<uint32_t>(kocc(N, occ) + static_cast<int>(N / 2));
-        m.stf[k] = cf32(static_cast<float>(pol[(i + 2 * lg) % (N / 4)]), 0.0f) * fac;
-        m.code[k] = CODE_STF;
-    }
+    m.stf = stf_values(b, N_eff_TX);
+    for (uint32_t k = 0; k < Nf; ++k)
+        if (m.stf[k] != cf32(0, 0)) m.code[k] = CODE_STF;
     // DRS tables (drs.cpp:196-254)
     m.drs_k.resize(2 * 4 * (N / 4));
     m.drs_v.resize(8 * (N / 4));

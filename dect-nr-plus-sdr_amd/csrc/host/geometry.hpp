@@ -58,6 +58,8 @@ struct maps_t {
     std::vector<float> drs_v;          // [8 ts][N_occ/4], +-1
 };
 maps_t build_maps(uint32_t b, uint32_t N_TS, uint32_t N_eff_TX, uint32_t N_DF);
+// STF values with DC (length N_b_OCC+1) for N_eff_TX, scale 1.0
+std::vector<cf32> stf_values(uint32_t b, uint32_t N_eff_TX);
 
 std::vector<cf32> W_matrix(uint32_t N_TS, uint32_t N_TX, uint32_t codebook, float* scaling);
 uint32_t W_codebooks(uint32_t N_TS, uint32_t N_TX);

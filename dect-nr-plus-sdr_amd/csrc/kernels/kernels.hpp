@@ -144,4 +144,45 @@ struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epo
 };
 hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st);
 
+
+// ---- synchronisation (sync.hip): sync_chunk_t::search() per window, reports in search order
+struct sync_res {  // layout of dnrp_sync_result (include/dnrp.h)
+    uint32_t found, det_ant;
+    float det_rms, det_metric;
+    uint32_t det_time, det_time_jb, coarse_local, fine_local;
+    int64_t coarse_64, fine_64;
+    float coarse_metric[8], rms[8];
+    float cfo_frac, cfo_int;
+    uint32_t u, b, N_eff_TX, pad;
+    float xc_metric[4];
+    uint32_t xc_idx[4];
+};
+struct sync_args {
+    uint32_t n_ant, n_pattern, stf_len, pattern, step, search_len, D, bos, n_steps;
+    uint32_t L, M, delay, hl, m_star, p_star;  // sync resampler (RX direction, L/M swapped)
+    uint32_t npp;                              // floats in taps_pp
+    const float* taps;                         // h[(hl+1)*L]
+    const float* taps_pp;                      // input-major block taps (polyphase.hpp)
+    float rms_min, prefactor;
+    float uw[8];                               // cover-sequence pairwise products
+    uint32_t n_uw;
+    const float2* iq;                          // window w, antenna a: iq + w*win_stride + a*ant_stride
+    uint64_t win_stride, ant_stride;
+    uint32_t S_win;
+    float* P;                                  // [n][n_ant][n_steps] step powers
+    float2* Cs;                                // [n][n_ant][n_steps] step correlations
+    uint32_t max_reports;
+    sync_res* res;                             // [n][max_reports]
+    uint32_t* n_found;                         // [n]
+    // fine search (crosscorrelator.cpp): hw rate, FFT correlation against the STF templates
+    uint32_t Ltx, Mtx, xc_l, xc_len, tmpl_len, n_templates, log2_fft;
+    const float2* tmpl_f;                      // [n_templates][n_fft] conj(DFT(template)) / n_fft
+    const float2* tw_fft;                      // forward twiddles of n_fft
+    uint32_t u, b;
+};
+hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st);
+hipError_t launch_sync_detect(const sync_args& a, uint32_t n, hipStream_t st);
+hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st);
+size_t sync_detect_lds(const sync_args& a);
+
 }  // namespace dnrp::dev

@@ -1,0 +1,660 @@
+// Synchronisation kernels: sync_chunk_t::search() (lib/src/phy/rx/sync/sync_chunk.cpp:143-279)
+// for a batch of windows, each window one chunk whose sync resampler starts with zero history.
+//
+//  sync_steps_kernel   one WG per (window, antenna, tile of 64 detection steps): sync resampler
+//                      (M/L polyphase, register blocks) into LDS, then per step the power
+//                      sum |x|^2 and the pattern-lag correlation sum x[n-P] conj(x[n]) over the
+//                      step's samples (autocorrelator_detection.cpp:107-128, 152-178). These are the
+//                      only per-sample passes over the window; everything after reads them.
+//  sync_detect_kernel  one WG per window, the detection / coarse-peak state machine:
+//                      detection conditions on moving sums of the step values (RMS limits,
+//                      front/back RMS, coarse metric band, streak; autocorrelator_detection.cpp:
+//                      186-280, movsum_uw.cpp:55-74), then for every detection the per-sample
+//                      coarse-peak search over one STF with the smoothed metric
+//                      (autocorrelator_peak.cpp:145-264), validity, metric-weighted coarse peak
+//                      time, RMS and fractional CFO at the peak (:311-394), skip after the peak.
+//                      Windowed sums are exact prefix differences in double (the reference keeps
+//                      float running sums with periodic re-summation).
+//  sync_fine_kernel    one WG per report: CFO pre-rotation of the strongest antenna's hw-rate
+//                      samples around the coarse peak and cross-correlation with every STF
+//                      template (crosscorrelator.cpp:80-251) as one forward FFT plus one inverse
+//                      FFT per template, argmax over the search range, N_eff_TX, fine peak.
+#include "device_common.hpp"
+#include "kernels.hpp"
+#include "polyphase.hpp"
+
+namespace dnrp::dev {
+
+constexpr uint32_t SYNC_THREADS = 256;
+constexpr uint32_t SYNC_TILE_STEPS = 64;
+constexpr uint32_t SYNC_PAD_PEAK = 32;  // samples before the coarse-peak region (weighted peak can sit left of it)
+
+__device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+// lb[y] for y in [y0, y0 + cnt) of one antenna (input x[i] valid for i in [0, S_win), zero history)
+// into dst[y - y0]. taps: LDS block taps (pp path) or the global natural taps (generic path).
+// Whole block participates; ends with a barrier.
+template <int LR, int MR, int HLR>
+__device__ void sync_resample(const sync_args& A, const float2* __restrict__ x, int64_t y0, uint32_t cnt,
+                              float2* stage, float2* dst, const float* taps) {
+    const int64_t S = A.S_win;
+    if constexpr (LR == 1) {
+        for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+            const int64_t y = y0 + i;
+            dst[i] = (y >= 0 && y < S) ? x[y] : make_float2(0.f, 0.f);
+        }
+        __syncthreads();
+    } else if constexpr (LR == 0) {  // generic L/M (os_min 4/8): direct FIR per output
+        for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+            const int64_t y = y0 + i;
+            float2 acc = make_float2(0.f, 0.f);
+            if (y >= 0) {
+                const uint64_t t = A.delay + static_cast<uint64_t>(y) * A.M;
+                const int64_t p = static_cast<int64_t>(t / A.L);
+                const uint32_t ph = static_cast<uint32_t>(t % A.L);
+                for (uint32_t d = 0; d <= A.hl; ++d) {
+                    const int64_t q = p - d;
+                    if (q < 0 || q >= S) continue;
+                    const float h = A.taps[ph + d * A.L];
+                    acc.x = fmaf(x[q].x, h, acc.x);
+                    acc.y = fmaf(x[q].y, h, acc.y);
+                }
+            }
+            dst[i] = acc;
+        }
+        __syncthreads();
+    } else {
+        using PB = pp_block<LR, MR, HLR>;
+        const int64_t ms = A.m_star;
+        const int64_t q0 = floordiv(y0 - ms, LR), q1 = floordiv(y0 + cnt - ms + LR - 1, LR);
+        const int64_t in0 = static_cast<int64_t>(A.p_star) + MR * q0 - HLR;
+        const uint32_t n_in = static_cast<uint32_t>(MR * (q1 - 1 - q0) + PB::W);
+        for (uint32_t i = threadIdx.x; i < n_in; i += blockDim.x) {
+            const int64_t q = in0 + i;
+            stage[i] = (q >= 0 && q < S) ? x[q] : make_float2(0.f, 0.f);
+        }
+        __syncthreads();
+        for (int64_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+            float2 yv[LR];
+            PB::run(stage + MR * (q - q0), taps, yv);
+            const int64_t mb = ms + LR * q;
+#pragma unroll
+            for (int k = 0; k < LR; ++k) {
+                const int64_t idx = mb + k - y0;
+                if (idx >= 0 && idx < static_cast<int64_t>(cnt)) dst[idx] = (mb + k >= 0) ? yv[k] : make_float2(0.f, 0.f);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__host__ __device__ inline uint32_t sync_stage_cap(uint32_t L, uint32_t M, uint32_t hl, uint32_t cnt) {
+    if (L <= 1) return 0;
+    const uint32_t W = hl + 1 + ((L - 1) * M) / L;
+    return M * (cnt / L + 2) + W + M;
+}
+
+// ===================================================================== per-step sums
+template <int LR, int MR, int HLR>
+__global__ void __launch_bounds__(SYNC_THREADS) sync_steps_kernel(sync_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const uint32_t ntile = (A.n_steps + SYNC_TILE_STEPS - 1) / SYNC_TILE_STEPS;
+    const uint32_t tile = blockIdx.x % ntile;
+    const uint32_t a = (blockIdx.x / ntile) % A.n_ant;
+    const uint32_t w = blockIdx.x / (ntile * A.n_ant);
+    float* taps = reinterpret_cast<float*>(smem);
+    const uint32_t tap_f2 = (A.npp + 3) / 4 * 2;
+    float2* lb = smem + tap_f2;
+    const uint32_t s0 = tile * SYNC_TILE_STEPS;
+    const uint32_t s1 = min(s0 + SYNC_TILE_STEPS, A.n_steps);
+    const int64_t y0 = static_cast<int64_t>(s0) * A.step - A.pattern;
+    const uint32_t cnt = (s1 - s0) * A.step + A.pattern;
+    float2* stage = lb + (cnt + 1) / 2 * 2;
+    if (LR > 1)
+        for (uint32_t i = threadIdx.x; i < A.npp; i += blockDim.x) taps[i] = A.taps_pp[i];
+    const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
+    sync_resample<LR, MR, HLR>(A, x, y0, cnt, stage, lb, taps);
+    // step s = s0 + tid/4, quarter tid%4 of its samples; reduce over the 4 lanes
+    const uint32_t sl = threadIdx.x >> 2, part = threadIdx.x & 3u;
+    const uint32_t s = s0 + sl, seg = A.step >> 2;
+    float pw = 0.f;
+    float2 c = make_float2(0.f, 0.f);
+    if (s < s1) {
+        const uint32_t i0 = (s - s0) * A.step + A.pattern + part * seg;  // index of y = s*step + part*seg
+        for (uint32_t j = 0; j < seg; ++j) {
+            const float2 v = lb[i0 + j];
+            pw = fmaf(v.x, v.x, fmaf(v.y, v.y, pw));
+            if (s >= 4) {
+                const float2 u = lb[i0 + j - A.pattern];  // A = x[n - P], B = x[n]: A conj(B)
+                c.x = fmaf(u.x, v.x, fmaf(u.y, v.y, c.x));
+                c.y = fmaf(u.y, v.x, fmaf(-u.x, v.y, c.y));
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+        pw += __shfl_xor(pw, o);
+        c.x += __shfl_xor(c.x, o);
+        c.y += __shfl_xor(c.y, o);
+    }
+    if (s < s1 && part == 0) {
+        const size_t o = (static_cast<size_t>(w) * A.n_ant + a) * A.n_steps + s;
+        A.P[o] = pw;
+        A.Cs[o] = c;
+    }
+}
+
+// ===================================================================== detection + coarse peak
+struct det_eval {
+    float rms, metric;
+};
+
+// autocorrelator_detection.cpp:186-280 at the step whose B block starts at s*step (movsums after
+// the push: power over the last 4*n_pattern step values, correlation over the last 4*(n_pattern-1)
+// with the cover pairwise products per group of 4; front = newest + oldest register, back = the
+// two after the oldest: movsum.hpp get_sum_front/get_sum_back with ptr at the oldest element)
+__device__ bool detect_eval(const sync_args& A, const float* __restrict__ P, const float2* __restrict__ Cs, uint32_t s,
+                            det_eval& out) {
+    const uint32_t np = 4 * A.n_pattern, nc = 4 * A.n_uw;
+    double pw = 0.0;
+    for (uint32_t i = 0; i < np; ++i) pw += P[s - (np - 1) + i];
+    const double rms = sqrt(pw / static_cast<double>(A.stf_len));
+    if (rms < static_cast<double>(A.rms_min) || 2.0 < rms) return false;
+    const double back = static_cast<double>(P[s - (np - 2)]) + P[s - (np - 3)];
+    const double front = static_cast<double>(P[s - (np - 1)]) + P[s];
+    if (sqrt(back) * 0.5 >= sqrt(front)) return false;
+    double cr = 0.0, ci = 0.0;
+    for (uint32_t g = 0; g < A.n_uw; ++g) {
+        double gr = 0.0, gi = 0.0;
+        for (uint32_t j = 0; j < 4; ++j) {
+            const float2 v = Cs[s - (nc - 1) + 4 * g + j];
+            gr += v.x;
+            gi += v.y;
+        }
+        cr += A.uw[g] * gr;
+        ci += A.uw[g] * gi;
+    }
+    const double q = static_cast<double>(A.prefactor) * sqrt(cr * cr + ci * ci) / pw;
+    const double metric = q * q;
+    if (metric < static_cast<double>(0.18f) || static_cast<double>(1.5f) < metric) return false;
+    if (!(static_cast<double>(0.18f) < metric)) return false;  // streak_t(0.18, 0, 1)::check
+    out.rms = static_cast<float>(rms);
+    out.metric = static_cast<float>(metric);
+    return true;
+}
+
+// exclusive prefix of n double2 values in v[] (in place), one wavefront; v[n] = total
+__device__ void wave_scan_d2(double2* v, uint32_t n, uint32_t lane) {
+    const uint32_t per = (n + 63) / 64;
+    const uint32_t b = lane * per, e = min(b + per, n);
+    double sx = 0.0, sy = 0.0;
+    for (uint32_t i = b; i < e; ++i) {
+        sx += v[i].x;
+        sy += v[i].y;
+    }
+    double ix = sx, iy = sy;  // inclusive scan over lanes
+    for (int o = 1; o < 64; o <<= 1) {
+        const double tx = __shfl_up(ix, o), ty = __shfl_up(iy, o);
+        if (static_cast<int>(lane) >= o) {
+            ix += tx;
+            iy += ty;
+        }
+    }
+    double rx = ix - sx, ry = iy - sy;
+    for (uint32_t i = b; i < e; ++i) {
+        const double2 t = v[i];
+        v[i] = make_double2(rx, ry);
+        rx += t.x;
+        ry += t.y;
+    }
+    if (lane == 63) v[n] = make_double2(ix, iy);
+}
+
+struct peak_lds {
+    double2* ckc;  // correlation prefix at every 16th product
+    double* ckp;   // power prefix at every 16th sample
+    double* met;   // metric per position of the peak search
+};
+
+// autocorrelator_peak.cpp:145-264 for one antenna: per-sample metric over [r0, r0 + D), smoothed
+// by the (2 bos + 1)-long moving mean (zero-initialised), last maximum wins (update on >=).
+// lbuf[i] = lb[yb + i], yb = r0 - stf_len - SYNC_PAD_PEAK.
+__device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t region, const peak_lds& L, uint32_t r0,
+                            double* red, float& pk_metric, uint32_t& pk_idx) {
+    const uint32_t P = A.pattern, yoff = A.stf_len + SYNC_PAD_PEAK;  // lbuf index of r0
+    const uint32_t nprod = region - P, nsc = (nprod + 15) / 16, nsp = (region + 15) / 16;
+    // segment sums: products prod(y) = lb[y-P] conj(lb[y]) indexed from lbuf index P; powers from 0
+    for (uint32_t g = threadIdx.x; g < nsc + nsp; g += blockDim.x) {
+        if (g < nsc) {
+            double sx = 0.0, sy = 0.0;
+            for (uint32_t j = 16 * g; j < min(16 * g + 16, nprod); ++j) {
+                const float2 c = cmulc(lbuf[j], lbuf[j + P]);
+                sx += c.x;
+                sy += c.y;
+            }
+            L.ckc[g] = make_double2(sx, sy);
+        } else {
+            const uint32_t h = g - nsc;
+            double sp = 0.0;
+            for (uint32_t j = 16 * h; j < min(16 * h + 16, region); ++j) sp += cnorm(lbuf[j]);
+            L.ckp[h] = sp;
+        }
+    }
+    __syncthreads();
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    if (wv == 0) wave_scan_d2(L.ckc, nsc, lane);
+    if (wv == 1) {  // power prefix: scan as double2 with zero imaginary parts via a temporary view
+        const uint32_t per = (nsp + 63) / 64;
+        const uint32_t b = lane * per, e = min(b + per, nsp);
+        double s = 0.0;
+        for (uint32_t i = b; i < e; ++i) s += L.ckp[i];
+        double inc = s;
+        for (int o = 1; o < 64; o <<= 1) {
+            const double t = __shfl_up(inc, o);
+            if (static_cast<int>(lane) >= o) inc += t;
+        }
+        double r = inc - s;
+        for (uint32_t i = b; i < e; ++i) {
+            const double t = L.ckp[i];
+            L.ckp[i] = r;
+            r += t;
+        }
+        if (lane == 63) L.ckp[nsp] = inc;
+    }
+    __syncthreads();
+    // prefix helpers: PC(z) = sum of prod with product index < z; PP(z) = sum of power index < z
+    auto PC = [&](uint32_t z, double& rx, double& ry) {
+        const uint32_t g = z >> 4;
+        double2 c = L.ckc[g];
+        for (uint32_t j = 16 * g; j < z; ++j) {
+            const float2 v = cmulc(lbuf[j], lbuf[j + P]);
+            c.x += v.x;
+            c.y += v.y;
+        }
+        rx = c.x;
+        ry = c.y;
+    };
+    auto PP = [&](uint32_t z) {
+        const uint32_t g = z >> 4;
+        double p = L.ckp[g];
+        for (uint32_t j = 16 * g; j < z; ++j) p += cnorm(lbuf[j]);
+        return p;
+    };
+    const uint32_t D = A.D, per = (D + blockDim.x - 1) / blockDim.x;
+    const uint32_t xb = threadIdx.x * per, xe = min(xb + per, D);
+    const uint32_t Lw = P * A.n_uw;  // correlation window (products)
+    // metric(x), x = r0 + i: corr over products y in [x - Lw + 1, x]; product index of y = (y - yb) - P
+    if (xb < xe) {
+        const uint32_t pi_end = yoff + xb - P + 1;  // product index just past y = x
+        double cr = 0.0, ci = 0.0;
+        for (uint32_t k = 0; k <= A.n_uw; ++k) {
+            const float ck = (k > 0 ? A.uw[k - 1] : 0.f) - (k < A.n_uw ? A.uw[k] : 0.f);
+            if (ck == 0.f) continue;
+            double rx, ry;
+            PC(pi_end - Lw + P * k, rx, ry);
+            cr += ck * rx;
+            ci += ck * ry;
+        }
+        double pw = PP(yoff + xb + 1) - PP(yoff + xb + 1 - A.stf_len);
+        for (uint32_t i = xb; i < xe; ++i) {
+            if (i > xb) {  // slide by one sample: every prefix point advances by one product / sample
+                const uint32_t pe = yoff + i - P;  // product index entering (y = x)
+                for (uint32_t k = 0; k <= A.n_uw; ++k) {
+                    const float ck = (k > 0 ? A.uw[k - 1] : 0.f) - (k < A.n_uw ? A.uw[k] : 0.f);
+                    if (ck == 0.f) continue;
+                    const float2 v = cmulc(lbuf[pe - Lw + P * k], lbuf[pe - Lw + P * k + P]);
+                    cr += ck * static_cast<double>(v.x);
+                    ci += ck * static_cast<double>(v.y);
+                }
+                pw += static_cast<double>(cnorm(lbuf[yoff + i])) - static_cast<double>(cnorm(lbuf[yoff + i - A.stf_len]));
+            }
+            const double q = static_cast<double>(A.prefactor) * sqrt(cr * cr + ci * ci) / pw;
+            L.met[i] = q * q;
+        }
+    }
+    __syncthreads();
+    // smoother (length 2 bos + 1, zero history) and last-maximum argmax
+    const uint32_t ns = 2 * A.bos + 1;
+    double best = -1.0;
+    uint32_t bidx = 0;
+    if (xb < xe) {
+        double sm = 0.0;
+        for (uint32_t j = 0; j < ns; ++j)
+            if (xb >= j) sm += L.met[xb - j];
+        for (uint32_t i = xb; i < xe; ++i) {
+            if (i > xb) {
+                sm += L.met[i];
+                if (i >= ns) sm -= L.met[i - ns];
+            }
+            const double mean = sm / static_cast<double>(ns);
+            if (mean >= best) {
+                best = mean;
+                bidx = i;
+            }
+        }
+    }
+    // block argmax: largest value, latest index among equal values
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const uint32_t oi = __shfl_xor(bidx, o);
+        if (ob > best || (ob == best && oi > bidx)) {
+            best = ob;
+            bidx = oi;
+        }
+    }
+    __syncthreads();
+    if (lane == 0) {
+        red[2 * wv] = best;
+        reinterpret_cast<uint32_t*>(red + 16)[wv] = bidx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t v = 1; v < (blockDim.x >> 6); ++v) {
+            const double ob = red[2 * v];
+            const uint32_t oi = reinterpret_cast<uint32_t*>(red + 16)[v];
+            if (ob > best || (ob == best && oi > bidx)) {
+                best = ob;
+                bidx = oi;
+            }
+        }
+        pk_metric = static_cast<float>(best);
+        pk_idx = r0 + bidx - A.bos;  // metric_smoother_bos_offset_to_center_samples
+    }
+    __syncthreads();
+}
+
+struct sync_shared {  // block scalars, at the start of the dynamic LDS (no static __shared__)
+    double red[24];
+    int s_min;
+    float s_rms, s_metric;
+    uint32_t s_ant;
+    float s_pk_metric[8];
+    uint32_t s_pk_idx[8];
+};
+constexpr uint32_t SYNC_SHARED_F2 = (sizeof(sync_shared) + 15) / 16 * 2;  // float2 slots, 16-B multiple
+
+template <int LR, int MR, int HLR>
+__global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    sync_shared& sh = *reinterpret_cast<sync_shared*>(smem);
+    double* red = sh.red;
+    int& s_min = sh.s_min;
+    float& s_rms = sh.s_rms;
+    float& s_metric = sh.s_metric;
+    uint32_t& s_ant = sh.s_ant;
+    float* s_pk_metric = sh.s_pk_metric;
+    uint32_t* s_pk_idx = sh.s_pk_idx;
+    const uint32_t w = blockIdx.x;
+    float* taps = reinterpret_cast<float*>(smem + SYNC_SHARED_F2);
+    const uint32_t tap_f2 = (A.npp + 3) / 4 * 2;
+    const uint32_t region = A.stf_len + A.D + SYNC_PAD_PEAK;
+    float2* lbuf = smem + SYNC_SHARED_F2 + tap_f2;
+    float2* stage = lbuf + (region + 1) / 2 * 2;
+    peak_lds pl;  // aliases the staging area (dead once the resampler has run)
+    pl.ckc = reinterpret_cast<double2*>(stage);
+    pl.ckp = reinterpret_cast<double*>(pl.ckc + (region + 15) / 16 + 2);
+    pl.met = pl.ckp + (region + 15) / 16 + 2;
+    if (LR > 1)
+        for (uint32_t i = threadIdx.x; i < A.npp; i += blockDim.x) taps[i] = A.taps_pp[i];
+    __syncthreads();
+    const float* Pw = A.P + static_cast<size_t>(w) * A.n_ant * A.n_steps;
+    const float2* Cw = A.Cs + static_cast<size_t>(w) * A.n_ant * A.n_steps;
+    sync_res* out = A.res + static_cast<size_t>(w) * A.max_reports;
+    uint32_t nrep = 0, s_cur = 4, ignore = A.stf_len + A.pattern;
+    while (nrep < A.max_reports) {
+        // ---------------- detection: first step at or after s_cur meeting the conditions
+        if (threadIdx.x == 0) s_min = 0x7FFFFFFF;
+        __syncthreads();
+        for (uint32_t base = s_cur; base < A.n_steps; base += blockDim.x) {
+            const uint32_t s = base + threadIdx.x;
+            if (s < A.n_steps && (s + 1) * A.step >= ignore) {
+                for (uint32_t a = 0; a < A.n_ant; ++a) {
+                    det_eval e;
+                    if (detect_eval(A, Pw + a * A.n_steps, Cw + a * A.n_steps, s, e)) {
+                        atomicMin(&s_min, static_cast<int>(s));
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            const int found = s_min;
+            __syncthreads();
+            if (found != 0x7FFFFFFF) break;
+        }
+        const int sd = s_min;
+        __syncthreads();
+        if (sd == 0x7FFFFFFF) break;
+        if (threadIdx.x == 0) {
+            for (uint32_t a = 0; a < A.n_ant; ++a) {
+                det_eval e;
+                if (detect_eval(A, Pw + a * A.n_steps, Cw + a * A.n_steps, static_cast<uint32_t>(sd), e)) {
+                    s_ant = a;
+                    s_rms = e.rms;
+                    s_metric = e.metric;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        s_cur = static_cast<uint32_t>(sd) + 1;
+        const uint32_t det_time = s_cur * A.step, r0 = det_time - A.pattern;
+        const float det_metric = s_metric;
+        // ---------------- coarse peak search over one STF on every antenna
+        const int64_t yb = static_cast<int64_t>(r0) - A.stf_len - SYNC_PAD_PEAK;
+        for (uint32_t a = 0; a < A.n_ant; ++a) {
+            const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
+            sync_resample<LR, MR, HLR>(A, x, yb, region, stage, lbuf, taps);
+            peak_search(A, lbuf, region, pl, r0, red, s_pk_metric[a], s_pk_idx[a]);
+        }
+        // post_processing_validity (autocorrelator_peak.cpp:311-364), float as in the reference
+        float cm[8];
+        float wsum = 0.f, msum = 0.f;
+        uint32_t nvalid = 0;
+        for (uint32_t a = 0; a < A.n_ant; ++a) {
+            cm[a] = 0.f;
+            const float m = s_pk_metric[a];
+            if (det_metric + (-0.25f) >= m) continue;
+            if (static_cast<int64_t>(det_time) + static_cast<int64_t>(-0.3 * static_cast<double>(A.stf_len)) >=
+                static_cast<int64_t>(s_pk_idx[a]))
+                continue;
+            cm[a] = m;
+            wsum += m * static_cast<float>(s_pk_idx[a]);
+            ++nvalid;
+        }
+        for (uint32_t a = 0; a < A.n_ant; ++a) msum += cm[a];
+        if (nvalid == 0) continue;  // false alarm: detection resumes after this step
+        const uint32_t wpk = static_cast<uint32_t>(roundf(wsum / msum));
+        if (wpk < A.stf_len - 1) continue;  // STF would start before the chunk (asserted in the reference)
+        const uint32_t cpl = wpk - (A.stf_len - 1);
+        // post_processing_at_coarse_peak (:366-394): RMS and fractional CFO over the STF at the peak
+        float cfo_w = 0.f, msum2 = 0.f, rms[8];
+        for (uint32_t a = 0; a < A.n_ant; ++a) {
+            rms[a] = 0.f;
+            if (!(cm[a] > 0.f)) continue;
+            const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
+            sync_resample<LR, MR, HLR>(A, x, cpl, A.stf_len, stage, lbuf, taps);
+            double cr = 0.0, ci = 0.0, pw = 0.0;
+            const uint32_t Lw = A.pattern * A.n_uw;
+            for (uint32_t i = threadIdx.x; i < A.stf_len; i += blockDim.x) {
+                pw += cnorm(lbuf[i]);
+                if (i < Lw) {
+                    const float2 c = cmulc(lbuf[i], lbuf[i + A.pattern]);
+                    const float u = A.uw[i / A.pattern];
+                    cr += u * static_cast<double>(c.x);
+                    ci += u * static_cast<double>(c.y);
+                }
+            }
+            pw = block_sum(pw, red);
+            cr = block_sum(cr, red);
+            ci = block_sum(ci, red);
+            const float m = s_pk_metric[a];
+            msum2 += m;
+            rms[a] = sqrtf(static_cast<float>(pw) / static_cast<float>(A.stf_len));
+            cfo_w += m * atan2f(static_cast<float>(ci), static_cast<float>(cr)) / static_cast<float>(A.pattern);
+        }
+        if (threadIdx.x == 0) {
+            sync_res r{};
+            r.found = 1;
+            r.det_ant = s_ant;
+            r.det_rms = s_rms;
+            r.det_metric = det_metric;
+            r.det_time = det_time;
+            r.det_time_jb = r0;
+            r.coarse_local = cpl;
+            double g = static_cast<double>(cpl);  // rx_pacer.cpp:306-313
+            g *= static_cast<double>(A.M);
+            g /= static_cast<double>(A.L);
+            r.coarse_64 = static_cast<int64_t>(static_cast<uint32_t>(round(g)));
+            for (uint32_t a = 0; a < 8; ++a) {
+                r.coarse_metric[a] = a < A.n_ant ? cm[a] : 0.f;
+                r.rms[a] = a < A.n_ant ? rms[a] : 0.f;
+            }
+            r.cfo_frac = cfo_w / msum2;
+            r.cfo_int = 0.f;  // coarse_peak_f_domain.cpp:195-199
+            r.u = A.u;
+            r.b = A.b;  // coarse_peak_f_domain.cpp:75-120: b of the radio device class
+            out[nrep] = r;
+        }
+        ignore = cpl + static_cast<uint32_t>(2.0 * static_cast<double>(A.stf_len));  // skip_after_peak
+        ++nrep;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        A.n_found[w] = nrep;
+        for (uint32_t k = nrep; k < A.max_reports; ++k) out[k].found = 0;
+    }
+}
+
+// ===================================================================== fine peak
+__global__ void __launch_bounds__(SYNC_THREADS) sync_fine_kernel(sync_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    float* s_val = reinterpret_cast<float*>(smem);  // [4]
+    uint32_t* s_idx = reinterpret_cast<uint32_t*>(smem + 2);  // [4]
+    sync_res* rp = A.res + blockIdx.x;
+    if (!rp->found) return;
+    const uint32_t w = blockIdx.x / A.max_reports;
+    const uint32_t nf = 1u << A.log2_fft;
+    float2* xb = smem + 4;
+    float2* yb = xb + nf;
+    float2* Sb = yb + nf;
+    // strongest antenna: first maximum of coarse_peak_array (ant.cpp:104-108)
+    uint32_t best = 0;
+    for (uint32_t a = 1; a < A.n_ant; ++a)
+        if (rp->coarse_metric[a] > rp->coarse_metric[best]) best = a;
+    const float cfo_hw = (rp->cfo_frac + rp->cfo_int) * static_cast<float>(A.Mtx) / static_cast<float>(A.Ltx);
+    const int64_t base = rp->coarse_64 - static_cast<int64_t>(A.xc_l);
+    const uint32_t stage_len = A.xc_len - 1 + A.tmpl_len;
+    const float2* x = A.iq + w * A.win_stride + best * A.ant_stride;
+    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) {
+        float2 v = make_float2(0.f, 0.f);
+        const int64_t q = base + i;
+        if (i < stage_len && q >= 0 && q < static_cast<int64_t>(A.S_win))
+            v = cmul(x[q], phasor(static_cast<double>(cfo_hw) * static_cast<double>(i)));
+        xb[i] = v;
+    }
+    __syncthreads();
+    const float2* S = fft_pow2<-1>(xb, yb, A.tw_fft, A.log2_fft);
+    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) Sb[i] = S[i];
+    __syncthreads();
+    float xm[4];
+    uint32_t xi[4];
+    for (uint32_t k = 0; k < A.n_templates; ++k) {
+        const float2* T = A.tmpl_f + static_cast<size_t>(k) * nf;
+        for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) xb[i] = cmul(Sb[i], T[i]);
+        __syncthreads();
+        const float2* R = fft_pow2<+1>(xb, yb, A.tw_fft, A.log2_fft);
+        float bv = -1.f;
+        uint32_t bi = 0xFFFFFFFFu;
+        for (uint32_t j = threadIdx.x; j < A.xc_len; j += blockDim.x) {
+            const float m = cnorm(R[j]);
+            if (m > bv) {  // first maximum (volk_32fc_index_max_32u)
+                bv = m;
+                bi = j;
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o);
+            const uint32_t oi = __shfl_xor(bi, o);
+            if (ov > bv || (ov == bv && oi < bi)) {
+                bv = ov;
+                bi = oi;
+            }
+        }
+        if ((threadIdx.x & 63u) == 0) {
+            s_val[threadIdx.x >> 6] = bv;
+            s_idx[threadIdx.x >> 6] = bi;
+        }
+        __syncthreads();
+        for (uint32_t v = 0; v < blockDim.x / 64; ++v)
+            if (s_val[v] > bv || (s_val[v] == bv && s_idx[v] < bi)) {
+                bv = s_val[v];
+                bi = s_idx[v];
+            }
+        xm[k] = sqrtf(bv);
+        xi[k] = bi;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        uint32_t kbest = 0;
+        float msum_max = 0.f;
+        for (uint32_t k = 0; k < A.n_templates; ++k)
+            if (msum_max < xm[k]) {  // strictly larger (crosscorrelator.cpp:214-226)
+                msum_max = xm[k];
+                kbest = k;
+            }
+        for (uint32_t k = 0; k < 4; ++k) {
+            rp->xc_metric[k] = k < A.n_templates ? xm[k] : 0.f;
+            rp->xc_idx[k] = k < A.n_templates ? xi[k] : 0u;
+        }
+        rp->N_eff_TX = 1u << kbest;
+        const float wi = xm[kbest] * static_cast<float>(xi[kbest]);
+        rp->fine_local = static_cast<uint32_t>(roundf(wi / msum_max));
+        rp->fine_64 = base + rp->fine_local;
+    }
+}
+
+// ===================================================================== launchers
+size_t sync_detect_lds(const sync_args& a) {
+    const uint32_t region = a.stf_len + a.D + SYNC_PAD_PEAK;
+    const size_t taps = (a.npp + 3) / 4 * 2 * sizeof(float2);
+    const size_t lb = (region + 1) / 2 * 2 * sizeof(float2);
+    const size_t stage = sync_stage_cap(a.L, a.M, a.hl, region) * sizeof(float2);
+    const size_t alias = ((region + 15) / 16 + 2) * (sizeof(double2) + sizeof(double)) + a.D * sizeof(double);
+    return SYNC_SHARED_F2 * sizeof(float2) + taps + lb + (stage > alias ? stage : alias);
+}
+
+#define SYNC_DISPATCH(KERNEL, GRID, LDS)                                                   \
+    do {                                                                                   \
+        if (a.L == 9 && a.M == 10 && a.hl == 24)                                           \
+            hipLaunchKernelGGL((KERNEL<9, 10, 24>), GRID, dim3(SYNC_THREADS), LDS, st, a); \
+        else if (a.L == 9 && a.M == 10 && a.hl == 4)                                       \
+            hipLaunchKernelGGL((KERNEL<9, 10, 4>), GRID, dim3(SYNC_THREADS), LDS, st, a);  \
+        else if (a.L == 1 && a.M == 1)                                                     \
+            hipLaunchKernelGGL((KERNEL<1, 1, 0>), GRID, dim3(SYNC_THREADS), LDS, st, a);   \
+        else                                                                               \
+            hipLaunchKernelGGL((KERNEL<0, 0, 0>), GRID, dim3(SYNC_THREADS), LDS, st, a);   \
+    } while (0)
+
+hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
+    const uint32_t ntile = (a.n_steps + SYNC_TILE_STEPS - 1) / SYNC_TILE_STEPS;
+    const uint32_t cnt = SYNC_TILE_STEPS * a.step + a.pattern;
+    const size_t lds = (a.npp + 3) / 4 * 2 * sizeof(float2) + (cnt + 1) / 2 * 2 * sizeof(float2) +
+                       sync_stage_cap(a.L, a.M, a.hl, cnt) * sizeof(float2);
+    const dim3 g(n * a.n_ant * ntile);
+    SYNC_DISPATCH(sync_steps_kernel, g, lds);
+    return hipGetLastError();
+}
+
+hipError_t launch_sync_detect(const sync_args& a, uint32_t n, hipStream_t st) {
+    const dim3 g(n);
+    SYNC_DISPATCH(sync_detect_kernel, g, sync_detect_lds(a));
+    return hipGetLastError();
+}
+
+hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st) {
+    const size_t lds = (4 + 3 * (size_t(1) << a.log2_fft)) * sizeof(float2);
+    hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(SYNC_THREADS), lds, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace dnrp::dev

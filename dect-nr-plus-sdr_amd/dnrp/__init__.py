@@ -2,6 +2,7 @@
 
 Mirrors the reference's per-worker PHY objects with batched calls:
   Phy.tx_batch      <- tx_t::generate_tx_packet      (lib/src/phy/tx/tx.cpp:165-314)
+  Phy.rx_sync_batch <- sync_chunk_t::search()         (lib/src/phy/rx/sync/sync_chunk.cpp:143-279)
   Phy.rx_pcc_batch  <- rx_synced_t::demoddecod_rx_pcc (rx_synced.cpp:186-323)
   Phy.rx_pdc_batch  <- rx_synced_t::demoddecod_rx_pdc (rx_synced.cpp:325-436)
   Phy.add_network_id <- tx_rx_t::add_new_network_id (tx_rx.hpp:52)
@@ -11,6 +12,8 @@ there is no fallback path.
 """
 import ctypes as C
 import os
+
+import numpy as np
 
 # torch ships its own HIP runtime (torch/lib/libamdhip64.so, SONAME libamdhip64.so.7). Loading it
 # first lets libdnrp.so bind to the same runtime instead of a second copy from /opt/rocm, so
@@ -62,6 +65,45 @@ class SyncReport(C.Structure):
                 ("u", C.c_uint32), ("b", C.c_uint32), ("N_eff_TX", C.c_uint32)]
 
 
+class SyncCfg(C.Structure):
+    _fields_ = [("u", C.c_uint32), ("b", C.c_uint32), ("N_ant_limited", C.c_uint32), ("chunk_len", C.c_uint32),
+                ("max_reports", C.c_uint32)]
+
+
+class SyncResult(C.Structure):
+    _fields_ = [("found", C.c_uint32), ("detection_ant_idx", C.c_uint32), ("detection_rms", C.c_float),
+                ("detection_metric", C.c_float), ("detection_time_local", C.c_uint32),
+                ("detection_time_with_jump_back_local", C.c_uint32), ("coarse_peak_time_local", C.c_uint32),
+                ("fine_peak_time_local", C.c_uint32), ("coarse_peak_time", C.c_int64), ("fine_peak_time", C.c_int64),
+                ("coarse_peak_array", C.c_float * 8), ("rms_array", C.c_float * 8), ("cfo_fractional_rad", C.c_float),
+                ("cfo_integer_rad", C.c_float), ("u", C.c_uint32), ("b", C.c_uint32), ("N_eff_TX", C.c_uint32),
+                ("reserved", C.c_uint32), ("fine_peak_metric", C.c_float * 4), ("fine_peak_index", C.c_uint32 * 4)]
+
+
+def _np_dtype(st):
+    names, formats, offsets = [], [], []
+    for name, ct in st._fields_:
+        names.append(name)
+        if hasattr(ct, "_length_"):
+            formats.append((np.dtype(ct._type_), (ct._length_,)))
+        else:
+            formats.append(np.dtype(ct))
+        offsets.append(getattr(st, name).offset)
+    return np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": C.sizeof(st)})
+
+
+SYNC_RESULT_DTYPE = _np_dtype(SyncResult)
+SYNC_REPORT_DTYPE = _np_dtype(SyncReport)
+
+
+def sync_reports(results):
+    """dnrp_sync_result rows -> dnrp_sync_report array for rx_pcc_batch (vectorised)."""
+    r = np.zeros(len(results), SYNC_REPORT_DTYPE)
+    for k in ("fine_peak_time", "cfo_fractional_rad", "cfo_integer_rad", "u", "b", "N_eff_TX"):
+        r[k] = results[k]
+    return r
+
+
 class PccReport(C.Structure):
     _fields_ = [("snr_dB", C.c_float), ("cfo_fractional_rad", C.c_float), ("sto_fractional", C.c_float),
                 ("rms", C.c_float * 8)]
@@ -76,7 +118,7 @@ class PdcReq(C.Structure):
 
 
 EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_get_packet_sizes",
-           "dnrp_compute_packet_sizes", "dnrp_tx_batch",
+           "dnrp_compute_packet_sizes", "dnrp_tx_batch", "dnrp_rx_sync_batch",
            "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_kernel_time_total", "dnrp_strerror"]
 
 _lib = None
@@ -96,7 +138,9 @@ def lib():
         L.dnrp_compute_packet_sizes.argtypes = [C.POINTER(Cfg), C.POINTER(PsDef), C.POINTER(PacketSizes)]
         L.dnrp_tx_batch.argtypes = [P, C.POINTER(PsDef), C.c_uint32, C.POINTER(TxDesc), P, P, C.c_uint32, P,
                                     C.c_uint32, P]
-        L.dnrp_rx_pcc_batch.argtypes = [P, C.c_uint32, C.POINTER(SyncReport), P, C.c_uint32, P,
+        L.dnrp_rx_sync_batch.argtypes = [P, C.POINTER(SyncCfg), C.c_uint32, P, C.c_uint64, C.c_uint64, C.c_uint32,
+                                         P, P, P]
+        L.dnrp_rx_pcc_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P,
                                         C.POINTER(PccReport), P]
         L.dnrp_rx_pdc_batch.argtypes = [P, C.POINTER(PsDef), C.c_uint32, C.POINTER(PdcReq), P, C.c_uint32,
                                         C.POINTER(PdcReport), P]
@@ -174,9 +218,28 @@ class Phy:
                                  C.c_void_p(pdc_d.data_ptr()), pdc_d.shape[1], C.c_void_p(iq_out.data_ptr()),
                                  iq_out.shape[2], _stream_ptr(stream)), "dnrp_tx_batch")
 
+    def rx_sync_batch(self, sc, iq, n, S_win, win_stride, ant_stride, res=None, n_found=None, stream=None):
+        """sync_chunk_t::search() on n windows of the device cf32 tensor iq (strides in samples).
+        res: numpy SYNC_RESULT_DTYPE [n, max_reports] (pinned memory keeps the copy asynchronous);
+        valid after sync(). Returns (res, n_found)."""
+        if res is None:
+            res = np.zeros((n, sc.max_reports), SYNC_RESULT_DTYPE)
+        if n_found is None:
+            n_found = np.zeros(n, np.uint32)
+        assert res.dtype == SYNC_RESULT_DTYPE and res.size >= n * sc.max_reports and res.flags.c_contiguous
+        _chk(lib().dnrp_rx_sync_batch(self._ctx, C.byref(sc), n, C.c_void_p(iq.data_ptr()), win_stride, ant_stride,
+                                      S_win, C.c_void_p(res.ctypes.data), C.c_void_p(n_found.ctypes.data),
+                                      _stream_ptr(stream)), "dnrp_rx_sync_batch")
+        return res, n_found
+
     def rx_pcc_batch(self, reports, iq_in, pcc_llr, want_report=False, stream=None):
+        """reports: list of SyncReport or a numpy SYNC_REPORT_DTYPE array (see sync_reports())."""
         n = len(reports)
-        arr = (SyncReport * n)(*reports)
+        if isinstance(reports, np.ndarray):
+            assert reports.dtype == SYNC_REPORT_DTYPE and reports.flags.c_contiguous
+            arr = C.c_void_p(reports.ctypes.data)
+        else:
+            arr = C.cast((SyncReport * n)(*reports), C.c_void_p)
         rep = (PccReport * n)() if want_report else None
         _chk(lib().dnrp_rx_pcc_batch(self._ctx, n, arr, C.c_void_p(iq_in.data_ptr()), iq_in.shape[2],
                                      C.c_void_p(pcc_llr.data_ptr()), rep, _stream_ptr(stream)), "dnrp_rx_pcc_batch")

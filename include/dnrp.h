@@ -15,6 +15,8 @@
  *   dnrp_tx_batch          <- tx_t::generate_tx_packet (lib/include/dectnrp/phy/tx/tx.hpp:80-81,
  *                             lib/src/phy/tx/tx.cpp:165-314), FEC boundary between rate matching
  *                             and scrambling (pcc_enc.cpp:212, pdc_enc.cpp:218-221)
+ *   dnrp_rx_sync_batch     <- sync_chunk_t::search() per window (lib/include/dectnrp/phy/rx/sync/
+ *                             sync_chunk.hpp:72, lib/src/phy/rx/sync/sync_chunk.cpp:143-279)
  *   dnrp_rx_pcc_batch      <- rx_synced_t::demoddecod_rx_pcc up to the descrambled PCC d-bits
  *                             (lib/include/dectnrp/phy/rx/rx_synced/rx_synced.hpp:93,
  *                              rx_synced.cpp:186-302, pcc_enc.cpp:297)
@@ -101,6 +103,36 @@ typedef struct {
     uint32_t u, b, N_eff_TX;
 } dnrp_sync_report;
 
+/* Synchronisation of one batch of windows (sync_chunk_t, worker_pool_config_t subset) */
+typedef struct {
+    uint32_t u, b;          /* radio device class u_min / b_min: the STF searched for (sync_chunk.cpp:54-57) */
+    uint32_t N_ant_limited; /* antennas searched, <= cfg.N_TX_max (RX_SYNC_PARAM_AUTOCORRELATOR_ANTENNA_LIMIT) */
+    uint32_t chunk_len;     /* hw samples per chunk; the search covers chunk_len/L*M + 4 STFs at the
+                               DECT rate (sync_chunk.cpp:63-66), the window must hold the peak and
+                               cross-correlation samples after it (zeros are read past S_win) */
+    uint32_t max_reports;   /* packets reported per window (successive search() calls on one chunk) */
+} dnrp_sync_cfg;
+
+/* sync_report_t (phy/rx/sync/sync_report.hpp:29-98) of one synchronised packet. "local" times are
+ * DECT-rate sample indices of the chunk's resampled buffer, the others hw sample indices relative
+ * to the window start. fine_peak_time / cfo_fractional_rad / cfo_integer_rad / u / b / N_eff_TX are
+ * what dnrp_rx_pcc_batch consumes (as a dnrp_sync_report). */
+typedef struct {
+    uint32_t found;                   /* 1: packet synchronised; 0: slot unused */
+    uint32_t detection_ant_idx;
+    float detection_rms, detection_metric;
+    uint32_t detection_time_local, detection_time_with_jump_back_local;
+    uint32_t coarse_peak_time_local, fine_peak_time_local;
+    int64_t coarse_peak_time;
+    int64_t fine_peak_time;
+    float coarse_peak_array[8];       /* > 0: antenna had a valid coarse peak (its smoothed metric) */
+    float rms_array[8];
+    float cfo_fractional_rad, cfo_integer_rad;
+    uint32_t u, b, N_eff_TX, reserved;
+    float fine_peak_metric[4];        /* |xcorr| maximum per STF template N_eff_TX = 1, 2, 4, 8 */
+    uint32_t fine_peak_index[4];
+} dnrp_sync_result;
+
 /* PHY part of pcc_report_t plus the sync_report_t values rx_synced_t refines (rx_synced.cpp:530-580) */
 typedef struct {
     float snr_dB;             /* estimator_snr after STF + DRS of the PCC symbols */
@@ -142,6 +174,18 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
                   uint32_t S, void* stream);
 
 /*
+ * Synchronisation: sync_chunk_t::search() on n windows, each window one chunk whose sync resampler
+ * starts with zero history at sample 0 (reset_localbuffer, sync_chunk.cpp:300-311). Detection,
+ * coarse peak and fine peak as in the reference; up to max_reports packets per window in search
+ * order (the reference returns them from successive search() calls).
+ *   iq       device cf32; window w, antenna a, sample i at iq[2*(w*win_stride + a*ant_stride + i)]
+ *            (strides in samples: [n][N_RX][S] windows or per-antenna continuous streams)
+ *   res      host [n][max_reports]; n_found host [n] (optional). Valid after dnrp_sync().
+ */
+int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32_t n, const float* iq, uint64_t win_stride,
+                       uint64_t ant_stride, uint32_t S_win, dnrp_sync_result* res, uint32_t* n_found, void* stream);
+
+/*
  * RX phase 1: synchronised PCC demodulation of n packets (same u, b, N_eff_TX).
  *   iq_in    device [n][N_RX][S_in] cf32 slot windows, N_RX = cfg.N_TX_max
  *   pcc_llr  device [n][196] int16, descrambled
@@ -164,8 +208,8 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const 
 int dnrp_sync(dnrp_ctx* ctx, void* stream);
 
 /* Kernel timing (only when the environment has DNRP_TIMING=1 at dnrp_ctx_create): HIP events
- * recorded on the caller's stream around each launch. Names: "tx", "rx_stf", "rx_fft_pcc",
- * "rx_pcc", "rx_fft_pdc", "rx_pdc". */
+ * recorded on the caller's stream around each launch. Names: "tx", "sync_steps", "sync_detect",
+ * "sync_fine", "rx_stf", "rx_fft_pcc", "rx_pcc", "rx_fft_pdc", "rx_pdc". */
 int dnrp_last_kernel_ms(const dnrp_ctx* ctx, const char* name, float* ms);
 int dnrp_kernel_time_total(dnrp_ctx* ctx, const char* name, float* total_ms, uint32_t* count, int reset);
 

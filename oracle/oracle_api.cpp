@@ -2,6 +2,7 @@
 // extern "C" surface of the oracle for ctypes (tests/, bench.py cpu_baseline, smoke()).
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <random>
 #include <thread>
@@ -289,6 +290,86 @@ double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_
         return std::chrono::duration<double>(t1 - t0).count();
     } catch (...) {
         return -2.0;
+    }
+}
+
+// Synchronisation of one window (= one chunk starting at iq[0]); reports in search order.
+// scfg: u, b, os_min, L, M, N_ant, N_ant_limited, chunk_len ; iq [N_ant_limited][S_win] cf32
+// out [max_reports][SYNC_NF] doubles: found, det_ant, det_rms, det_metric, det_time, det_time_jb,
+//   coarse_local, coarse_64, cfo_frac, u, b, N_eff_TX, fine_local, fine_64, coarse_metric[8],
+//   rms[8], xc_metric[4], xc_idx[4]
+static constexpr int SYNC_NF = 38;
+int oracle_sync(const uint32_t* scfg, const float* iq, uint32_t S_win, uint32_t max_reports, int use_float,
+                double* out) {
+    try {
+        sync_cfg_t c;
+        c.u = scfg[0];
+        c.b = scfg[1];
+        c.os_min = scfg[2];
+        c.L = scfg[3];
+        c.M = scfg[4];
+        c.N_ant = scfg[5];
+        c.N_ant_limited = scfg[6];
+        c.chunk_len = scfg[7];
+        const auto r = use_float ? sync_search<float>(c, iq, S_win, max_reports)
+                                 : sync_search<double>(c, iq, S_win, max_reports);
+        for (size_t i = 0; i < r.size(); ++i) {
+            const auto& o = r[i];
+            double* d = out + i * SYNC_NF;
+            const double v[14] = {double(o.found), double(o.det_ant), o.det_rms, o.det_metric, double(o.det_time),
+                                  double(o.det_time_jb), double(o.coarse_local), double(o.coarse_64), o.cfo_frac,
+                                  double(o.u), double(o.b), double(o.N_eff_TX), double(o.fine_local),
+                                  double(o.fine_64)};
+            for (int k = 0; k < 14; ++k) d[k] = v[k];
+            for (int k = 0; k < 8; ++k) d[14 + k] = o.coarse_metric[k];
+            for (int k = 0; k < 8; ++k) d[22 + k] = o.rms[k];
+            for (int k = 0; k < 4; ++k) d[30 + k] = o.xc_metric[k];
+            for (int k = 0; k < 4; ++k) d[34 + k] = o.xc_idx[k];
+        }
+        return static_cast<int>(r.size());
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle_sync: %s\n", e.what());
+        return -2;
+    }
+}
+
+// out: geometry n_pattern, bos, stf_len, pattern, step, A, B, C, D, search_len, lb_len, xc_l,
+//      xc_len, tmpl_len, n_templates ; *rms_min
+int oracle_sync_geometry(const uint32_t* scfg, uint32_t* out, float* rms_min) {
+    sync_cfg_t c;
+    c.u = scfg[0];
+    c.b = scfg[1];
+    c.os_min = scfg[2];
+    c.L = scfg[3];
+    c.M = scfg[4];
+    c.N_ant = scfg[5];
+    c.N_ant_limited = scfg[6];
+    c.chunk_len = scfg[7];
+    const auto g = sync_geometry(c);
+    const uint32_t v[] = {g.n_pattern, g.bos, g.stf_len, g.pattern, g.step, g.A, g.B, g.C, g.D, g.search_len,
+                          g.lb_len, g.xc_l, g.xc_len, g.tmpl_len, g.n_templates};
+    std::memcpy(out, v, sizeof(v));
+    *rms_min = g.rms_min;
+    return 0;
+}
+
+// STF template (cf32 interleaved, tmpl_len samples)
+int oracle_stf_template(const uint32_t* scfg, uint32_t N_eff_TX, float* out) {
+    try {
+        sync_cfg_t c;
+        c.u = scfg[0];
+        c.b = scfg[1];
+        c.os_min = scfg[2];
+        c.L = scfg[3];
+        c.M = scfg[4];
+        const auto t = stf_template(c, N_eff_TX);
+        for (size_t i = 0; i < t.size(); ++i) {
+            out[2 * i] = static_cast<float>(t[i].real());
+            out[2 * i + 1] = static_cast<float>(t[i].imag());
+        }
+        return static_cast<int>(t.size());
+    } catch (...) {
+        return -2;
     }
 }
 

@@ -55,4 +55,33 @@ void tx_packet(const cfg_t& cfg, const packet_sizes_t& ps, const tx_desc_t& d, c
 template <typename R>
 void rx_packet(const cfg_t& cfg, const packet_sizes_t& ps, const rx_in_t& in, rx_out_t& out);
 
+
+// ---------------------------------------------------------------- synchronisation (oracle_sync.cpp)
+struct sync_cfg_t {  // radio device class minima u/b (sync_chunk.cpp:54-57), resampler L/M (TX values)
+    uint32_t u = 8, b = 16, os_min = 1, L = 10, M = 9;
+    uint32_t N_ant = 1, N_ant_limited = 1;  // physical antennas (templates), antennas searched
+    uint32_t chunk_len = 0;                 // hw samples of the chunk (search covers A + B)
+};
+struct sync_geom_t {
+    uint32_t n_pattern, bos, stf_len, pattern, step, A, B, C, D, search_len, lb_len;
+    uint32_t xc_l, xc_len, tmpl_len, n_templates;
+    float rms_min;
+};
+struct sync_out_t {  // sync_report_t (sync_report.hpp:29-98)
+    uint32_t found, det_ant;
+    float det_rms, det_metric;
+    uint32_t det_time, det_time_jb, coarse_local;
+    int64_t coarse_64;
+    float coarse_metric[8], rms[8];
+    float cfo_frac;
+    uint32_t u, b, N_eff_TX, fine_local;
+    int64_t fine_64;
+    float xc_metric[4];
+    uint32_t xc_idx[4];
+};
+sync_geom_t sync_geometry(const sync_cfg_t& c);
+std::vector<cd> stf_template(const sync_cfg_t& c, uint32_t N_eff_TX);
+template <typename R>
+std::vector<sync_out_t> sync_search(const sync_cfg_t& c, const float* iq, uint32_t S_win, uint32_t max_reports);
+
 }  // namespace orc

@@ -55,6 +55,9 @@ def lib():
         L.oracle_k_b_occ.argtypes = [C.c_uint32, np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS"),
                                      C.c_uint32]
         L.oracle_special.argtypes = [C.c_float, F32P]
+        L.oracle_sync.argtypes = [U32P, F32P, C.c_uint32, C.c_uint32, C.c_int, F64P]
+        L.oracle_sync_geometry.argtypes = [U32P, U32P, C.POINTER(C.c_float)]
+        L.oracle_stf_template.argtypes = [U32P, C.c_uint32, F32P]
         _lib = L
     return _lib
 
@@ -171,3 +174,52 @@ def special(z):
     out = np.zeros(5, np.float32)
     lib().oracle_special(np.float32(z), out)
     return out
+
+
+# ---- synchronisation (oracle_sync.cpp)
+SYNC_KEYS = ["found", "det_ant", "det_rms", "det_metric", "det_time", "det_time_jb", "coarse_local", "coarse_64",
+             "cfo_frac", "u", "b", "N_eff_TX", "fine_local", "fine_64"]
+SYNC_GEOM_KEYS = ["n_pattern", "bos", "stf_len", "pattern", "step", "A", "B", "C", "D", "search_len", "lb_len",
+                  "xc_l", "xc_len", "tmpl_len", "n_templates"]
+
+
+def sync_cfg(u, b, os_min=1, L=10, M=9, n_ant=1, n_lim=None, chunk_len=0):
+    return np.array([u, b, os_min, L, M, n_ant, n_ant if n_lim is None else n_lim, chunk_len], dtype=np.uint32)
+
+
+def sync_geometry(scfg):
+    out = np.zeros(len(SYNC_GEOM_KEYS), np.uint32)
+    r = C.c_float()
+    lib().oracle_sync_geometry(np.asarray(scfg, np.uint32), out, C.byref(r))
+    g = dict(zip(SYNC_GEOM_KEYS, map(int, out)))
+    g["rms_min"] = r.value
+    return g
+
+
+def stf_template(scfg, n_eff_tx):
+    g = sync_geometry(scfg)
+    out = np.zeros(2 * g["tmpl_len"], np.float32)
+    n = lib().oracle_stf_template(np.asarray(scfg, np.uint32), n_eff_tx, out)
+    assert n == g["tmpl_len"], n
+    return out.view(np.complex64).copy()
+
+
+def sync(scfg, iq, max_reports=4, use_float=False):
+    """iq: complex64 [N_ant_limited, S_win] window (chunk starting at iq[:, 0]). Returns a list of dicts."""
+    iq = np.ascontiguousarray(iq, dtype=np.complex64)
+    out = np.zeros((max_reports, 38), np.float64)
+    n = lib().oracle_sync(np.asarray(scfg, np.uint32), iq.view(np.float32).reshape(-1), iq.shape[1], max_reports,
+                          int(use_float), out)
+    assert n >= 0, n
+    res = []
+    for i in range(n):
+        d = {k: out[i, j] for j, k in enumerate(SYNC_KEYS)}
+        for k in ("found", "det_ant", "det_time", "det_time_jb", "coarse_local", "coarse_64", "u", "b", "N_eff_TX",
+                  "fine_local", "fine_64"):
+            d[k] = int(d[k])
+        d["coarse_metric"] = out[i, 14:22].copy()
+        d["rms"] = out[i, 22:30].copy()
+        d["xc_metric"] = out[i, 30:34].copy()
+        d["xc_idx"] = out[i, 34:38].astype(np.int64)
+        res.append(d)
+    return res

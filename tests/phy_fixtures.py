@@ -40,3 +40,35 @@ def channel(rng, iq_tx, n_rx, S_in, offset, cfo_hw_rad, snr_db, H=None):
         sigma = np.sqrt(p / 10 ** (snr_db / 10) / 2)
         out += sigma * (rng.standard_normal(out.shape) + 1j * rng.standard_normal(out.shape))
     return out.astype(np.complex64)
+
+
+def sync_window(rng, O, name, S_win, starts, cfo_dect_rad, snr_db=30.0, n_rx=None, seed_bits=None):
+    """One sync window (complex64 [n_rx, S_win]) holding oracle-TX packets of configuration `name`
+    starting at the hw-sample offsets `starts` (each with its own random N_RX x N_TX mixing), CFO
+    cfo_dect_rad per DECT-rate sample (the TX mixer applies it at the hw rate), AWGN at snr_db
+    relative to the packet power. Returns (window, [(pcc_d, pdc_d, network_id, plcf_type)])."""
+    psd, cfgt = CONFIGS[name]
+    cf = O.cfg(cfgt[0], cfgt[1], os_min=cfgt[3], L=cfgt[4], M=cfgt[5])
+    ps = O.psdef(*psd)
+    sz = O.packet_sizes(ps)
+    n_rx = n_rx or cfgt[2]
+    S_slot = O.dims(cf, ps)["N_packet_os_rs"]
+    win = np.zeros((n_rx, S_win), np.complex128)
+    meta, p_sig = [], []
+    for i, st in enumerate(starts):
+        pcc = rng.integers(0, 256, 25, dtype=np.uint8)
+        pdc = rng.integers(0, 256, (sz["G"] + 7) // 8, dtype=np.uint8)
+        nid, pt = 100 + i % 6, 1 + i % 2
+        x, _ = O.tx(cf, ps, pcc, pdc, S_slot, network_id=nid, plcf_type=pt,
+                    phase_inc=cfo_dect_rad * cfgt[5] / cfgt[4])
+        H = mixing_matrix(rng, n_rx, x.shape[0])
+        y = H @ x
+        n = min(S_slot, S_win - st)
+        win[:, st:st + n] += y[:, :n]
+        p_sig.append(np.mean(np.abs(y[:, : S_slot // 2]) ** 2))
+        meta.append((pcc, pdc, nid, pt))
+    if snr_db is not None:
+        p = np.mean(p_sig) if p_sig else 0.05
+        sigma = np.sqrt(p / 10 ** (snr_db / 10) / 2)
+        win += sigma * (rng.standard_normal(win.shape) + 1j * rng.standard_normal(win.shape))
+    return win.astype(np.complex64), meta

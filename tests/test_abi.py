@@ -61,6 +61,7 @@ def test_null_arguments():
     assert L.dnrp_compute_packet_sizes(None, None, None) == -1
     assert L.dnrp_tx_batch(None, None, 0, None, None, None, 0, None, 0, None) == -1
     assert L.dnrp_sync(None, None) == -1
+    assert L.dnrp_rx_sync_batch(None, None, 0, None, 0, 0, 0, None, None, None) == -1
 
 
 def _grid():

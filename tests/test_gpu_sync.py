@@ -1,0 +1,151 @@
+"""GPU synchronisation parity: dnrp_rx_sync_batch (kernels/sync.hip) against the oracle restatement
+of sync_chunk_t::search() (oracle/oracle_sync.cpp) on identical windows.
+
+Tolerances: found flags, report count, detection antenna and time, N_eff_TX and the fine peak time
+exact; coarse peak time within 1 DECT sample (smoothed-metric plateau: float vs double sums can
+move the last maximum by one position); fractional CFO within 2e-6 rad per DECT sample; RMS and
+metrics within 1e-3 relative. Then the synchronised chain: GPU sync -> GPU PCC/PDC demodulation
+against the oracle RX started from the oracle's own sync report (int16 LLRs within 1 LSB).
+"""
+import numpy as np
+import pytest
+
+import oracle_py as O
+import phy_fixtures as F
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+def _phy(name, max_batch=8):
+    import dnrp
+    ps, cf = F.CONFIGS[name]
+    u_max, b_max, ntx, os_min, L, M = cf
+    phy = dnrp.Phy(u_max, b_max, ntx, os_min, L, M, max_batch=max_batch)
+    for nid in range(100, 106):
+        phy.add_network_id(nid)
+    return phy
+
+
+def _compare(g, o, where):
+    assert int(g["found"]) == o["found"] == 1, where
+    assert int(g["detection_ant_idx"]) == o["det_ant"], where
+    assert int(g["detection_time_local"]) == o["det_time"], (where, int(g["detection_time_local"]), o["det_time"])
+    assert abs(int(g["coarse_peak_time_local"]) - o["coarse_local"]) <= 1, (where, int(g["coarse_peak_time_local"]),
+                                                                            o["coarse_local"])
+    assert int(g["N_eff_TX"]) == o["N_eff_TX"], where
+    assert int(g["fine_peak_time"]) == o["fine_64"], (where, int(g["fine_peak_time"]), o["fine_64"])
+    assert abs(float(g["cfo_fractional_rad"]) - o["cfo_frac"]) < 2e-6, (where, float(g["cfo_fractional_rad"]),
+                                                                         o["cfo_frac"])
+    np.testing.assert_allclose(g["detection_metric"], o["det_metric"], rtol=1e-3)
+    np.testing.assert_allclose(g["coarse_peak_array"], o["coarse_metric"], rtol=1e-3, atol=1e-6)
+    np.testing.assert_allclose(g["rms_array"], o["rms"], rtol=1e-3, atol=1e-7)
+    nt = int(np.count_nonzero(o["xc_metric"]))
+    np.testing.assert_allclose(g["fine_peak_metric"][:nt], o["xc_metric"][:nt], rtol=1e-3)
+
+
+def _run(phy, sc, windows, max_reports, stream_layout=False):
+    """windows: list of complex64 [n_ant, S]. Returns the GPU results [n, max_reports]."""
+    dev = torch.device("cuda:0")
+    n = len(windows)
+    n_ant, S = windows[0].shape
+    if stream_layout:  # per-antenna continuous streams, window w at w*S
+        streams = np.concatenate(windows, axis=1)  # [n_ant, n*S]
+        t = torch.from_numpy(np.ascontiguousarray(streams).view(np.float32).reshape(n_ant, n * S, 2)).to(dev)
+        res, cnt = phy.rx_sync_batch(sc, t, n, S, S, n * S)
+    else:
+        t = torch.from_numpy(np.stack(windows).view(np.float32).reshape(n, n_ant, S, 2)).to(dev)
+        res, cnt = phy.rx_sync_batch(sc, t, n, S, n_ant * S, S)
+    phy.sync()
+    return res, cnt
+
+
+@pytest.mark.parametrize("name,S_win,chunk,stream_layout", [
+    ("C4", 20480, 4096, False), ("C3", 20480, 4096, True), ("C2", 1500, 400, False)])
+def test_sync_parity(name, S_win, chunk, stream_layout):
+    import dnrp
+    rng = np.random.default_rng(21)
+    psd, cfgt = F.CONFIGS[name]
+    n_ant = cfgt[2]
+    phy = _phy(name)
+    windows, truth = [], []
+    for i in range(5):
+        start = int(rng.integers(0.15 * S_win, 0.3 * S_win))
+        cfo = rng.uniform(-1.75, 1.75) * 2 * np.pi / (64 * psd[1])
+        win, _ = F.sync_window(rng, O, name, S_win, [start], cfo)
+        windows.append(win)
+        truth.append((start, cfo))
+    noise, _ = F.sync_window(rng, O, name, S_win, [], 0.0)
+    windows.append(noise)
+    sc = dnrp.SyncCfg(psd[0], psd[1], n_ant, chunk, 2)
+    res, cnt = _run(phy, sc, windows, 2, stream_layout)
+    osc = O.sync_cfg(psd[0], psd[1], L=cfgt[4], M=cfgt[5], n_ant=n_ant, chunk_len=chunk)
+    for w, win in enumerate(windows):
+        ref = O.sync(osc, win, max_reports=2)
+        assert int(cnt[w]) == len(ref), (w, int(cnt[w]), len(ref))
+        for k, o in enumerate(ref):
+            _compare(res[w, k], o, (name, w, k))
+        for k in range(len(ref), 2):
+            assert int(res[w, k]["found"]) == 0
+        if w < len(truth):
+            assert int(res[w, 0]["fine_peak_time"]) == truth[w][0]
+
+
+def test_sync_two_packets_per_window():
+    import dnrp
+    rng = np.random.default_rng(23)
+    phy = _phy("C2")
+    windows = [F.sync_window(rng, O, "C2", 3000, [300 + 7 * i, 1650 - 5 * i], 0.4 * (i - 1) * 2 * np.pi / 64)[0]
+               for i in range(3)]
+    sc = dnrp.SyncCfg(1, 1, 1, 3000, 4)
+    res, cnt = _run(phy, sc, windows, 4)
+    osc = O.sync_cfg(1, 1, n_ant=1, chunk_len=3000)
+    for w, win in enumerate(windows):
+        ref = O.sync(osc, win, max_reports=4)
+        assert len(ref) == 2 and int(cnt[w]) == 2
+        for k, o in enumerate(ref):
+            _compare(res[w, k], o, (w, k))
+
+
+def test_sync_then_demodulate_c4():
+    """GPU sync -> GPU RX on the synchronised windows vs the oracle RX from the oracle sync report."""
+    import dnrp
+    rng = np.random.default_rng(25)
+    name = "C4"
+    psd, cfgt = F.CONFIGS[name]
+    phy = _phy(name)
+    ps = dnrp.psdef(*psd)
+    sz = phy.packet_sizes(ps)
+    S = sz["N_samples_packet_os_rs"]
+    pre = 2400
+    windows, metas = [], []
+    for i in range(2):
+        cfo = rng.uniform(-1.75, 1.75) * 2 * np.pi / 1024
+        win, meta = F.sync_window(rng, O, name, S, [pre + int(rng.integers(0, 32))], cfo)
+        windows.append(win)
+        metas.append(meta[0])
+    sc = dnrp.SyncCfg(psd[0], psd[1], 4, 89280, 1)
+    res, cnt = _run(phy, sc, windows, 1)
+    assert list(cnt) == [1, 1]
+    dev = torch.device("cuda:0")
+    iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(2, 4, S, 2)).to(dev)
+    reps = dnrp.sync_reports(res[:, 0])
+    pcc_llr = torch.zeros((2, 196), dtype=torch.int16, device=dev)
+    pdc_llr = torch.zeros((2, sz["G"]), dtype=torch.int16, device=dev)
+    phy.rx_pcc_batch(reps, iq, pcc_llr)
+    phy.rx_pdc_batch(ps, [dnrp.PdcReq(m[2], m[3]) for m in metas], pdc_llr)
+    phy.sync()
+    g_pcc, g_pdc = pcc_llr.cpu().numpy(), pdc_llr.cpu().numpy()
+    ocf = O.cfg(cfgt[0], cfgt[1], os_min=cfgt[3], L=cfgt[4], M=cfgt[5])
+    osc = O.sync_cfg(psd[0], psd[1], L=cfgt[4], M=cfgt[5], n_ant=4, chunk_len=89280)
+    for i, win in enumerate(windows):
+        o = O.sync(osc, win, max_reports=1)[0]
+        assert o["fine_64"] == int(res[i, 0]["fine_peak_time"])
+        r = O.rx(ocf, O.psdef(*psd), win, o["fine_64"], float(np.float32(o["cfo_frac"])), metas[i][2], metas[i][3])
+        d_pdc = np.abs(g_pdc[i].astype(np.int32) - r["pdc_llr"].astype(np.int32))
+        d_pcc = np.abs(g_pcc[i].astype(np.int32) - r["pcc_llr"].astype(np.int32))
+        assert d_pcc.max() <= 1 and d_pdc.max() <= 2, (d_pcc.max(), d_pdc.max())
+        assert np.mean(d_pdc > 1) < 1e-4
+        bits = np.unpackbits(metas[i][1])[: sz["G"]]
+        assert np.mean((g_pdc[i] > 0).astype(np.uint8) != bits) < 1e-3
