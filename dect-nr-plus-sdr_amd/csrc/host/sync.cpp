@@ -179,6 +179,7 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     a.win_stride = win_stride;
     a.ant_stride = ant_stride;
     a.S_win = S_win;
+    a.n_win = n;
     a.max_reports = sc->max_reports;
     a.Ltx = c.L;
     a.Mtx = c.M;

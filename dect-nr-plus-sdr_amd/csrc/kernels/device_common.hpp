@@ -28,6 +28,40 @@ __device__ __forceinline__ float2 phasor(double phi) {
     return make_float2(__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r));
 }
 
+// Copy x[q0 + i], i in [0, n), into dst[i] (zero outside [0, S)) with U loads in flight per thread
+// (tid / nt: this thread's index in the copying group, a wavefront or the workgroup). A plain
+// strided loop issues one load and waits for it every iteration.
+template <int U, class T, class F>
+__device__ __forceinline__ void stage_gen(T* dst, uint32_t n, uint32_t tid, uint32_t nt, F&& load) {
+    for (uint32_t base = 0; base < n; base += nt * U) {
+        T v[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t i = base + tid + j * nt;
+            v[j] = i < n ? load(i) : T{};
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t i = base + tid + j * nt;
+            if (i < n) dst[i] = v[j];
+        }
+    }
+}
+
+template <int U>
+__device__ __forceinline__ void stage_span(float2* dst, const float2* __restrict__ x, int64_t q0, uint32_t n, int64_t S,
+                                           uint32_t tid, uint32_t nt) {
+    stage_gen<U>(dst, n, tid, nt, [&](uint32_t i) {
+        const int64_t q = q0 + i;
+        return (q >= 0 && q < S) ? x[q] : make_float2(0.f, 0.f);
+    });
+}
+
+template <int U, class T>
+__device__ __forceinline__ void stage_copy(T* dst, const T* __restrict__ src, uint32_t n, uint32_t tid, uint32_t nt) {
+    stage_gen<U>(dst, n, tid, nt, [&](uint32_t i) { return src[i]; });
+}
+
 // FFT plan passed by value: radix sequence (each 2, 3 or 4), product = N
 struct fft_plan {
     uint32_t N;

@@ -168,7 +168,7 @@ struct sync_args {
     uint32_t n_uw;
     const float2* iq;                          // window w, antenna a: iq + w*win_stride + a*ant_stride
     uint64_t win_stride, ant_stride;
-    uint32_t S_win;
+    uint32_t S_win, n_win;
     float* P;                                  // [n][n_ant][n_steps] step powers
     float2* Cs;                                // [n][n_ant][n_steps] step correlations
     uint32_t max_reports;

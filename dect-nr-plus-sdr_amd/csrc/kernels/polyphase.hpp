@@ -44,6 +44,32 @@ struct pp_block {
             }
         }
     }
+
+    // B blocks per lane sharing every tap-row read: block b's window starts at xw[b].
+    // LDS bytes per FMA fall from (16 LP/4 + 8) / (2L) to (16 LP/4 + 8 B) / (2 L B).
+    template <int B>
+    __device__ static __forceinline__ void run_multi(const float2* const (&xw)[B], const float* g, float2 (&y)[B][L]) {
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int k = 0; k < L; ++k) y[b][k] = make_float2(0.f, 0.f);
+        const v4f* rows = reinterpret_cast<const v4f*>(g);
+        for (int i = 0; i < W; ++i) {
+            v4f t[LP / 4];
+#pragma unroll
+            for (int c = 0; c < LP / 4; ++c) t[c] = rows[i * (LP / 4) + c];
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const float2 xv = xw[b][i];
+#pragma unroll
+                for (int k = 0; k < L; ++k) {
+                    const float tv = t[k / 4][k % 4];
+                    y[b][k].x = fmaf(xv.x, tv, y[b][k].x);
+                    y[b][k].y = fmaf(xv.y, tv, y[b][k].y);
+                }
+            }
+        }
+    }
 };
 
 }  // namespace dnrp::dev

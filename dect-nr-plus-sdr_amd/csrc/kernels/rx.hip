@@ -28,12 +28,16 @@ __device__ void resample_block(const rx_front_args& A, const float2* __restrict_
     const int64_t p1 = static_cast<int64_t>(t1 / A.L);
     const int64_t q0 = p0 - static_cast<int64_t>(A.hl);
     const uint32_t n_in = static_cast<uint32_t>(p1 - q0 + 1);
-    for (uint32_t i = threadIdx.x; i < n_in; i += blockDim.x) {
-        const int64_t q = q0 + i;  // input index relative to the fine peak
-        const int64_t g = fine_peak + q;
-        float2 v = make_float2(0.f, 0.f);
-        if (q >= 0 && g >= 0 && g < static_cast<int64_t>(A.S_in)) v = x[g];
-        inbuf[i] = v;
+    // input index q relative to the fine peak, zero history before it: valid for q in
+    // [max(0, -fine_peak), S_in - fine_peak)
+    if (fine_peak >= 0) {
+        stage_span<8>(inbuf, x + fine_peak, q0, n_in, static_cast<int64_t>(A.S_in) - fine_peak, threadIdx.x, blockDim.x);
+    } else {
+        for (uint32_t i = threadIdx.x; i < n_in; i += blockDim.x) {
+            const int64_t q = q0 + i;
+            const int64_t g = fine_peak + q;
+            inbuf[i] = (q >= 0 && g >= 0 && g < static_cast<int64_t>(A.S_in)) ? x[g] : make_float2(0.f, 0.f);
+        }
     }
     __syncthreads();
     const uint32_t dT = blockDim.x * A.M, dp = dT / A.L, dph = dT % A.L;
@@ -89,7 +93,7 @@ __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
     float2* Ys = twl + Nd;               // [N_RX][Nf]
     float* taps = reinterpret_cast<float*>(Ys + A.N_RX * Nf);
     for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) twl[i] = A.tw[i];
-    for (uint32_t i = threadIdx.x; i < (A.hl + 1) * A.L; i += blockDim.x) taps[i] = A.taps[i];
+    stage_copy<4>(taps, A.taps, (A.hl + 1) * A.L, threadIdx.x, blockDim.x);
     const rx_pkt_in in = A.pin[pkt];
     const uint32_t P = n_stf / A.n_pattern;
     double cs_re = 0.0, cs_im = 0.0;
@@ -207,11 +211,11 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
     float2* inbuf = rot + Nf;                  // input span of a pass
     const uint32_t in_cap = LR > 0 ? rx_in_cap(Nd, A.CP, LR, MR, PB::W) : (Nd * A.M) / A.L + A.hl + 4;
     float* taps = reinterpret_cast<float*>(inbuf + in_cap);
-    for (uint32_t i = threadIdx.x; i < Nd; i += RX_THREADS) twl[i] = A.tw[i];
+    stage_copy<4>(twl, A.tw, Nd, threadIdx.x, RX_THREADS);
     if (LR == 0)
         for (uint32_t i = threadIdx.x; i < (A.hl + 1) * A.L; i += RX_THREADS) taps[i] = A.taps[i];
     else
-        for (uint32_t i = threadIdx.x; i < A.npp; i += RX_THREADS) taps[i] = A.taps_pp[i];
+        stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, RX_THREADS);
     const rx_pkt_in in = A.pin[pkt];
     const rx_pkt_state S = A.st[pkt];
     const uint32_t n_stf = A.STF_CP + Nd;
@@ -234,10 +238,7 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
             const int64_t in0 = static_cast<int64_t>(A.p_star) + int64_t(MR) * qb0 - HLR;
             const uint32_t n_in = static_cast<uint32_t>(MR * (qb1 - 1 - qb0) + PB::W);
             const float2* src = x + in.fine_peak + in0;
-            for (uint32_t i = threadIdx.x; i < n_in; i += RX_THREADS) {
-                const int64_t qi = in0 + i;
-                inbuf[i] = (qi >= 0 && qi < q_hi) ? src[i] : make_float2(0.f, 0.f);
-            }
+            stage_span<8>(inbuf, src - in0, in0, n_in, q_hi, threadIdx.x, RX_THREADS);
             __syncthreads();
             for (int q = qb0 + static_cast<int>(threadIdx.x); q < qb1; q += RX_THREADS) {
                 const int mb = static_cast<int>(A.m_star) + LR * q;
@@ -320,8 +321,8 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     float2* twl = smem;                                  // Nd
     float* taps = reinterpret_cast<float*>(twl + Nd);    // npp
     float2* reg0 = twl + Nd + (A.npp + 1) / 2;           // RXW_SYMS regions
-    for (uint32_t i = threadIdx.x; i < Nd; i += RX_THREADS) twl[i] = A.tw[i];
-    for (uint32_t i = threadIdx.x; i < A.npp; i += RX_THREADS) taps[i] = A.taps_pp[i];
+    stage_copy<4>(twl, A.tw, Nd, threadIdx.x, RX_THREADS);
+    stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, RX_THREADS);
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t l = A.sym_first + blk * RXW_SYMS + w;
     const bool active = l < A.sym_first + A.sym_count;
@@ -337,11 +338,7 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     // valid input window relative to the fine peak: history is zero before it (rx_synced.cpp:711-740)
     const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak;
     const float2* src = A.iq + (size_t(pkt) * A.N_RX + a) * A.S_in + in.fine_peak + in0;
-    if (active)
-        for (uint32_t i = lane; i < n_in; i += 64) {
-            const int64_t qi = in0 + i;
-            R[i] = (qi >= 0 && qi < q_hi) ? src[i] : make_float2(0.f, 0.f);
-        }
+    if (active) stage_span<20>(R, src - in0, in0, n_in, q_hi, lane, 64);
     __syncthreads();  // twiddles / taps (and this wave's own staging)
     if (!active) return;
     // resampling + phase-continuous mixer, outputs in registers

@@ -39,10 +39,7 @@ __device__ void sync_resample(const sync_args& A, const float2* __restrict__ x, 
                               float2* stage, float2* dst, const float* taps) {
     const int64_t S = A.S_win;
     if constexpr (LR == 1) {
-        for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-            const int64_t y = y0 + i;
-            dst[i] = (y >= 0 && y < S) ? x[y] : make_float2(0.f, 0.f);
-        }
+            stage_span<8>(dst, x, y0, cnt, S, threadIdx.x, blockDim.x);
         __syncthreads();
     } else if constexpr (LR == 0) {  // generic L/M (os_min 4/8): direct FIR per output
         for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
@@ -69,10 +66,7 @@ __device__ void sync_resample(const sync_args& A, const float2* __restrict__ x, 
         const int64_t q0 = floordiv(y0 - ms, LR), q1 = floordiv(y0 + cnt - ms + LR - 1, LR);
         const int64_t in0 = static_cast<int64_t>(A.p_star) + MR * q0 - HLR;
         const uint32_t n_in = static_cast<uint32_t>(MR * (q1 - 1 - q0) + PB::W);
-        for (uint32_t i = threadIdx.x; i < n_in; i += blockDim.x) {
-            const int64_t q = in0 + i;
-            stage[i] = (q >= 0 && q < S) ? x[q] : make_float2(0.f, 0.f);
-        }
+        stage_span<8>(stage, x, in0, n_in, S, threadIdx.x, blockDim.x);
         __syncthreads();
         for (int64_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
             float2 yv[LR];
@@ -111,7 +105,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_steps_kernel(sync_args A) {
     const uint32_t cnt = (s1 - s0) * A.step + A.pattern;
     float2* stage = lb + (cnt + 1) / 2 * 2;
     if (LR > 1)
-        for (uint32_t i = threadIdx.x; i < A.npp; i += blockDim.x) taps[i] = A.taps_pp[i];
+        stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, blockDim.x);
     const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
     sync_resample<LR, MR, HLR>(A, x, y0, cnt, stage, lb, taps);
     // step s = s0 + tid/4, quarter tid%4 of its samples; reduce over the 4 lanes
@@ -141,6 +135,105 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_steps_kernel(sync_args A) {
         const size_t o = (static_cast<size_t>(w) * A.n_ant + a) * A.n_steps + s;
         A.P[o] = pw;
         A.Cs[o] = c;
+    }
+}
+
+// ---- pp resampler path: one wavefront per range of SYNC_WB_STEPS-ish steps, no workgroup barrier
+// after the table load. The wave stages its hw-rate input span in its own LDS region, resamples it
+// with B polyphase blocks per lane (pp_block::run_multi: one tap-row read serves B blocks, which
+// keeps the LDS traffic per FMA under the 128 B/clk/CU the VALU needs), writes the outputs back into
+// the region and sums the steps from there.
+constexpr int SYNC_WB = 4;  // blocks per lane
+
+__host__ __device__ inline uint32_t sync_wave_steps(uint32_t L, uint32_t step, uint32_t pattern) {
+    return (64u * SYNC_WB * L - pattern - 2 * L) / step;  // steps whose span (+ lookback) fits 64 B blocks
+}
+__host__ __device__ inline uint32_t sync_wave_region(uint32_t L, uint32_t M, uint32_t hl) {  // float2 per wave
+    const uint32_t W = hl + 1 + ((L - 1) * M) / L;
+    return (M * (64 * SYNC_WB - 1) + W + 1) / 2 * 2;
+}
+
+template <int LR, int MR, int HLR, int WPG>
+__global__ void __launch_bounds__(64 * WPG) sync_steps_wave_kernel(sync_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    using PB = pp_block<LR, MR, HLR>;
+    float* taps = reinterpret_cast<float*>(smem);
+    const uint32_t tap_f2 = (A.npp + 3) / 4 * 2;
+    const uint32_t region = sync_wave_region(LR, MR, HLR);
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    float2* R = smem + tap_f2 + wv * region;
+    const uint32_t sw = sync_wave_steps(LR, A.step, A.pattern);
+    const uint32_t parts = (A.n_steps + sw - 1) / sw;
+    const uint32_t gw = blockIdx.x * WPG + wv;
+    const uint32_t part = gw % parts;
+    const uint32_t a = (gw / parts) % A.n_ant;
+    const uint32_t w = gw / (parts * A.n_ant);
+    const uint32_t s0 = part * sw, s1 = min(s0 + sw, A.n_steps);
+    const int64_t y0 = static_cast<int64_t>(s0) * A.step - A.pattern;
+    const uint32_t cnt = (s1 - s0) * A.step + A.pattern;
+    const int64_t ms = A.m_star;
+    const int64_t q0 = floordiv(y0 - ms, LR), q1 = floordiv(y0 + cnt - ms + LR - 1, LR);
+    const int64_t in0 = static_cast<int64_t>(A.p_star) + MR * q0 - HLR;
+    const uint32_t n_in = static_cast<uint32_t>(MR * (q1 - 1 - q0) + PB::W);
+    const bool live = w < A.n_win;
+    if (live) {
+        const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
+        const int64_t S = A.S_win;
+        stage_span<24>(R, x, in0, n_in, S, lane, 64);
+    }
+    stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, blockDim.x);
+    __syncthreads();
+    if (!live) return;
+    float2 y[SYNC_WB][LR];
+    const float2* xw[SYNC_WB];
+#pragma unroll
+    for (int b = 0; b < SYNC_WB; ++b) xw[b] = R + MR * (lane + 64 * b);
+    PB::template run_multi<SYNC_WB>(xw, taps, y);
+    __builtin_amdgcn_wave_barrier();
+    const int64_t nblk = q1 - q0;
+#pragma unroll
+    for (int b = 0; b < SYNC_WB; ++b) {
+        const int64_t j = lane + 64 * b;
+        if (j < nblk) {
+            const int64_t mb = ms + LR * (q0 + j);
+#pragma unroll
+            for (int k = 0; k < LR; ++k) {
+                const int64_t idx = mb + k - y0;
+                if (idx >= 0 && idx < static_cast<int64_t>(cnt)) R[idx] = (mb + k >= 0) ? y[b][k] : make_float2(0.f, 0.f);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // steps: 32 per round, half of each step's samples per lane (reduced over the lane pair). Each
+    // lane walks its half starting at its own rotation (j + lane) mod half, so the 32 lanes of a
+    // ds_read_b64 half-wave hit 32 different bank pairs (step starts are 0 mod 64 banks).
+    const uint32_t half = A.step >> 1, h = lane & 1u, rot = lane % half;
+    for (uint32_t sb = s0; sb < s1; sb += 32) {
+        const uint32_t s = sb + (lane >> 1);
+        float pw = 0.f;
+        float2 c = make_float2(0.f, 0.f);
+        if (s < s1) {
+            const uint32_t i0 = (s - s0) * A.step + A.pattern + h * half;
+            for (uint32_t j = 0; j < half; ++j) {
+                uint32_t jj = j + rot;
+                if (jj >= half) jj -= half;
+                const float2 v = R[i0 + jj];
+                pw = fmaf(v.x, v.x, fmaf(v.y, v.y, pw));
+                if (s >= 4) {
+                    const float2 u = R[i0 + jj - A.pattern];
+                    c.x = fmaf(u.x, v.x, fmaf(u.y, v.y, c.x));
+                    c.y = fmaf(u.y, v.x, fmaf(-u.x, v.y, c.y));
+                }
+            }
+        }
+        pw += __shfl_xor(pw, 1);
+        c.x += __shfl_xor(c.x, 1);
+        c.y += __shfl_xor(c.y, 1);
+        if (s < s1 && h == 0) {
+            const size_t o = (static_cast<size_t>(w) * A.n_ant + a) * A.n_steps + s;
+            A.P[o] = pw;
+            A.Cs[o] = c;
+        }
     }
 }
 
@@ -224,10 +317,14 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
     const uint32_t P = A.pattern, yoff = A.stf_len + SYNC_PAD_PEAK;  // lbuf index of r0
     const uint32_t nprod = region - P, nsc = (nprod + 15) / 16, nsp = (region + 15) / 16;
     // segment sums: products prod(y) = lb[y-P] conj(lb[y]) indexed from lbuf index P; powers from 0
+    // (each thread starts its 16-sample segment at its own rotation: segment starts are 32 banks
+    // apart, so an unrotated walk would put a half-wave on two bank pairs)
     for (uint32_t g = threadIdx.x; g < nsc + nsp; g += blockDim.x) {
         if (g < nsc) {
             double sx = 0.0, sy = 0.0;
-            for (uint32_t j = 16 * g; j < min(16 * g + 16, nprod); ++j) {
+            for (uint32_t t = 0; t < 16; ++t) {
+                const uint32_t j = 16 * g + ((t + g) & 15u);
+                if (j >= nprod) continue;
                 const float2 c = cmulc(lbuf[j], lbuf[j + P]);
                 sx += c.x;
                 sy += c.y;
@@ -236,7 +333,10 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
         } else {
             const uint32_t h = g - nsc;
             double sp = 0.0;
-            for (uint32_t j = 16 * h; j < min(16 * h + 16, region); ++j) sp += cnorm(lbuf[j]);
+            for (uint32_t t = 0; t < 16; ++t) {
+                const uint32_t j = 16 * h + ((t + h) & 15u);
+                if (j < region) sp += cnorm(lbuf[j]);
+            }
             L.ckp[h] = sp;
         }
     }
@@ -395,7 +495,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
     pl.ckp = reinterpret_cast<double*>(pl.ckc + (region + 15) / 16 + 2);
     pl.met = pl.ckp + (region + 15) / 16 + 2;
     if (LR > 1)
-        for (uint32_t i = threadIdx.x; i < A.npp; i += blockDim.x) taps[i] = A.taps_pp[i];
+        stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, blockDim.x);
     __syncthreads();
     const float* Pw = A.P + static_cast<size_t>(w) * A.n_ant * A.n_steps;
     const float2* Cw = A.Cs + static_cast<size_t>(w) * A.n_ant * A.n_steps;
@@ -635,7 +735,17 @@ size_t sync_detect_lds(const sync_args& a) {
             hipLaunchKernelGGL((KERNEL<0, 0, 0>), GRID, dim3(SYNC_THREADS), LDS, st, a);   \
     } while (0)
 
+constexpr int SYNC_WPG = 2;  // waves per workgroup of the wave kernel
+
 hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
+    if (a.L == 9 && a.M == 10 && a.hl == 24) {
+        const uint32_t sw = sync_wave_steps(9, a.step, a.pattern);
+        const uint32_t waves = n * a.n_ant * ((a.n_steps + sw - 1) / sw);
+        const size_t lds = (a.npp + 3) / 4 * 2 * sizeof(float2) + SYNC_WPG * size_t(sync_wave_region(9, 10, 24)) * sizeof(float2);
+        hipLaunchKernelGGL((sync_steps_wave_kernel<9, 10, 24, SYNC_WPG>), dim3((waves + SYNC_WPG - 1) / SYNC_WPG),
+                           dim3(64 * SYNC_WPG), lds, st, a);
+        return hipGetLastError();
+    }
     const uint32_t ntile = (a.n_steps + SYNC_TILE_STEPS - 1) / SYNC_TILE_STEPS;
     const uint32_t cnt = SYNC_TILE_STEPS * a.step + a.pattern;
     const size_t lds = (a.npp + 3) / 4 * 2 * sizeof(float2) + (cnt + 1) / 2 * 2 * sizeof(float2) +

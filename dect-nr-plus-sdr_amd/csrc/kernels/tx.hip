@@ -121,7 +121,7 @@ struct tx_wg {
 };
 
 template <bool WAVE>
-__device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem) {
+__device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem, uint32_t (*rc)[16] = nullptr) {
     tx_wg w;
     w.A = &A;
     const uint32_t run = blockIdx.x % A.n_runs, pa = blockIdx.x / A.n_runs;
@@ -156,19 +156,74 @@ __device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem) {
 
     // ---- staging: tables, PCC symbols, beamforming row, taps, descrambled PDC bytes
     const uint8_t* dpcc = A.pcc_d + size_t(w.pkt) * 25;
-    for (uint32_t i = threadIdx.x; i < w.Nd; i += TX_THREADS) w.twl[i] = A.tw[i];
-    for (uint32_t i = threadIdx.x; i < (1u << A.N_bps); i += TX_THREADS) w.qtab[i] = A.qam[i];
+    if constexpr (WAVE) {
+        // wave path (N_b_DFT_os = 1024): every global load of the staging phase, the symbol's
+        // cell codes included, is issued before the first LDS store -> one memory round trip
+        const uint32_t t = threadIdx.x;
+        const uint32_t b = t >> 6, lane = t & 63u, l = w.s0 + b;
+        if (rc)
+#pragma unroll
+            for (int m = 0; m < 16; ++m) (*rc)[m] = b < w.nsl ? w.code(l, lane + 64 * m) : 0u;
+        float2 r_tw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r_tw[j] = A.tw[t + TX_THREADS * j];
+        const uint32_t nq = 1u << A.N_bps;
+        const float2 r_q = t < nq ? A.qam[t] : make_float2(0.f, 0.f);
+        uint32_t r_pcc = 0;
+        if (t < 98) r_pcc = uint32_t(dpcc[(2 * t) >> 3] ^ A.pcc_seq[(2 * t) >> 3]);
+        const float2 r_w = t < A.N_TS ? A.W[(w.P.codebook * A.N_TX + w.ant) * A.N_TS + t] : make_float2(0.f, 0.f);
+        float r_h[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t i = t + TX_THREADS * j;
+            r_h[j] = i < A.npp ? A.taps_pp[i] : 0.f;
+        }
+        uint32_t r_sb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t i = t + TX_THREADS * j, g = w.sbyte0 + i;
+            r_sb[j] = (i < A.stage_bytes && g < w.pdc_bytes) ? uint32_t(w.dpdc[g] ^ w.cpdc[g]) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w.twl[t + TX_THREADS * j] = r_tw[j];
+        if (t < nq) w.qtab[t] = r_q;
+        if (t < 98) {  // QPSK (TS 36.211 7.1.2): (1 - 2 b0, 1 - 2 b1) / sqrt(2)
+            const uint32_t q = bits_of(r_pcc, 0u, 2 * t, 2);
+            w.pccs[t] = make_float2((q & 2u) ? -0.70710678f : 0.70710678f, (q & 1u) ? -0.70710678f : 0.70710678f);
+        }
+        if (t < A.N_TS) w.wrow[t] = r_w;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (t + TX_THREADS * j < A.npp) w.hpl[t + TX_THREADS * j] = r_h[j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (t + TX_THREADS * j < A.stage_bytes) w.sb[t + TX_THREADS * j] = static_cast<uint8_t>(r_sb[j]);
+        // tails beyond the register batch (not reached by the shipped configurations)
+        for (uint32_t i = t + 2 * TX_THREADS; i < A.npp; i += TX_THREADS) w.hpl[i] = A.taps_pp[i];
+        for (uint32_t i = t + 8 * TX_THREADS; i < A.stage_bytes; i += TX_THREADS) {
+            const uint32_t g = w.sbyte0 + i;
+            w.sb[i] = g < w.pdc_bytes ? static_cast<uint8_t>(w.dpdc[g] ^ w.cpdc[g]) : 0u;
+        }
+        return w;
+    }
+    // every copy keeps several loads in flight per thread (stage_gen): a plain strided loop waits
+    // for each load before issuing the next
+    stage_copy<4>(w.twl, A.tw, w.Nd, threadIdx.x, TX_THREADS);
+    stage_copy<1>(w.qtab, A.qam, 1u << A.N_bps, threadIdx.x, TX_THREADS);
     for (uint32_t j = threadIdx.x; j < 98; j += TX_THREADS) {
         const uint32_t bo = (2 * j) >> 3;
         w.pccs[j] = A.qpsk[bits_of(dpcc[bo] ^ A.pcc_seq[bo], 0u, 2 * j, 2)];
     }
     for (uint32_t i = threadIdx.x; i < A.N_TS; i += TX_THREADS)
         w.wrow[i] = A.W[(w.P.codebook * A.N_TX + w.ant) * A.N_TS + i];
-    for (uint32_t i = threadIdx.x; i < A.npp; i += TX_THREADS) w.hpl[i] = A.taps_pp[i];
-    for (uint32_t i = threadIdx.x; i < A.stage_bytes; i += TX_THREADS) {
-        const uint32_t g = w.sbyte0 + i;
-        w.sb[i] = g < w.pdc_bytes ? static_cast<uint8_t>(w.dpdc[g] ^ w.cpdc[g]) : 0u;
-    }
+    stage_copy<2>(w.hpl, A.taps_pp, A.npp, threadIdx.x, TX_THREADS);
+    const uint8_t* __restrict__ dp = w.dpdc;
+    const uint8_t* __restrict__ cp = w.cpdc;
+    const uint32_t sb0 = w.sbyte0, nb = w.pdc_bytes;
+    stage_gen<8>(w.sb, A.stage_bytes, threadIdx.x, TX_THREADS, [&](uint32_t i) {
+        const uint32_t g = sb0 + i;
+        return g < nb ? static_cast<uint8_t>(dp[g] ^ cp[g]) : static_cast<uint8_t>(0u);
+    });
     return w;
 }
 
@@ -199,6 +254,64 @@ __device__ __forceinline__ void tx_resample(const tx_wg& w) {
         const int q_lo = floor_div(static_cast<int>(m_lo) - static_cast<int>(A.m_star), LR);
         const int q_hi = floor_div(static_cast<int>(m_hi) - static_cast<int>(A.m_star) + LR - 1, LR);
         const int idx_max = static_cast<int>(A.lin_len) - PB::W;
+        if (q_hi - q_lo <= 2 * static_cast<int>(TX_THREADS) && m_hi - m_lo <= A.lin_len) {
+            // coalesced stores: the blocks' outputs go through LDS (over the consumed input buffer)
+            // and leave as contiguous 16-B lane stores; a direct store from the block layout would
+            // spread every store instruction over ~40 cache lines (lanes 10 outputs apart)
+            float2 y[2][LR];
+            int mbs[2];
+            {
+                // both blocks of the thread in one pass over the tap rows (pp_block::run_multi);
+                // clamped window starts only occur for outputs that are not stored
+                const float2* xw[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int q = q_lo + static_cast<int>(threadIdx.x) + r * static_cast<int>(TX_THREADS);
+                    const int pb = static_cast<int>(A.p_star) + MR * q;
+                    xw[r] = w.lin + min(max(pb - HLR + lin_off, 0), idx_max);
+                }
+                PB::template run_multi<2>(xw, w.hpl, y);
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int q = q_lo + static_cast<int>(threadIdx.x) + r * static_cast<int>(TX_THREADS);
+                mbs[r] = static_cast<int>(A.m_star) + LR * q;
+                if (q < q_hi) {
+                    if (P.do_mix) {
+                        float2 rot = phasor(P.ph0 + static_cast<double>(mbs[r]) * P.inc);
+#pragma unroll
+                        for (int k = 0; k < LR; ++k) {
+                            y[r][k] = cmul(y[r][k], rot);
+                            rot = cmul(rot, step1);
+                        }
+                    }
+                }
+            }
+            __syncthreads();  // every lane's reads of lin are done
+            float2* ob = w.lin;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int q = q_lo + static_cast<int>(threadIdx.x) + r * static_cast<int>(TX_THREADS);
+                if (q < q_hi) {
+#pragma unroll
+                    for (int k = 0; k < LR; ++k) {
+                        const uint32_t m = static_cast<uint32_t>(mbs[r] + k);
+                        if (m - m_lo < m_hi - m_lo) ob[m - m_lo] = y[r][k];
+                    }
+                }
+            }
+            __syncthreads();
+            const uint32_t n = m_hi - m_lo;
+            const uint32_t head = min(n, (reinterpret_cast<uintptr_t>(out + m_lo) & 15u) ? 1u : 0u);
+            if (threadIdx.x < head) out[m_lo] = ob[0];
+            const uint32_t npair = (n - head) / 2;
+            float4* o4 = reinterpret_cast<float4*>(out + m_lo + head);
+            for (uint32_t i = threadIdx.x; i < npair; i += TX_THREADS) {
+                const float2 a = ob[head + 2 * i], b = ob[head + 2 * i + 1];
+                o4[i] = make_float4(a.x, a.y, b.x, b.y);
+            }
+            if (threadIdx.x == 0 && ((n - head) & 1u)) out[m_hi - 1] = ob[n - 1];
+        } else
         for (int q = q_lo + static_cast<int>(threadIdx.x); q < q_hi; q += TX_THREADS) {
             const int mb = static_cast<int>(A.m_star) + LR * q;
             const int pb = static_cast<int>(A.p_star) + MR * q;        // newest input of output mb
@@ -241,14 +354,11 @@ __device__ __forceinline__ void tx_resample(const tx_wg& w) {
 template <int LR, int MR, int HLR>
 __global__ void __launch_bounds__(TX_THREADS) tx_kernel_wave(tx_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    const tx_wg w = tx_setup<true>(A, smem);
+    uint32_t rc[16];  // cell codes of the wave's 16 bins per lane, loaded with the staging
+    const tx_wg w = tx_setup<true>(A, smem, &rc);
     tx_zero_pads(w);
     const uint32_t b = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t l = w.s0 + b;
-    // cell codes of the wave's 16 bins per lane: independent loads, issued before the barrier
-    uint32_t rc[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) rc[m] = b < w.nsl ? w.code(l, lane + 64 * m) : 0u;
     __syncthreads();
     if (b < w.nsl) {
         float2 v[16];

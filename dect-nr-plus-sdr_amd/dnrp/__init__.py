@@ -213,7 +213,7 @@ class Phy:
     def tx_batch(self, ps, descs, pcc_d, pdc_d, iq_out, stream=None):
         """pcc_d uint8 [n,25], pdc_d uint8 [n,stride], iq_out float32 [n,N_TX,S,2] (torch, device)."""
         n = len(descs)
-        arr = (TxDesc * n)(*descs)
+        arr = descs if isinstance(descs, C.Array) else (TxDesc * n)(*descs)
         _chk(lib().dnrp_tx_batch(self._ctx, C.byref(ps), n, arr, C.c_void_p(pcc_d.data_ptr()),
                                  C.c_void_p(pdc_d.data_ptr()), pdc_d.shape[1], C.c_void_p(iq_out.data_ptr()),
                                  iq_out.shape[2], _stream_ptr(stream)), "dnrp_tx_batch")
@@ -247,7 +247,7 @@ class Phy:
 
     def rx_pdc_batch(self, ps, reqs, pdc_llr, want_report=False, stream=None):
         n = len(reqs)
-        arr = (PdcReq * n)(*reqs)
+        arr = reqs if isinstance(reqs, C.Array) else (PdcReq * n)(*reqs)
         rep = (PdcReport * n)() if want_report else None
         _chk(lib().dnrp_rx_pdc_batch(self._ctx, C.byref(ps), n, arr, C.c_void_p(pdc_llr.data_ptr()),
                                      pdc_llr.shape[1], rep, _stream_ptr(stream)), "dnrp_rx_pdc_batch")

@@ -247,9 +247,11 @@ int oracle_rx(const uint32_t* cfg, const uint32_t* psdef, uint32_t N_RX, const f
 }
 
 // CPU baseline: n_packets TX+RX loopback slot-pairs (float path), one packet per thread at a time
-// (worker_tx_rx_t model). Returns wall seconds, or negative on error.
+// (worker_tx_rx_t model). With sync_chunk > 0 each RX window holds the packet after sync_pre
+// hw samples and is synchronised first (sync_chunk_t::search, float path), RX starting at the
+// found fine peak. Returns wall seconds, or negative on error.
 double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_t n_packets, uint32_t n_threads,
-                             uint64_t seed) {
+                             uint64_t seed, uint32_t sync_pre, uint32_t sync_chunk) {
     try {
         packet_sizes_t q;
         if (!get_packet_sizes(to_psdef(psdef), q)) return -1.0;
@@ -273,9 +275,30 @@ double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_
                 d.plcf_type = 1 + i % 2;
                 std::vector<std::vector<std::complex<float>>> v;
                 tx_packet<float>(c, q, d, pcc.data(), pdc.data(), v, S);
-                for (size_t a = 0; a < v.size(); ++a)
-                    std::memcpy(&iq[2ull * a * S], v[a].data(), S * 8);
-                rx_in_t in{iq.data(), q.tm.N_TX, S, 0, 0.0, d.network_id, d.plcf_type};
+                int64_t fine = 0;
+                if (sync_chunk) {
+                    std::fill(iq.begin(), iq.end(), 0.0f);
+                    for (size_t a = 0; a < v.size(); ++a)
+                        std::memcpy(&iq[2ull * (a * S + sync_pre)], v[a].data(), (S - sync_pre) * 8);
+                    sync_cfg_t sc;
+                    sc.u = q.psdef.u;
+                    sc.b = q.psdef.b;
+                    sc.os_min = c.os_min;
+                    sc.L = c.L;
+                    sc.M = c.M;
+                    sc.N_ant = sc.N_ant_limited = q.tm.N_TX;
+                    sc.chunk_len = sync_chunk;
+                    const auto r = sync_search<float>(sc, iq.data(), S, 1);
+                    if (r.empty()) {
+                        err = 2;
+                        continue;
+                    }
+                    fine = r[0].fine_64;
+                } else {
+                    for (size_t a = 0; a < v.size(); ++a)
+                        std::memcpy(&iq[2ull * a * S], v[a].data(), S * 8);
+                }
+                rx_in_t in{iq.data(), q.tm.N_TX, S, fine, 0.0, d.network_id, d.plcf_type};
                 rx_out_t o;
                 rx_packet<float>(c, q, in, o);
                 if (o.pdc_llr.size() != q.G) err = 1;
@@ -286,7 +309,7 @@ double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_
         for (uint32_t t = 0; t < n_threads; ++t) th.emplace_back(worker, t);
         for (auto& t : th) t.join();
         const auto t1 = std::chrono::steady_clock::now();
-        if (err) return -3.0;
+        if (err) return -3.0 - err;
         return std::chrono::duration<double>(t1 - t0).count();
     } catch (...) {
         return -2.0;

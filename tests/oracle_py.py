@@ -45,7 +45,7 @@ def lib():
         L.oracle_tx.argtypes = [U32P, U32P, U32P, F64P, U8P, U8P, F32P, C.c_uint32, C.c_int]
         L.oracle_rx.argtypes = [U32P, U32P, C.c_uint32, F32P, C.c_uint32, C.c_int64, C.c_double, C.c_uint32,
                                 C.c_uint32, I16P, I16P, C.c_void_p, C.c_void_p, F32P, C.c_int]
-        L.oracle_loopback_timed.argtypes = [U32P, U32P, C.c_uint32, C.c_uint32, C.c_uint64]
+        L.oracle_loopback_timed.argtypes = [U32P, U32P, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
         L.oracle_loopback_timed.restype = C.c_double
         L.oracle_numerology.argtypes = [C.c_uint32, C.c_uint32, U32P, C.POINTER(C.c_double)]
         L.oracle_tm_mode.argtypes = [C.c_uint32, U32P]
@@ -125,8 +125,8 @@ def rx(cf, ps, iq, fine_peak=0, cfo_rad=0.0, network_id=100, plcf_type=1, use_fl
                 cfo_fine=float(meta[8]), sto=float(meta[9]), snr_pcc=float(meta[10]), snr_pdc=float(meta[11]))
 
 
-def loopback_timed(cf, ps, n_packets, n_threads, seed=0xDEC7):
-    return lib().oracle_loopback_timed(cf, ps, n_packets, n_threads, seed)
+def loopback_timed(cf, ps, n_packets, n_threads, seed=0xDEC7, sync_pre=0, sync_chunk=0):
+    return lib().oracle_loopback_timed(cf, ps, n_packets, n_threads, seed, sync_pre, sync_chunk)
 
 
 def pack_bits(bits):
