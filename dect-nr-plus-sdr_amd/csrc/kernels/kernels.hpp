@@ -10,7 +10,8 @@
 namespace dnrp::dev {
 
 // TX cell codes: type in bits 29-31; PCC/PDC: cell index j in bits 0-19 and the transmit
-// diversity pair index ((j >> 1) % mod) in bits 20-23 (host-precomputed); DRS: stream | sign << 3
+// diversity TS pair A | B << 4 of cell j (pair table entry (j >> 1) % mod) in bits 20-27
+// (host-precomputed); DRS: stream | sign << 3
 enum : uint32_t {
     CODE_J_MASK = 0xFFFFFu,
     CODE_PAIR_SHIFT = 20,
@@ -38,6 +39,9 @@ struct tx_args {
     // before them (resampler history) into a linear cyclic-prefixed buffer of lin_len samples
     uint32_t K, n_runs, HP, lin_len, bufB_len;
     uint32_t stage_bytes;  // PDC source bytes of one run staged in LDS (0: read HBM directly)
+    // streaming mode (N_b_DFT_os = 1024): one WG per (packet, antenna) walks symbol groups
+    // {0..g0_last}, then 4 symbols per group; history = the previous group's last HP samples
+    uint32_t stream, g0_last, n_grp;
     uint32_t dbg;          // TEMP: section-skip mask for profiling
     uint32_t pair[12];     // transmit diversity TS pairs, A | B << 4
     const uint32_t* code;

@@ -54,6 +54,7 @@ struct pp_block {
 #pragma unroll
             for (int k = 0; k < L; ++k) y[b][k] = make_float2(0.f, 0.f);
         const v4f* rows = reinterpret_cast<const v4f*>(g);
+#pragma unroll 2
         for (int i = 0; i < W; ++i) {
             v4f t[LP / 4];
 #pragma unroll

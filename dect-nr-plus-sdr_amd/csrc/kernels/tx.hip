@@ -69,7 +69,7 @@ struct tx_wg {
             return (j & 1u) ? make_float2(nb.x, -nb.y) : make_float2(-nb.x, nb.y);
         };
         const uint32_t ty = c & CODE_MASK, j = c & CODE_J_MASK;
-        const uint32_t pr = A->pair[(c >> CODE_PAIR_SHIFT) & 0xFu];
+        const uint32_t pr = (c >> CODE_PAIR_SHIFT) & 0xFFu;  // TS pair A | B << 4 (host-precomputed)
         float2 v = make_float2(0.f, 0.f);
         if (ty == CODE_STF) {
             const uint32_t k = n <= N / 2 ? N / 2 + n : n - A->off_lower;
@@ -103,6 +103,22 @@ struct tx_wg {
         else if (n >= A->off_lower && n < A->off_lower + N / 2)
             k = n - A->off_lower;
         return (n < Nd && k != 0xFFFFFFFFu) ? A->code[size_t(l) * Nf + k] : 0u;
+    }
+
+    // wave path (N_b_DFT_os = 1024): the wave's whole symbol v[m] = x[lane + 64 m] into its CP
+    // layout: 16 plain stores, then the cyclic prefix copied from the symbol's tail and, for the
+    // STF, the cover sequence (ofdm.cpp:62-79, stf.cpp:104-138) in short rolled loops
+    __device__ void put_symbol(uint32_t l, const float2 (&v)[16], uint32_t lane) const {
+        float2* dst = slot(l);
+        const uint32_t cp = l == 0 ? A->STF_CP : A->CP;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) dst[cp + lane + 64 * m] = v[m];
+        __builtin_amdgcn_wave_barrier();  // a wave's LDS accesses complete in order
+        for (uint32_t i = lane; i < cp; i += 64) dst[i] = dst[cp + ((i + 2048u - cp) & 1023u)];
+        if (l == 0) {
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t i = lane; i < cp + 1024; i += 64) dst[i] = cscale(dst[i], k_cover[min(i / A->pattern_len, 8u)]);
+        }
     }
 
     // time-domain sample n of symbol l into its CP layout (ofdm.cpp:62-79, stf.cpp:104-138)
@@ -143,8 +159,9 @@ __device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem, uint32
     w.lin = smem;  // [lin_len] head pad | symbols s0..l_last | tail pad
     float2* p = w.lin + A.lin_len;
     if (!WAVE) p += A.bufB_len;  // block FFT ping-pong partner / output staging
-    w.twl = p;
-    w.qtab = w.twl + w.Nd;
+    // wave path: the FFT reads the (L2/L1-resident) global twiddle table, no LDS copy
+    w.twl = WAVE ? const_cast<float2*>(A.tw) : p;
+    w.qtab = WAVE ? p : w.twl + w.Nd;
     w.pccs = w.qtab + 256;
     w.wrow = w.pccs + 98;
     w.hpl = reinterpret_cast<float*>(w.wrow + 8);
@@ -164,9 +181,6 @@ __device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem, uint32
         if (rc)
 #pragma unroll
             for (int m = 0; m < 16; ++m) (*rc)[m] = b < w.nsl ? w.code(l, lane + 64 * m) : 0u;
-        float2 r_tw[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) r_tw[j] = A.tw[t + TX_THREADS * j];
         const uint32_t nq = 1u << A.N_bps;
         const float2 r_q = t < nq ? A.qam[t] : make_float2(0.f, 0.f);
         uint32_t r_pcc = 0;
@@ -184,8 +198,6 @@ __device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem, uint32
             const uint32_t i = t + TX_THREADS * j, g = w.sbyte0 + i;
             r_sb[j] = (i < A.stage_bytes && g < w.pdc_bytes) ? uint32_t(w.dpdc[g] ^ w.cpdc[g]) : 0u;
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w.twl[t + TX_THREADS * j] = r_tw[j];
         if (t < nq) w.qtab[t] = r_q;
         if (t < 98) {  // QPSK (TS 36.211 7.1.2): (1 - 2 b0, 1 - 2 b1) / sqrt(2)
             const uint32_t q = bits_of(r_pcc, 0u, 2 * t, 2);
@@ -371,11 +383,196 @@ __global__ void __launch_bounds__(TX_THREADS) tx_kernel_wave(tx_args A) {
         }
         float2* xb = w.slot(l);  // the symbol's own slot (>= 1152 samples) is the exchange buffer
         if (!(A.dbg & 2)) wave_fft1024<+1>(v, xb, w.twl, lane);
-#pragma unroll
-        for (int m = 0; m < 16; ++m) w.put(l, lane + 64 * m, v[m]);
+        __builtin_amdgcn_wave_barrier();
+        w.put_symbol(l, v, lane);
     }
     __syncthreads();
     if (!(A.dbg & 4)) tx_resample<LR, MR, HLR>(w);
+}
+
+// ---- N_b_DFT_os = 1024, streaming: one WG per (packet, antenna) walks the packet in symbol
+// groups (group 0 = the STF and the symbols that fill 4 symbol slots, then 4 symbols each). Per
+// group: wave b synthesises symbol b (cell mapping + wave_fft1024 + CP layout) into the linear
+// buffer behind the previous group's last HP samples (resampler history, kept in LDS: no symbol
+// is synthesised twice), then the workgroup resamples + mixes the group's outputs, stages them in
+// LDS and stores them with contiguous 16-B lanes. Tables are staged once per (packet, antenna).
+// Barriers wait for LDS only (global stores drain in the background).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int LR, int MR, int HLR>
+__global__ void __launch_bounds__(TX_THREADS) tx_kernel_stream(tx_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    using PB = pp_block<LR, MR, HLR>;
+    tx_wg w;
+    w.A = &A;
+    w.pkt = blockIdx.x / A.N_TX;
+    w.ant = blockIdx.x % A.N_TX;
+    w.P = A.pk[w.pkt];
+    w.Nd = 1024;
+    w.N = A.N_occ;
+    w.Nf = w.N + 1;
+    w.hl = A.hl;
+    w.len0 = A.STF_CP + w.Nd;
+    w.lenD = A.CP + w.Nd;
+    w.lin = smem;
+    w.twl = const_cast<float2*>(A.tw);
+    w.qtab = w.lin + A.lin_len;
+    w.pccs = w.qtab + 256;
+    w.wrow = w.pccs + 98;
+    w.hpl = reinterpret_cast<float*>(w.wrow + 8);
+    w.sb = reinterpret_cast<uint8_t*>(w.hpl + A.npp);
+    w.dpdc = A.pdc_d + size_t(w.pkt) * A.pdc_stride;
+    w.cpdc = w.P.pdc_seq;
+    w.pdc_bytes = (A.G + 7) / 8;
+    const uint32_t t = threadIdx.x, b = t >> 6, lane = t & 63u;
+    const uint32_t bpc = A.N_SS * A.N_bps;
+    auto set_group = [&](uint32_t g) {
+        w.l_first = g == 0 ? 0u : A.g0_last + 1 + 4 * (g - 1);
+        w.l_last = g == 0 ? A.g0_last : min(w.l_first + 3, A.N_DF);
+        w.s0 = w.l_first;
+        w.nsl = w.l_last - w.l_first + 1;
+        w.base_q = w.bsym(w.l_first);
+        w.last_run = (g + 1 == A.n_grp);
+        w.sbyte0 = (A.pdc_off[max(w.l_first, 1u)] * bpc) >> 3;
+    };
+    auto load_codes = [&](uint32_t (&rc)[16]) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) rc[m] = b < w.nsl ? w.code(w.l_first + b, lane + 64 * m) : 0u;
+    };
+    auto load_bytes = [&](uint32_t (&r)[8]) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t i = t + TX_THREADS * j, g = w.sbyte0 + i;
+            r[j] = (i < A.stage_bytes && g < w.pdc_bytes) ? uint32_t(w.dpdc[g] ^ w.cpdc[g]) : 0u;
+        }
+    };
+    auto store_bytes = [&](const uint32_t (&r)[8]) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (t + TX_THREADS * j < A.stage_bytes) w.sb[t + TX_THREADS * j] = static_cast<uint8_t>(r[j]);
+        for (uint32_t i = t + 8 * TX_THREADS; i < A.stage_bytes; i += TX_THREADS) {  // beyond the batch
+            const uint32_t g = w.sbyte0 + i;
+            w.sb[i] = g < w.pdc_bytes ? static_cast<uint8_t>(w.dpdc[g] ^ w.cpdc[g]) : 0u;
+        }
+    };
+
+    // ---- one-time staging (one memory round trip): tables + group 0's codes and PDC bytes
+    set_group(0);
+    uint32_t rc[16], rb[8];
+    load_codes(rc);
+    load_bytes(rb);
+    {
+        const uint8_t* dpcc = A.pcc_d + size_t(w.pkt) * 25;
+        const uint32_t nq = 1u << A.N_bps;
+        const float2 r_q = t < nq ? A.qam[t] : make_float2(0.f, 0.f);
+        uint32_t r_pcc = 0;
+        if (t < 98) r_pcc = uint32_t(dpcc[(2 * t) >> 3] ^ A.pcc_seq[(2 * t) >> 3]);
+        const float2 r_w = t < A.N_TS ? A.W[(w.P.codebook * A.N_TX + w.ant) * A.N_TS + t] : make_float2(0.f, 0.f);
+        float r_h[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) r_h[j] = t + TX_THREADS * j < A.npp ? A.taps_pp[t + TX_THREADS * j] : 0.f;
+        if (t < nq) w.qtab[t] = r_q;
+        if (t < 98) {  // QPSK (TS 36.211 7.1.2): (1 - 2 b0, 1 - 2 b1) / sqrt(2)
+            const uint32_t q = bits_of(r_pcc, 0u, 2 * t, 2);
+            w.pccs[t] = make_float2((q & 2u) ? -0.70710678f : 0.70710678f, (q & 1u) ? -0.70710678f : 0.70710678f);
+        }
+        if (t < A.N_TS) w.wrow[t] = r_w;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (t + TX_THREADS * j < A.npp) w.hpl[t + TX_THREADS * j] = r_h[j];
+        for (uint32_t i = t + 2 * TX_THREADS; i < A.npp; i += TX_THREADS) w.hpl[i] = A.taps_pp[i];
+        store_bytes(rb);
+        for (uint32_t i = t; i < A.HP; i += TX_THREADS) w.lin[i] = make_float2(0.f, 0.f);  // nothing before the packet
+    }
+    lds_barrier();
+
+    float2* out = reinterpret_cast<float2*>(A.out) + size_t(w.pkt * A.N_TX + w.ant) * A.S;
+    const float2 step1 = w.P.do_mix ? phasor(w.P.inc) : make_float2(1.f, 0.f);
+    auto n_out = [&](uint32_t B) {  // outputs m with delay + m*M < B*L (B*L < 2^32: host-checked)
+        const uint32_t tt = B * A.L;
+        return tt > A.delay ? min((tt - A.delay + A.M - 1) / A.M, A.n_keep) : 0u;
+    };
+    for (uint32_t g = 0; g < A.n_grp; ++g) {
+        const uint32_t span = w.bsym(w.l_last + 1) - w.base_q;
+        // ---- symbols of the group (one per wavefront)
+        if (b < w.nsl) {
+            const uint32_t l = w.l_first + b;
+            float2 v[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) v[m] = w.bin(rc[m], lane + 64 * m, l);
+            float2* xb = w.slot(l);  // the symbol's own slot (>= 1152 samples) is the exchange buffer
+            wave_fft1024<+1>(v, xb, w.twl, lane);
+            __builtin_amdgcn_wave_barrier();
+            w.put_symbol(l, v, lane);
+        }
+        if (w.last_run)  // flush inputs after the packet: zeros (earlier groups left outputs there)
+            for (uint32_t i = A.HP + span + t; i < A.lin_len; i += TX_THREADS) w.lin[i] = make_float2(0.f, 0.f);
+        lds_barrier();
+        // ---- resample + mix the group's outputs into registers (<= 3 blocks per thread)
+        const uint32_t B_lo = w.base_q, B_hi = w.last_run ? w.bsym(A.N_DF + 1) + w.hl : w.bsym(w.l_last + 1);
+        const uint32_t m_lo = n_out(B_lo), m_hi = n_out(B_hi);
+        const int lin_off = static_cast<int>(A.HP) - static_cast<int>(w.base_q);
+        const int idx_max = static_cast<int>(A.lin_len) - PB::W;
+        const int q_lo = floor_div(static_cast<int>(m_lo) - static_cast<int>(A.m_star), LR);
+        const int q_hi = floor_div(static_cast<int>(m_hi) - static_cast<int>(A.m_star) + LR - 1, LR);
+        auto win = [&](int q) {
+            const int pb = static_cast<int>(A.p_star) + MR * q;
+            return w.lin + min(max(pb - HLR + lin_off, 0), idx_max);  // clamped windows feed unstored outputs only
+        };
+        float2 y[2][LR], y2[LR];
+        {
+            const float2* xw[2] = {win(q_lo + static_cast<int>(t)), win(q_lo + static_cast<int>(t + TX_THREADS))};
+            PB::template run_multi<2>(xw, w.hpl, y);
+        }
+        const int q2 = q_lo + static_cast<int>(t + 2 * TX_THREADS);
+        if (q2 < q_hi) PB::run(win(q2), w.hpl, y2);
+        float2 hist = make_float2(0.f, 0.f);
+        if (t < A.HP) hist = w.lin[span + t];  // the next group's resampler history
+        lds_barrier();
+        // ---- outputs through LDS (behind the history slots) for contiguous stores
+        float2* ob = w.lin + A.HP;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int q = q_lo + static_cast<int>(t + r * TX_THREADS);
+            if (q < q_hi) {
+                const int mb = static_cast<int>(A.m_star) + LR * q;
+                float2 rot = w.P.do_mix ? phasor(w.P.ph0 + static_cast<double>(mb) * w.P.inc) : make_float2(1.f, 0.f);
+#pragma unroll
+                for (int k = 0; k < LR; ++k) {
+                    const uint32_t m = static_cast<uint32_t>(mb + k);
+                    float2 v = r < 2 ? y[r < 2 ? r : 0][k] : y2[k];
+                    if (w.P.do_mix) {
+                        v = cmul(v, rot);
+                        rot = cmul(rot, step1);
+                    }
+                    if (m - m_lo < m_hi - m_lo) ob[m - m_lo] = v;
+                }
+            }
+        }
+        lds_barrier();
+        // ---- next group's codes / PDC bytes in flight while the outputs leave
+        const bool last = w.last_run, more = g + 1 < A.n_grp;
+        if (more) {
+            set_group(g + 1);
+            load_codes(rc);
+            load_bytes(rb);
+        }
+        const uint32_t n = m_hi - m_lo;
+        const uint32_t head = min(n, (reinterpret_cast<uintptr_t>(out + m_lo) & 15u) ? 1u : 0u);
+        if (t < head) out[m_lo] = ob[0];
+        const uint32_t npair = (n - head) / 2;
+        float4* o4 = reinterpret_cast<float4*>(out + m_lo + head);
+        for (uint32_t i = t; i < npair; i += TX_THREADS) {
+            const float2 a = ob[head + 2 * i], c = ob[head + 2 * i + 1];
+            o4[i] = make_float4(a.x, a.y, c.x, c.y);
+        }
+        if (t == 0 && ((n - head) & 1u)) out[m_hi - 1] = ob[n - 1];
+        if (last)  // GI and slot tail (tx.cpp:706-714)
+            for (uint32_t m = m_hi + t; m < A.S; m += TX_THREADS) out[m] = make_float2(0.f, 0.f);
+        if (t < A.HP) w.lin[t] = hist;
+        if (more) store_bytes(rb);
+        lds_barrier();
+    }
 }
 
 // ---- other FFT sizes: workgroup-wide batched Stockham FFT
@@ -416,12 +613,25 @@ __global__ void __launch_bounds__(TX_THREADS) tx_kernel(tx_args A) {
 
 size_t tx_lds_bytes(const tx_args& a) {
     const bool wave = a.plan.N == 1024;
-    return (size_t(a.lin_len) + (wave ? 0 : a.bufB_len) + a.plan.N + 256 + 98 + 8) * sizeof(float2) +
+    return (size_t(a.lin_len) + (wave ? 0 : a.bufB_len + a.plan.N) + 256 + 98 + 8) * sizeof(float2) +
            a.npp * sizeof(float) + ((a.stage_bytes + 2 + 15) & ~15u);
 }
 
 hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
     const bool wave = a.plan.N == 1024;
+    if (a.stream) {
+        if (!wave || a.N_bps > 8 || a.npp > 2 * TX_THREADS) return hipErrorInvalidValue;
+        const size_t lds = size_t(a.lin_len + 256 + 98 + 8) * sizeof(float2) + a.npp * sizeof(float) +
+                           ((a.stage_bytes + 15) & ~15u);
+        const dim3 g(n * a.N_TX), b(TX_THREADS);
+        if (a.L == 10 && a.M == 9 && a.hl == 22)
+            hipLaunchKernelGGL((tx_kernel_stream<10, 9, 22>), g, b, lds, st, a);
+        else if (a.L == 10 && a.M == 9 && a.hl == 4)
+            hipLaunchKernelGGL((tx_kernel_stream<10, 9, 4>), g, b, lds, st, a);
+        else
+            return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     if (a.K + 1 > TX_MAX_SLOTS || a.plan.N > TX_BIN_REG * TX_THREADS || a.N_bps > 8) return hipErrorInvalidValue;
     if (wave && (a.K + 1) * 64 > TX_THREADS) return hipErrorInvalidValue;
     const size_t lds = tx_lds_bytes(a);
