@@ -292,6 +292,44 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         *err = DNRP_ENOMEM;
         return nullptr;
     }
+    // MIMO report tables (estimator_mimo.cpp:80-160): per TS the latest DRS symbol carrying it, its
+    // cells at offset step/2 + c*step (step = N_DRS_cells_b / 4) and their DRS values
+    {
+        const uint32_t NTS = tm.N_eff_TX, nd = t->maps.drs_v.size() / 8, step = nd / 4, off = step / 2;
+        std::vector<uint32_t> cells(NTS * 4, 0);
+        std::vector<float> signs(NTS * 4, 1.f);
+        for (uint32_t ts = 0; ts < NTS; ++ts) {
+            const geo::drs_sym_t* last = nullptr;
+            for (const auto& d : t->maps.drs)
+                if (d.ts_first <= ts && ts <= d.ts_last) last = &d;
+            if (!last) continue;
+            for (uint32_t c = 0; c < 4; ++c) {
+                const uint32_t i = off + c * step;
+                cells[ts * 4 + c] = (last->l << 16) | t->maps.drs_k[(last->parity * 4 + ts % 4) * nd + i];
+                signs[ts * 4 + c] = t->maps.drs_v[ts * nd + i];
+            }
+        }
+        static const uint32_t A_nonzero[9] = {0, 0, 2, 0, 12, 0, 0, 0, 0};  // beamforming_...mapping.hpp:110-119, N_TS = 1
+        auto book = [&](uint32_t N, dbuf& W, dbuf& sc, uint32_t& ncb, uint32_t& A0) {
+            if (N < 2) return true;
+            ncb = geo::W_codebooks(1, N);
+            A0 = A_nonzero[N];
+            std::vector<float2> w;
+            std::vector<float> s;
+            for (uint32_t cb = 0; cb < ncb; ++cb) {
+                float f = 1.f;
+                for (const auto& v : geo::W_matrix(1, N, cb, &f)) w.push_back(make_float2(v.real(), v.imag()));
+                s.push_back(f);
+            }
+            return W.upload(w) && sc.upload(s);
+        };
+        t->N_TS = NTS;
+        if (!t->mimo_cells.upload(cells) || !t->mimo_signs.upload(signs) || !book(NTS, t->Wtx, t->stx, t->ncb_tx, t->A_tx) ||
+            !book(ctx->cfg.N_TX_max, t->Wrx, t->srx, t->ncb_rx, t->A_rx)) {
+            *err = DNRP_ENOMEM;
+            return nullptr;
+        }
+    }
     auto* r = t.get();
     ctx->rx2t[key] = std::move(t);
     return r;
@@ -705,10 +743,39 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const 
                            pdc_llr, llr_stride, st)) != DNRP_OK)
         return err;
     if (rep) {
+        // MIMO report at the packet end (rx_synced.cpp:417-436; the reference runs it after a
+        // successful CRC, which is the caller's decision here)
+        if (!ctx->mimo_out.ensure(size_t(ctx->cfg.max_batch) * 3 * sizeof(uint32_t))) return DNRP_ENOMEM;
+        dev::rx_mimo_args ma{};
+        ma.N_RX = ctx->cfg.N_TX_max;
+        ma.N_TS = t2->N_TS;
+        ma.Nf_pad = ctx->rx_Nf_pad;
+        ma.n_sym_total = ctx->rx_nsym_cap + 1;
+        ma.ncb_tx = t2->ncb_tx;
+        ma.A_tx = t2->A_tx;
+        ma.ncb_rx = t2->ncb_rx;
+        ma.A_rx = t2->A_rx;
+        ma.cells = t2->mimo_cells.as<uint32_t>();
+        ma.signs = t2->mimo_signs.as<float>();
+        ma.Wtx = t2->Wtx.as<float2>();
+        ma.stx = t2->stx.as<float>();
+        ma.Wrx = t2->Wrx.as<float2>();
+        ma.srx = t2->srx.as<float>();
+        ma.Y = ctx->Y.as<float2>();
+        ma.out = ctx->mimo_out.as<uint32_t>();
+        if (dev::launch_rx_mimo(ma, n, st) != hipSuccess) return DNRP_EDEVICE;
         std::vector<dev::rx_pkt_state> S(n);
+        std::vector<uint32_t> mo(3 * size_t(n));
         HIPCHK(hipMemcpyAsync(S.data(), ctx->rx_st.p, sizeof(dev::rx_pkt_state) * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(mo.data(), ma.out, mo.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        for (uint32_t i = 0; i < n; ++i) rep[i].snr_dB = S[i].snr_pdc;
+        for (uint32_t i = 0; i < n; ++i) {
+            rep[i].snr_dB = S[i].snr_pdc;
+            rep[i].mimo_N_RX = ma.N_RX;
+            rep[i].mimo_N_TS_other = mo[3 * i];
+            rep[i].tm_3_7_beamforming_idx = mo[3 * i + 1];
+            rep[i].tm_3_7_beamforming_reciprocal_idx = mo[3 * i + 2];
+        }
     }
     return DNRP_OK;
 }

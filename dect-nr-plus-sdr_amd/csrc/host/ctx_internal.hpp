@@ -127,6 +127,9 @@ struct rx2_tables {  // per (psdef): PDC phase
     geo::maps_t maps;
     dbuf pdc_k, pdc_sym;
     rx_plan_dev bplan;  // PDC phase back end
+    // MIMO report (estimator_mimo_t): wideband DRS cells, single-stream codebooks
+    uint32_t N_TS = 1, ncb_tx = 0, A_tx = 0, ncb_rx = 0, A_rx = 0;
+    dbuf mimo_cells, mimo_signs, Wtx, stx, Wrx, srx;
 };
 
 struct netid_seq {
@@ -160,7 +163,7 @@ struct dnrp_ctx {
     std::map<uint32_t, std::unique_ptr<netid_seq>> netid;
     dbuf pcc_seq;
     // batch scratch
-    dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d;
+    dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d, mimo_out;
     pinned st_tx, st_rxin, st_seq, st_rep;
     // retained RX phase-1 state
     rx1_tables* rx1_last = nullptr;

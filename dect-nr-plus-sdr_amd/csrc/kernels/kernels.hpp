@@ -148,6 +148,20 @@ struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epo
 };
 hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st);
 
+struct rx_mimo_args {  // estimator_mimo_t::process_drs at the packet end, one wavefront per packet
+    uint32_t N_RX, N_TS, Nf_pad, n_sym_total;
+    uint32_t ncb_tx, A_tx, ncb_rx, A_rx;  // single-stream codebooks (1, N_TS) and (1, N_RX): size, first used
+    const uint32_t* cells;  // [N_TS][4]: symbol << 16 | subcarrier index of the wideband DRS cells
+    const float* signs;     // [N_TS][4]: DRS value (+-1)
+    const float2* Wtx;      // [ncb_tx][N_TS]
+    const float* stx;       // [ncb_tx] scaling factors
+    const float2* Wrx;      // [ncb_rx][N_RX]
+    const float* srx;
+    const float2* Y;
+    uint32_t* out;          // [n][3]: N_TS_other, tm_3_7_beamforming_idx, tm_3_7_beamforming_reciprocal_idx
+};
+hipError_t launch_rx_mimo(const rx_mimo_args& a, uint32_t n, hipStream_t st);
+
 
 // ---- synchronisation (sync.hip): sync_chunk_t::search() per window, reports in search order
 struct sync_res {  // layout of dnrp_sync_result (include/dnrp.h)

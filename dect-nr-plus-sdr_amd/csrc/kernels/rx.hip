@@ -345,11 +345,18 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     const double phi_stf = static_cast<double>(n_stf) * in.inc0;  // mixer phase at the first data sample
     const float2 step1 = phasor(S.inc1);
     float2 ys[BR][LR];
+    {
+        // all rounds of the lane in one pass over the tap rows (pp_block::run_multi); rounds past
+        // the symbol's last block read a valid window and are discarded
+        const float2* xw[BR];
+#pragma unroll
+        for (int rd = 0; rd < BR; ++rd) xw[rd] = R + MR * min(static_cast<int>(lane) + 64 * rd, qb1 - 1 - qb0);
+        PB::template run_multi<BR>(xw, taps, ys);
+    }
 #pragma unroll
     for (int rd = 0; rd < BR; ++rd) {
         const int q = qb0 + static_cast<int>(lane) + 64 * rd;
         if (q < qb1) {
-            PB::run(R + MR * (q - qb0), taps, ys[rd]);
             const int mb = static_cast<int>(A.m_star) + LR * q;
             float2 r = phasor(phi_stf + static_cast<double>(mb - static_cast<int>(n_stf)) * S.inc1);
 #pragma unroll
@@ -380,18 +387,26 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     wave_fft1024<-1>(v, R, twl, lane);
     // occupied bins: FFT bin n -> subcarrier index k (extract_bins), amplitude, STO derotation
     float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
+    // STO derotation exp(j sto_inc (k - N/2)) is linear in m on each half: two running phasors
+    // stepped by 64 bins instead of one sin/cos per bin
+    const float2 s64 = phasor(64.0 * S.sto_inc);
+    float2 pa = phasor(S.sto_inc * static_cast<double>(lane));  // n <= N/2: k - N/2 = n
+    float2 pb = phasor(S.sto_inc * (static_cast<double>(lane) - static_cast<double>(A.off_lower) -
+                                    static_cast<double>(N / 2)));  // upper FFT half: k - N/2 = n - off_lower - N/2
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         const uint32_t n = lane + 64 * m;
         uint32_t k = 0xFFFFFFFFu;
-        if (n <= N / 2)
+        float2 rot = pa;
+        if (n <= N / 2) {
             k = n + N / 2;
-        else if (n >= A.off_lower && n < A.off_lower + N / 2)
+        } else if (n >= A.off_lower && n < A.off_lower + N / 2) {
             k = n - A.off_lower;
-        if (k != 0xFFFFFFFFu) {
-            const float2 rot = phasor(S.sto_inc * (static_cast<double>(k) - static_cast<double>(N / 2)));
-            Yrow[k] = cmul(cscale(v[m], A.amp_scale), rot);
+            rot = pb;
         }
+        if (k != 0xFFFFFFFFu) Yrow[k] = cmul(cscale(v[m], A.amp_scale), rot);
+        pa = cmul(pa, s64);
+        pb = cmul(pb, s64);
     }
 }
 

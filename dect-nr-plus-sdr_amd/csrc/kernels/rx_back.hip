@@ -330,4 +330,69 @@ hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
+// ===================================================================== MIMO report
+// estimator_mimo.cpp:80-222 (mode_single_spatial_stream_3_7, metric HIGHEST_MIN_RX_POWER): lane wm
+// scores codebook entry wm (min over the receive side of |sum_tx sum_c H w|, times the entry's
+// scaling), the first maximum wins. H: the latest zero-forced DRS value of each (rx, ts) at the 4
+// wideband cells (RX_SYNCED_PARAM_MIMO_N_WIDEBAND_CELLS), float sums in the reference's order.
+__device__ uint32_t mimo_pick(const float2* H, uint32_t N_TX_virt, uint32_t N_RX_virt, bool transposed, uint32_t N_TS,
+                              const float2* W, const float* sc, uint32_t A0, uint32_t ncb, uint32_t lane) {
+    float best = -1.0e6f;
+    uint32_t bidx = 0xFFFFFFFFu;
+    for (uint32_t wm = A0 + lane; wm < ncb; wm += 64) {
+        float power_inner = 1.0e6f;
+        for (uint32_t rx = 0; rx < N_RX_virt; ++rx) {
+            float2 sum = make_float2(0.f, 0.f);
+            for (uint32_t tx = 0; tx < N_TX_virt; ++tx) {
+                const float2 w = W[wm * N_TX_virt + tx];
+                const uint32_t hrx = transposed ? tx : rx, hts = transposed ? rx : tx;
+                float2 part = make_float2(0.f, 0.f);
+                for (uint32_t c = 0; c < 4; ++c) part = cadd(part, cmul(H[(hrx * N_TS + hts) * 4 + c], w));
+                sum = cadd(sum, part);
+            }
+            const float p = hypotf(sum.x, sum.y);
+            if (p < power_inner) power_inner = p;
+        }
+        power_inner *= sc[wm];
+        if (best < power_inner) {
+            best = power_inner;
+            bidx = wm;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o);
+        const uint32_t oi = __shfl_xor(bidx, o);
+        if (ob > best || (ob == best && oi < bidx)) {
+            best = ob;
+            bidx = oi;
+        }
+    }
+    return bidx;
+}
+
+__global__ void __launch_bounds__(64) rx_mimo_kernel(rx_mimo_args A) {
+    __shared__ float2 H[8 * 8 * 4];
+    const uint32_t pkt = blockIdx.x, lane = threadIdx.x;
+    const float2* Yp = A.Y + size_t(pkt) * A.N_RX * A.n_sym_total * A.Nf_pad;
+    for (uint32_t e = lane; e < A.N_RX * A.N_TS * 4; e += 64) {
+        const uint32_t rx = e / (A.N_TS * 4), tc = e % (A.N_TS * 4);
+        const uint32_t cell = A.cells[tc];
+        H[e] = cscale(Yp[(size_t(rx) * A.n_sym_total + (cell >> 16)) * A.Nf_pad + (cell & 0xFFFFu)], A.signs[tc]);
+    }
+    __syncthreads();
+    const uint32_t idx = A.N_TS == 1 ? 0u : mimo_pick(H, A.N_TS, A.N_RX, false, A.N_TS, A.Wtx, A.stx, A.A_tx, A.ncb_tx, lane);
+    const uint32_t idr = A.N_RX == 1 ? 0u : mimo_pick(H, A.N_RX, A.N_TS, true, A.N_TS, A.Wrx, A.srx, A.A_rx, A.ncb_rx, lane);
+    if (lane == 0) {
+        A.out[3 * pkt] = A.N_TS;
+        A.out[3 * pkt + 1] = idx;
+        A.out[3 * pkt + 2] = idr;
+    }
+}
+
+hipError_t launch_rx_mimo(const rx_mimo_args& a, uint32_t n, hipStream_t st) {
+    if (a.N_RX > 8 || a.N_TS > 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rx_mimo_kernel, dim3(n), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
 }  // namespace dnrp::dev

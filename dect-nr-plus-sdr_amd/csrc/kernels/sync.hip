@@ -143,7 +143,13 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_steps_kernel(sync_args A) {
 // with B polyphase blocks per lane (pp_block::run_multi: one tap-row read serves B blocks, which
 // keeps the LDS traffic per FMA under the 128 B/clk/CU the VALU needs), writes the outputs back into
 // the region and sums the steps from there.
-constexpr int SYNC_WB = 4;  // blocks per lane
+#ifndef SYNC_WB_DEF
+#define SYNC_WB_DEF 4
+#endif
+#ifndef SYNC_WPG_DEF
+#define SYNC_WPG_DEF 2
+#endif
+constexpr int SYNC_WB = SYNC_WB_DEF;  // blocks per lane
 
 __host__ __device__ inline uint32_t sync_wave_steps(uint32_t L, uint32_t step, uint32_t pattern) {
     return (64u * SYNC_WB * L - pattern - 2 * L) / step;  // steps whose span (+ lookback) fits 64 B blocks
@@ -735,7 +741,7 @@ size_t sync_detect_lds(const sync_args& a) {
             hipLaunchKernelGGL((KERNEL<0, 0, 0>), GRID, dim3(SYNC_THREADS), LDS, st, a);   \
     } while (0)
 
-constexpr int SYNC_WPG = 2;  // waves per workgroup of the wave kernel
+constexpr int SYNC_WPG = SYNC_WPG_DEF;  // waves per workgroup of the wave kernel
 
 hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
     if (a.L == 9 && a.M == 10 && a.hl == 24) {

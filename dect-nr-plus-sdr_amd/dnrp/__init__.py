@@ -110,7 +110,8 @@ class PccReport(C.Structure):
 
 
 class PdcReport(C.Structure):
-    _fields_ = [("snr_dB", C.c_float)]
+    _fields_ = [("snr_dB", C.c_float), ("mimo_N_RX", C.c_uint32), ("mimo_N_TS_other", C.c_uint32),
+                ("tm_3_7_beamforming_idx", C.c_uint32), ("tm_3_7_beamforming_reciprocal_idx", C.c_uint32)]
 
 
 class PdcReq(C.Structure):

@@ -141,9 +141,14 @@ typedef struct {
     float rms[8];             /* per RX antenna, over the STF */
 } dnrp_pcc_report;
 
-/* PHY part of pdc_report_t (rx_synced.cpp:432-435) */
+/* PHY part of pdc_report_t (rx_synced.cpp:432-435) with its mimo_report_t
+ * (phy/rx/rx_synced/mimo/mimo_report.hpp; estimator_mimo.cpp:80-222) */
 typedef struct {
     float snr_dB;
+    uint32_t mimo_N_RX;                          /* own physical antennas */
+    uint32_t mimo_N_TS_other;                    /* transmit streams received (N_eff_TX) */
+    uint32_t tm_3_7_beamforming_idx;             /* codebook index recommended to the other side */
+    uint32_t tm_3_7_beamforming_reciprocal_idx;  /* codebook index for this side if reciprocal */
 } dnrp_pdc_report;
 
 /* per-packet PDC request = what maclow_phy_t / the HARQ process provide (interfaces/maclow_phy.hpp) */

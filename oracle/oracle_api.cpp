@@ -217,7 +217,8 @@ int oracle_tx(const uint32_t* cfg, const uint32_t* psdef, const uint32_t* desc_u
     }
 }
 
-// meta out: [0..7] rms, 8 cfo_fine_rad, 9 sto_fractional, 10 snr_pcc_db, 11 snr_pdc_db
+// meta out: [0..7] rms, 8 cfo_fine_rad, 9 sto_fractional, 10 snr_pcc_db, 11 snr_pdc_db,
+//           12 mimo N_TS_other, 13 tm_3_7_beamforming_idx, 14 tm_3_7_beamforming_reciprocal_idx
 int oracle_rx(const uint32_t* cfg, const uint32_t* psdef, uint32_t N_RX, const float* iq, uint32_t S_in,
               int64_t fine_peak, double cfo_rad, uint32_t network_id, uint32_t plcf_type, int16_t* pcc_llr,
               int16_t* pdc_llr, float* pcc_llr_f, float* pdc_llr_f, float* meta, int use_float) {
@@ -239,6 +240,9 @@ int oracle_rx(const uint32_t* cfg, const uint32_t* psdef, uint32_t N_RX, const f
         meta[9] = o.sto_fractional;
         meta[10] = o.snr_pcc_db;
         meta[11] = o.snr_pdc_db;
+        meta[12] = static_cast<float>(o.mimo_N_TS_other);
+        meta[13] = static_cast<float>(o.mimo_idx);
+        meta[14] = static_cast<float>(o.mimo_idx_reciprocal);
         return 0;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "oracle_rx: %s\n", e.what());

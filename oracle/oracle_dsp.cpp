@@ -590,6 +590,50 @@ struct rx_state_t {
         lut_eff = idx;
     }
 
+    // estimator_mimo_t::process_drs at the packet end (rx_synced.cpp:417-436,
+    // estimator_mimo.cpp:80-222): 4 wideband cells of the latest zero-forced DRS of every TS,
+    // single-stream codebook search maximising the minimum RX power, both directions
+    void mimo_report() {
+        const uint32_t n = ps.num.b * 14, step = n / 4, off = step / 2;  // RX_SYNCED_PARAM_MIMO_N_WIDEBAND_CELLS 4
+        const uint32_t NTS = N_eff_TX;
+        // stage[rx][tx][c]: float, as the reference's cf_t stages
+        auto pick = [&](uint32_t N_TX_virt, uint32_t N_RX_virt, auto&& H) -> uint32_t {
+            static const uint32_t A_nonzero[9] = {0, 0, 2, 0, 12, 0, 0, 0, 0};  // N_TS_N_TX_codebook_index_nonzero[1][.]
+            const uint32_t n_cb = W_codebook_max(1, N_TX_virt) + 1;
+            float power_outer = -1.0e6f;
+            int32_t ret = -1;
+            for (uint32_t wm = A_nonzero[N_TX_virt]; wm < n_cb; ++wm) {
+                const auto W = W_matrix(1, N_TX_virt, wm);
+                const float sc = static_cast<float>(W_scaling(1, N_TX_virt, wm));
+                float power_inner = 1.0e6f;
+                for (uint32_t rx = 0; rx < N_RX_virt; ++rx) {
+                    cf sum{0.0f, 0.0f};
+                    for (uint32_t tx = 0; tx < N_TX_virt; ++tx) {
+                        cf part{0.0f, 0.0f};
+                        const cf w(static_cast<float>(W[tx].real()), static_cast<float>(W[tx].imag()));
+                        for (uint32_t c = 0; c < 4; ++c) part += H(rx, tx, c) * w;
+                        sum += part;
+                    }
+                    power_inner = std::min(power_inner, std::abs(sum));
+                }
+                power_inner *= sc;
+                if (power_outer < power_inner) {
+                    power_outer = power_inner;
+                    ret = static_cast<int32_t>(wm);
+                }
+            }
+            return static_cast<uint32_t>(ret);
+        };
+        auto Hz = [&](uint32_t rx, uint32_t ts, uint32_t c) {
+            const cd v = zf[rx][ts][off + c * step];
+            return cf(static_cast<float>(v.real()), static_cast<float>(v.imag()));
+        };
+        out.mimo_N_TS_other = NTS;
+        out.mimo_idx = NTS == 1 ? 0u : pick(NTS, N_RX, Hz);
+        out.mimo_idx_reciprocal =
+            N_RX == 1 ? 0u : pick(N_RX, NTS, [&](uint32_t ts, uint32_t rx, uint32_t c) { return Hz(rx, ts, c); });
+    }
+
     void interpolate() {  // rx_synced.cpp:893-949 + channel_lut.cpp:66-165
         const chest_lut_t& L = mode_lr ? lut_lr[lut_eff] : lut0[lut_eff];
         const uint32_t n = L.nof_interp;
@@ -765,6 +809,7 @@ struct rx_state_t {
             }
         }
         out.snr_pdc_db = static_cast<float>(snr_db());
+        mimo_report();
         if (pcc_idx != 98 || pdc_idx != ps.N_PDC_subc || bits_idx != ps.G)
             throw std::runtime_error("RX cell count mismatch");
 

@@ -35,6 +35,7 @@ struct rx_out_t {
     std::vector<float> pcc_llr_f, pdc_llr_f; // pre-quantisation values, descrambled
     std::vector<float> rms;
     float cfo_fine_rad = 0, sto_fractional = 0, snr_pcc_db = 0, snr_pdc_db = 0;
+    uint32_t mimo_N_TS_other = 0, mimo_idx = 0, mimo_idx_reciprocal = 0;  // mimo_report_t
 };
 
 struct dims_t {

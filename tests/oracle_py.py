@@ -116,13 +116,14 @@ def rx(cf, ps, iq, fine_peak=0, cfo_rad=0.0, network_id=100, plcf_type=1, use_fl
     pdc = np.zeros(sz["G"], dtype=np.int16)
     pccf = np.zeros(196, dtype=np.float32)
     pdcf = np.zeros(sz["G"], dtype=np.float32)
-    meta = np.zeros(12, dtype=np.float32)
+    meta = np.zeros(16, dtype=np.float32)
     r = lib().oracle_rx(cf, ps, n_rx, iq.view(np.float32).reshape(-1), s_in, int(fine_peak), float(cfo_rad),
                         network_id, plcf_type, pcc, pdc, pccf.ctypes.data, pdcf.ctypes.data, meta,
                         int(use_float))
     assert r == 0, r
     return dict(pcc_llr=pcc, pdc_llr=pdc, pcc_llr_f=pccf, pdc_llr_f=pdcf, rms=meta[:8].copy(),
-                cfo_fine=float(meta[8]), sto=float(meta[9]), snr_pcc=float(meta[10]), snr_pdc=float(meta[11]))
+                cfo_fine=float(meta[8]), sto=float(meta[9]), snr_pcc=float(meta[10]), snr_pdc=float(meta[11]),
+                mimo_N_TS_other=int(meta[12]), mimo_idx=int(meta[13]), mimo_idx_reciprocal=int(meta[14]))
 
 
 def loopback_timed(cf, ps, n_packets, n_threads, seed=0xDEC7, sync_pre=0, sync_chunk=0):

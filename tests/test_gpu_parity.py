@@ -123,6 +123,9 @@ def test_rx_parity(name, snr):
         assert d_pdc.max() <= 1, (name, d_pdc.max(), np.argmax(d_pdc), np.mean(d_pdc))
         assert abs(r1.snr_dB - r["snr_pcc"]) < 0.05, (r1.snr_dB, r["snr_pcc"])
         assert abs(r2.snr_dB - r["snr_pdc"]) < 0.05, (r2.snr_dB, r["snr_pdc"])
+        # mimo_report_t (estimator_mimo.cpp): codebook recommendations exact
+        assert (r2.mimo_N_TS_other, r2.tm_3_7_beamforming_idx, r2.tm_3_7_beamforming_reciprocal_idx) == \
+            (r["mimo_N_TS_other"], r["mimo_idx"], r["mimo_idx_reciprocal"])
         assert abs(r1.sto_fractional - r["sto"]) < 1e-3
         for a in range(len(r["rms"])):
             assert abs(r1.rms[a] - r["rms"][a]) <= 1e-4 * max(1.0, r["rms"][a])

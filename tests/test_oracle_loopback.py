@@ -61,3 +61,25 @@ def test_gold_sequence_properties():
     assert abs(int(a.sum()) - 2048) < 150
     assert np.mean(a != b) > 0.4
     assert np.array_equal(O.gold(0x44454354, 100), a[:100])
+
+
+def test_mimo_report_codebook_search():
+    """estimator_mimo_t (A29): for a rank-one channel H = g w^T, the recommended single-stream
+    codebook entry (both directions) is the one matching w (maximises min RX power)."""
+    import phy_fixtures as F
+    psd, cfgt = F.CONFIGS["C4"]
+    cf = O.cfg(cfgt[0], cfgt[1])
+    ps = O.psdef(*psd)
+    sz = O.packet_sizes(ps)
+    rng = np.random.default_rng(12)
+    S = O.dims(cf, ps)["N_packet_os_rs"]
+    x, _ = O.tx(cf, ps, rng.integers(0, 256, 25, dtype=np.uint8),
+                rng.integers(0, 256, (sz["G"] + 7) // 8, dtype=np.uint8), S)
+    # W_2 codebook entry 17 = (1, j, j, -1) / 2 for 4 antennas (beamforming_and_antenna_port_mapping.cpp:252-257);
+    # the receiver sees TS streams through H[rx][ts]; a rank-one H = g (x) conj(w) aligns best with entry 17
+    w = np.array([1, 1j, 1j, -1]) / 2
+    g = np.array([1.0, 0.9, 1.1, 0.95])
+    H = np.outer(g, np.conj(w)).astype(np.complex64)
+    r = O.rx(cf, ps, (H @ x).astype(np.complex64))
+    assert r["mimo_N_TS_other"] == 4
+    assert r["mimo_idx"] == 17
