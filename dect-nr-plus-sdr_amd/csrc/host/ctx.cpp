@@ -565,13 +565,16 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     a.pdc_stride = pdc_stride;
     a.G = t->q.G;
     // symbol runs (tx.hip): K symbols per WG plus the preceding symbol as resampler history
-    // K = 3 symbols + history per 4-wave workgroup (C4, 4096 slots: K=1 23.4 ms, K=2 13.7 ms,
-    // K=3 12.7 ms per launch); DNRP_TX_STREAM=1 selects the experimental streaming kernel
+    // wave path (one wavefront per symbol slot): K = 6 symbols + history per 7-wave workgroup
+    // (C4, 4096 slots per launch: K=3 12.3 ms, K=4 16.6, K=5 15.2, K=6 11.4, K=7 15.9 — LDS sets
+    // 4 / 2 / 2 / 2 / 1 workgroups per CU); block path K = 3. DNRP_TX_RUN overrides.
     static const int K_env = [] {
         const char* e = std::getenv("DNRP_TX_RUN");
         return e ? std::atoi(e) : 0;
     }();
-    const uint32_t K = (K_env >= 1 && K_env <= 3) ? static_cast<uint32_t>(K_env) : 3u;
+    const bool wave = t->dm.Nd == 1024;
+    const uint32_t K_max = wave ? 7u : 3u;  // wave path: one wavefront per symbol slot, <= 8 slots
+    const uint32_t K = (K_env >= 1 && static_cast<uint32_t>(K_env) <= K_max) ? static_cast<uint32_t>(K_env) : (wave ? 6u : 3u);
     a.K = K;
     a.dbg = std::getenv("DNRP_TX_DBG") ? static_cast<uint32_t>(std::atoi(std::getenv("DNRP_TX_DBG"))) : 0u;
     a.n_runs = (t->q.N_DF_symb + 1 + K - 1) / K;
@@ -596,33 +599,6 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
         // output staging reuses bufB + twiddles + constellation: size bufB for the longest run
         const uint32_t max_out = static_cast<uint32_t>((uint64_t(span + t->rs.hl) * t->rs.L + t->rs.M - 1) / t->rs.M) + t->rs.L;
         a.bufB_len = std::max((K + 1) * t->dm.Nd, max_out > t->dm.Nd + 256 ? max_out - t->dm.Nd - 256 : 0u);
-        // streaming kernel (default for N_b_DFT_os = 1024 at L/M = 10/9): one WG per (packet,
-        // antenna), symbol groups of <= 4 slots, no history symbol re-synthesised
-        const bool stream_ok = t->dm.Nd == 1024 && t->rs.L == 10 && t->rs.M == 9 && (t->rs.hl == 22 || t->rs.hl == 4) &&
-                               t->npp <= 512 && t->q.N_bps <= 8 && K_env == 0 && std::getenv("DNRP_TX_STREAM") &&
-                               std::getenv("DNRP_TX_STREAM")[0] == '1';
-        if (stream_ok) {
-            const uint32_t N_DF = t->q.N_DF_symb;
-            uint32_t g0 = 0;
-            while (g0 + 1 <= N_DF && bsym(g0 + 2) <= 4 * lenD) ++g0;
-            uint32_t n_grp = 1 + (N_DF > g0 ? (N_DF - g0 + 3) / 4 : 0);
-            uint32_t gspan = 0, gmx = 0;
-            for (uint32_t g = 0; g < n_grp; ++g) {
-                const uint32_t lf = g == 0 ? 0 : g0 + 1 + 4 * (g - 1), ll = g == 0 ? g0 : std::min(lf + 3, N_DF);
-                gspan = std::max(gspan, bsym(ll + 1) - bsym(lf));
-                const uint64_t b0 = (uint64_t(t->pdc_off_h[std::max(lf, 1u)]) * bpc) >> 3;
-                const uint64_t b1 = ((uint64_t(t->pdc_off_h[ll + 1]) * bpc + 7) >> 3) + 1;
-                if (b1 > b0) gmx = std::max<uint32_t>(gmx, static_cast<uint32_t>(b1 - b0));
-            }
-            const uint32_t gout = static_cast<uint32_t>((uint64_t(gspan + t->rs.hl) * t->rs.L + t->rs.M - 1) / t->rs.M) + 2 * t->rs.L;
-            if (gout <= 3 * 256 * t->rs.L - 2 * t->rs.L && gmx <= 8192) {
-                a.stream = 1;
-                a.g0_last = g0;
-                a.n_grp = n_grp;
-                a.stage_bytes = (gmx + 3) / 4 * 4;
-                a.lin_len = a.HP + std::max(gspan + a.HP, gout);
-            }
-        }
     }
     a.code = t->code.as<uint32_t>();
     a.pdc_off = t->pdc_off.as<uint32_t>();

@@ -39,9 +39,6 @@ struct tx_args {
     // before them (resampler history) into a linear cyclic-prefixed buffer of lin_len samples
     uint32_t K, n_runs, HP, lin_len, bufB_len;
     uint32_t stage_bytes;  // PDC source bytes of one run staged in LDS (0: read HBM directly)
-    // streaming mode (N_b_DFT_os = 1024): one WG per (packet, antenna) walks symbol groups
-    // {0..g0_last}, then 4 symbols per group; history = the previous group's last HP samples
-    uint32_t stream, g0_last, n_grp;
     uint32_t dbg;          // TEMP: section-skip mask for profiling
     uint32_t pair[12];     // transmit diversity TS pairs, A | B << 4
     const uint32_t* code;

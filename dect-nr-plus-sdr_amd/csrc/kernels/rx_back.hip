@@ -177,6 +177,10 @@ hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st) {
 
 // ===================================================================== cells
 constexpr uint32_t CELL_THREADS = 512;
+#ifndef CELL_WCHUNK_DEF
+#define CELL_WCHUNK_DEF 4
+#endif
+constexpr uint32_t CELL_WCHUNK = CELL_WCHUNK_DEF;  // interpolation taps per weight-load batch
 
 template <int NRX, int NT>
 __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A) {
@@ -240,13 +244,19 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
             float2 h[NRX];
 #pragma unroll
             for (int a = 0; a < NRX; ++a) h[a] = make_float2(0.f, 0.f);
-            for (uint32_t i = 0; i < nI; ++i) {
-                const float wi = w[i];
+            for (uint32_t i0 = 0; i0 < nI; i0 += 2 * CELL_WCHUNK) {
+                float wc[2 * CELL_WCHUNK];
 #pragma unroll
-                for (int a = 0; a < NRX; ++a) {
-                    const float2 z = zfi[a * NT * nd2 + pos + i * step];
-                    h[a].x = fmaf(z.x, wi, h[a].x);
-                    h[a].y = fmaf(z.y, wi, h[a].y);
+                for (uint32_t ii = 0; ii < 2 * CELL_WCHUNK; ++ii) wc[ii] = i0 + ii < nI ? w[i0 + ii] : 0.f;
+#pragma unroll
+                for (uint32_t ii = 0; ii < 2 * CELL_WCHUNK; ++ii) {
+                    if (i0 + ii >= nI) break;
+#pragma unroll
+                    for (int a = 0; a < NRX; ++a) {
+                        const float2 z = zfi[a * NT * nd2 + pos + (i0 + ii) * step];
+                        h[a].x = fmaf(z.x, wc[ii], h[a].x);
+                        h[a].y = fmaf(z.y, wc[ii], h[a].y);
+                    }
                 }
             }
             float2 num = make_float2(0.f, 0.f);
@@ -280,16 +290,26 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
             for (int a = 0; a < NRX; ++a)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) h[a][c] = make_float2(0.f, 0.f);
-            for (uint32_t i = 0; i < nI; ++i) {
+            // weights in chunks of CELL_WCHUNK taps: all of a chunk's (global / L1) weight loads are
+            // in flight together instead of one dependent load per tap
+            for (uint32_t i0 = 0; i0 < nI; i0 += CELL_WCHUNK) {
+                float wc[4][CELL_WCHUNK];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float wi = w[c][i];
-                    const uint32_t p = pos[c] + i * step;
+                for (int c = 0; c < 4; ++c)
 #pragma unroll
-                    for (int a = 0; a < NRX; ++a) {
-                        const float2 z = zfi[a * NT * nd2 + p];
-                        h[a][c].x = fmaf(z.x, wi, h[a][c].x);
-                        h[a][c].y = fmaf(z.y, wi, h[a][c].y);
+                    for (uint32_t ii = 0; ii < CELL_WCHUNK; ++ii) wc[c][ii] = i0 + ii < nI ? w[c][i0 + ii] : 0.f;
+#pragma unroll
+                for (uint32_t ii = 0; ii < CELL_WCHUNK; ++ii) {
+                    if (i0 + ii >= nI) break;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const uint32_t p = pos[c] + (i0 + ii) * step;
+#pragma unroll
+                        for (int a = 0; a < NRX; ++a) {
+                            const float2 z = zfi[a * NT * nd2 + p];
+                            h[a][c].x = fmaf(z.x, wc[c][ii], h[a][c].x);
+                            h[a][c].y = fmaf(z.y, wc[c][ii], h[a][c].y);
+                        }
                     }
                 }
             }

@@ -23,8 +23,10 @@ namespace dnrp::dev {
 
 __constant__ float k_cover[9] = {1, -1, 1, 1, -1, -1, -1, -1, -1};  // stf.hpp:146-151
 
-constexpr uint32_t TX_THREADS = 256;
-constexpr uint32_t TX_MAX_SLOTS = 4;  // K + 1
+constexpr uint32_t TX_THREADS = 256;     // block-FFT path workgroup
+constexpr uint32_t TX_WAVE_MAX = 512;    // wave path: one wavefront per symbol slot, 64 (K + 1) threads
+constexpr uint32_t TX_MAX_SLOTS = 8;     // K + 1 (wave path)
+constexpr uint32_t TX_BLOCK_SLOTS = 4;   // K + 1 (block-FFT path)
 constexpr uint32_t TX_BIN_REG = 4;    // FFT bins per thread per symbol, block path (N_b_DFT_os <= 1024)
 
 __device__ __forceinline__ uint32_t bits_of(uint32_t b0, uint32_t b1, uint32_t bitoff, uint32_t nbits) {
@@ -189,13 +191,13 @@ __device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem, uint32
         float r_h[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const uint32_t i = t + TX_THREADS * j;
+            const uint32_t i = t + blockDim.x * j;
             r_h[j] = i < A.npp ? A.taps_pp[i] : 0.f;
         }
-        uint32_t r_sb[8];
+        uint32_t r_sb[12];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t i = t + TX_THREADS * j, g = w.sbyte0 + i;
+        for (int j = 0; j < 12; ++j) {
+            const uint32_t i = t + blockDim.x * j, g = w.sbyte0 + i;
             r_sb[j] = (i < A.stage_bytes && g < w.pdc_bytes) ? uint32_t(w.dpdc[g] ^ w.cpdc[g]) : 0u;
         }
         if (t < nq) w.qtab[t] = r_q;
@@ -206,13 +208,13 @@ __device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem, uint32
         if (t < A.N_TS) w.wrow[t] = r_w;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-            if (t + TX_THREADS * j < A.npp) w.hpl[t + TX_THREADS * j] = r_h[j];
+            if (t + blockDim.x * j < A.npp) w.hpl[t + blockDim.x * j] = r_h[j];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (t + TX_THREADS * j < A.stage_bytes) w.sb[t + TX_THREADS * j] = static_cast<uint8_t>(r_sb[j]);
+        for (int j = 0; j < 12; ++j)
+            if (t + blockDim.x * j < A.stage_bytes) w.sb[t + blockDim.x * j] = static_cast<uint8_t>(r_sb[j]);
         // tails beyond the register batch (not reached by the shipped configurations)
-        for (uint32_t i = t + 2 * TX_THREADS; i < A.npp; i += TX_THREADS) w.hpl[i] = A.taps_pp[i];
-        for (uint32_t i = t + 8 * TX_THREADS; i < A.stage_bytes; i += TX_THREADS) {
+        for (uint32_t i = t + 2 * blockDim.x; i < A.npp; i += blockDim.x) w.hpl[i] = A.taps_pp[i];
+        for (uint32_t i = t + 12 * blockDim.x; i < A.stage_bytes; i += blockDim.x) {
             const uint32_t g = w.sbyte0 + i;
             w.sb[i] = g < w.pdc_bytes ? static_cast<uint8_t>(w.dpdc[g] ^ w.cpdc[g]) : 0u;
         }
@@ -220,19 +222,19 @@ __device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem, uint32
     }
     // every copy keeps several loads in flight per thread (stage_gen): a plain strided loop waits
     // for each load before issuing the next
-    stage_copy<4>(w.twl, A.tw, w.Nd, threadIdx.x, TX_THREADS);
-    stage_copy<1>(w.qtab, A.qam, 1u << A.N_bps, threadIdx.x, TX_THREADS);
-    for (uint32_t j = threadIdx.x; j < 98; j += TX_THREADS) {
+    stage_copy<4>(w.twl, A.tw, w.Nd, threadIdx.x, blockDim.x);
+    stage_copy<1>(w.qtab, A.qam, 1u << A.N_bps, threadIdx.x, blockDim.x);
+    for (uint32_t j = threadIdx.x; j < 98; j += blockDim.x) {
         const uint32_t bo = (2 * j) >> 3;
         w.pccs[j] = A.qpsk[bits_of(dpcc[bo] ^ A.pcc_seq[bo], 0u, 2 * j, 2)];
     }
-    for (uint32_t i = threadIdx.x; i < A.N_TS; i += TX_THREADS)
+    for (uint32_t i = threadIdx.x; i < A.N_TS; i += blockDim.x)
         w.wrow[i] = A.W[(w.P.codebook * A.N_TX + w.ant) * A.N_TS + i];
-    stage_copy<2>(w.hpl, A.taps_pp, A.npp, threadIdx.x, TX_THREADS);
+    stage_copy<2>(w.hpl, A.taps_pp, A.npp, threadIdx.x, blockDim.x);
     const uint8_t* __restrict__ dp = w.dpdc;
     const uint8_t* __restrict__ cp = w.cpdc;
     const uint32_t sb0 = w.sbyte0, nb = w.pdc_bytes;
-    stage_gen<8>(w.sb, A.stage_bytes, threadIdx.x, TX_THREADS, [&](uint32_t i) {
+    stage_gen<8>(w.sb, A.stage_bytes, threadIdx.x, blockDim.x, [&](uint32_t i) {
         const uint32_t g = sb0 + i;
         return g < nb ? static_cast<uint8_t>(dp[g] ^ cp[g]) : static_cast<uint8_t>(0u);
     });
@@ -242,8 +244,8 @@ __device__ __forceinline__ tx_wg tx_setup(const tx_args& A, float2* smem, uint32
 // zero pads around the run's symbols: history before the packet, flush samples after it
 __device__ __forceinline__ void tx_zero_pads(const tx_wg& w) {
     const uint32_t data_end = w.A->HP + w.bsym(w.l_last + 1) - w.base_q;
-    for (uint32_t i = threadIdx.x; i < w.A->HP; i += TX_THREADS) w.lin[i] = make_float2(0.f, 0.f);
-    for (uint32_t i = data_end + threadIdx.x; i < w.A->lin_len; i += TX_THREADS) w.lin[i] = make_float2(0.f, 0.f);
+    for (uint32_t i = threadIdx.x; i < w.A->HP; i += blockDim.x) w.lin[i] = make_float2(0.f, 0.f);
+    for (uint32_t i = data_end + threadIdx.x; i < w.A->lin_len; i += blockDim.x) w.lin[i] = make_float2(0.f, 0.f);
 }
 
 // resample + mix every output whose newest input lies in the run (the last run adds the flush
@@ -266,7 +268,7 @@ __device__ __forceinline__ void tx_resample(const tx_wg& w) {
         const int q_lo = floor_div(static_cast<int>(m_lo) - static_cast<int>(A.m_star), LR);
         const int q_hi = floor_div(static_cast<int>(m_hi) - static_cast<int>(A.m_star) + LR - 1, LR);
         const int idx_max = static_cast<int>(A.lin_len) - PB::W;
-        if (q_hi - q_lo <= 2 * static_cast<int>(TX_THREADS) && m_hi - m_lo <= A.lin_len) {
+        if (q_hi - q_lo <= 2 * static_cast<int>(blockDim.x) && m_hi - m_lo <= A.lin_len) {
             // coalesced stores: the blocks' outputs go through LDS (over the consumed input buffer)
             // and leave as contiguous 16-B lane stores; a direct store from the block layout would
             // spread every store instruction over ~40 cache lines (lanes 10 outputs apart)
@@ -278,7 +280,7 @@ __device__ __forceinline__ void tx_resample(const tx_wg& w) {
                 const float2* xw[2];
 #pragma unroll
                 for (int r = 0; r < 2; ++r) {
-                    const int q = q_lo + static_cast<int>(threadIdx.x) + r * static_cast<int>(TX_THREADS);
+                    const int q = q_lo + static_cast<int>(threadIdx.x) + r * static_cast<int>(blockDim.x);
                     const int pb = static_cast<int>(A.p_star) + MR * q;
                     xw[r] = w.lin + min(max(pb - HLR + lin_off, 0), idx_max);
                 }
@@ -286,7 +288,7 @@ __device__ __forceinline__ void tx_resample(const tx_wg& w) {
             }
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
-                const int q = q_lo + static_cast<int>(threadIdx.x) + r * static_cast<int>(TX_THREADS);
+                const int q = q_lo + static_cast<int>(threadIdx.x) + r * static_cast<int>(blockDim.x);
                 mbs[r] = static_cast<int>(A.m_star) + LR * q;
                 if (q < q_hi) {
                     if (P.do_mix) {
@@ -303,7 +305,7 @@ __device__ __forceinline__ void tx_resample(const tx_wg& w) {
             float2* ob = w.lin;
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
-                const int q = q_lo + static_cast<int>(threadIdx.x) + r * static_cast<int>(TX_THREADS);
+                const int q = q_lo + static_cast<int>(threadIdx.x) + r * static_cast<int>(blockDim.x);
                 if (q < q_hi) {
 #pragma unroll
                     for (int k = 0; k < LR; ++k) {
@@ -318,13 +320,13 @@ __device__ __forceinline__ void tx_resample(const tx_wg& w) {
             if (threadIdx.x < head) out[m_lo] = ob[0];
             const uint32_t npair = (n - head) / 2;
             float4* o4 = reinterpret_cast<float4*>(out + m_lo + head);
-            for (uint32_t i = threadIdx.x; i < npair; i += TX_THREADS) {
+            for (uint32_t i = threadIdx.x; i < npair; i += blockDim.x) {
                 const float2 a = ob[head + 2 * i], b = ob[head + 2 * i + 1];
                 o4[i] = make_float4(a.x, a.y, b.x, b.y);
             }
             if (threadIdx.x == 0 && ((n - head) & 1u)) out[m_hi - 1] = ob[n - 1];
         } else
-        for (int q = q_lo + static_cast<int>(threadIdx.x); q < q_hi; q += TX_THREADS) {
+        for (int q = q_lo + static_cast<int>(threadIdx.x); q < q_hi; q += blockDim.x) {
             const int mb = static_cast<int>(A.m_star) + LR * q;
             const int pb = static_cast<int>(A.p_star) + MR * q;        // newest input of output mb
             const int idx = min(max(pb - HLR + lin_off, 0), idx_max);  // clamp: only unstored outputs clip
@@ -342,7 +344,7 @@ __device__ __forceinline__ void tx_resample(const tx_wg& w) {
             }
         }
     } else {
-        for (uint32_t m = m_lo + threadIdx.x; m < m_hi; m += TX_THREADS) {
+        for (uint32_t m = m_lo + threadIdx.x; m < m_hi; m += blockDim.x) {
             const uint64_t t = A.delay + uint64_t(m) * A.M;
             const int p = static_cast<int>(t / A.L);
             const uint32_t ph = static_cast<uint32_t>(t % A.L);
@@ -359,12 +361,12 @@ __device__ __forceinline__ void tx_resample(const tx_wg& w) {
         }
     }
     if (w.last_run)
-        for (uint32_t m = m_hi + threadIdx.x; m < A.S; m += TX_THREADS) out[m] = make_float2(0.f, 0.f);
+        for (uint32_t m = m_hi + threadIdx.x; m < A.S; m += blockDim.x) out[m] = make_float2(0.f, 0.f);
 }
 
 // ---- N_b_DFT_os = 1024: wavefront b owns slot b (symbol s0 + b)
 template <int LR, int MR, int HLR>
-__global__ void __launch_bounds__(TX_THREADS) tx_kernel_wave(tx_args A) {
+__global__ void __launch_bounds__(TX_WAVE_MAX) tx_kernel_wave(tx_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     uint32_t rc[16];  // cell codes of the wave's 16 bins per lane, loaded with the staging
     const tx_wg w = tx_setup<true>(A, smem, &rc);
@@ -390,191 +392,6 @@ __global__ void __launch_bounds__(TX_THREADS) tx_kernel_wave(tx_args A) {
     if (!(A.dbg & 4)) tx_resample<LR, MR, HLR>(w);
 }
 
-// ---- N_b_DFT_os = 1024, streaming: one WG per (packet, antenna) walks the packet in symbol
-// groups (group 0 = the STF and the symbols that fill 4 symbol slots, then 4 symbols each). Per
-// group: wave b synthesises symbol b (cell mapping + wave_fft1024 + CP layout) into the linear
-// buffer behind the previous group's last HP samples (resampler history, kept in LDS: no symbol
-// is synthesised twice), then the workgroup resamples + mixes the group's outputs, stages them in
-// LDS and stores them with contiguous 16-B lanes. Tables are staged once per (packet, antenna).
-// Barriers wait for LDS only (global stores drain in the background).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-template <int LR, int MR, int HLR>
-__global__ void __launch_bounds__(TX_THREADS) tx_kernel_stream(tx_args A) {
-    extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    using PB = pp_block<LR, MR, HLR>;
-    tx_wg w;
-    w.A = &A;
-    w.pkt = blockIdx.x / A.N_TX;
-    w.ant = blockIdx.x % A.N_TX;
-    w.P = A.pk[w.pkt];
-    w.Nd = 1024;
-    w.N = A.N_occ;
-    w.Nf = w.N + 1;
-    w.hl = A.hl;
-    w.len0 = A.STF_CP + w.Nd;
-    w.lenD = A.CP + w.Nd;
-    w.lin = smem;
-    w.twl = const_cast<float2*>(A.tw);
-    w.qtab = w.lin + A.lin_len;
-    w.pccs = w.qtab + 256;
-    w.wrow = w.pccs + 98;
-    w.hpl = reinterpret_cast<float*>(w.wrow + 8);
-    w.sb = reinterpret_cast<uint8_t*>(w.hpl + A.npp);
-    w.dpdc = A.pdc_d + size_t(w.pkt) * A.pdc_stride;
-    w.cpdc = w.P.pdc_seq;
-    w.pdc_bytes = (A.G + 7) / 8;
-    const uint32_t t = threadIdx.x, b = t >> 6, lane = t & 63u;
-    const uint32_t bpc = A.N_SS * A.N_bps;
-    auto set_group = [&](uint32_t g) {
-        w.l_first = g == 0 ? 0u : A.g0_last + 1 + 4 * (g - 1);
-        w.l_last = g == 0 ? A.g0_last : min(w.l_first + 3, A.N_DF);
-        w.s0 = w.l_first;
-        w.nsl = w.l_last - w.l_first + 1;
-        w.base_q = w.bsym(w.l_first);
-        w.last_run = (g + 1 == A.n_grp);
-        w.sbyte0 = (A.pdc_off[max(w.l_first, 1u)] * bpc) >> 3;
-    };
-    auto load_codes = [&](uint32_t (&rc)[16]) {
-#pragma unroll
-        for (int m = 0; m < 16; ++m) rc[m] = b < w.nsl ? w.code(w.l_first + b, lane + 64 * m) : 0u;
-    };
-    auto load_bytes = [&](uint32_t (&r)[8]) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t i = t + TX_THREADS * j, g = w.sbyte0 + i;
-            r[j] = (i < A.stage_bytes && g < w.pdc_bytes) ? uint32_t(w.dpdc[g] ^ w.cpdc[g]) : 0u;
-        }
-    };
-    auto store_bytes = [&](const uint32_t (&r)[8]) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (t + TX_THREADS * j < A.stage_bytes) w.sb[t + TX_THREADS * j] = static_cast<uint8_t>(r[j]);
-        for (uint32_t i = t + 8 * TX_THREADS; i < A.stage_bytes; i += TX_THREADS) {  // beyond the batch
-            const uint32_t g = w.sbyte0 + i;
-            w.sb[i] = g < w.pdc_bytes ? static_cast<uint8_t>(w.dpdc[g] ^ w.cpdc[g]) : 0u;
-        }
-    };
-
-    // ---- one-time staging (one memory round trip): tables + group 0's codes and PDC bytes
-    set_group(0);
-    uint32_t rc[16], rb[8];
-    load_codes(rc);
-    load_bytes(rb);
-    {
-        const uint8_t* dpcc = A.pcc_d + size_t(w.pkt) * 25;
-        const uint32_t nq = 1u << A.N_bps;
-        const float2 r_q = t < nq ? A.qam[t] : make_float2(0.f, 0.f);
-        uint32_t r_pcc = 0;
-        if (t < 98) r_pcc = uint32_t(dpcc[(2 * t) >> 3] ^ A.pcc_seq[(2 * t) >> 3]);
-        const float2 r_w = t < A.N_TS ? A.W[(w.P.codebook * A.N_TX + w.ant) * A.N_TS + t] : make_float2(0.f, 0.f);
-        float r_h[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) r_h[j] = t + TX_THREADS * j < A.npp ? A.taps_pp[t + TX_THREADS * j] : 0.f;
-        if (t < nq) w.qtab[t] = r_q;
-        if (t < 98) {  // QPSK (TS 36.211 7.1.2): (1 - 2 b0, 1 - 2 b1) / sqrt(2)
-            const uint32_t q = bits_of(r_pcc, 0u, 2 * t, 2);
-            w.pccs[t] = make_float2((q & 2u) ? -0.70710678f : 0.70710678f, (q & 1u) ? -0.70710678f : 0.70710678f);
-        }
-        if (t < A.N_TS) w.wrow[t] = r_w;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            if (t + TX_THREADS * j < A.npp) w.hpl[t + TX_THREADS * j] = r_h[j];
-        for (uint32_t i = t + 2 * TX_THREADS; i < A.npp; i += TX_THREADS) w.hpl[i] = A.taps_pp[i];
-        store_bytes(rb);
-        for (uint32_t i = t; i < A.HP; i += TX_THREADS) w.lin[i] = make_float2(0.f, 0.f);  // nothing before the packet
-    }
-    lds_barrier();
-
-    float2* out = reinterpret_cast<float2*>(A.out) + size_t(w.pkt * A.N_TX + w.ant) * A.S;
-    const float2 step1 = w.P.do_mix ? phasor(w.P.inc) : make_float2(1.f, 0.f);
-    auto n_out = [&](uint32_t B) {  // outputs m with delay + m*M < B*L (B*L < 2^32: host-checked)
-        const uint32_t tt = B * A.L;
-        return tt > A.delay ? min((tt - A.delay + A.M - 1) / A.M, A.n_keep) : 0u;
-    };
-    for (uint32_t g = 0; g < A.n_grp; ++g) {
-        const uint32_t span = w.bsym(w.l_last + 1) - w.base_q;
-        // ---- symbols of the group (one per wavefront)
-        if (b < w.nsl) {
-            const uint32_t l = w.l_first + b;
-            float2 v[16];
-#pragma unroll
-            for (int m = 0; m < 16; ++m) v[m] = w.bin(rc[m], lane + 64 * m, l);
-            float2* xb = w.slot(l);  // the symbol's own slot (>= 1152 samples) is the exchange buffer
-            wave_fft1024<+1>(v, xb, w.twl, lane);
-            __builtin_amdgcn_wave_barrier();
-            w.put_symbol(l, v, lane);
-        }
-        if (w.last_run)  // flush inputs after the packet: zeros (earlier groups left outputs there)
-            for (uint32_t i = A.HP + span + t; i < A.lin_len; i += TX_THREADS) w.lin[i] = make_float2(0.f, 0.f);
-        lds_barrier();
-        // ---- resample + mix the group's outputs into registers (<= 3 blocks per thread)
-        const uint32_t B_lo = w.base_q, B_hi = w.last_run ? w.bsym(A.N_DF + 1) + w.hl : w.bsym(w.l_last + 1);
-        const uint32_t m_lo = n_out(B_lo), m_hi = n_out(B_hi);
-        const int lin_off = static_cast<int>(A.HP) - static_cast<int>(w.base_q);
-        const int idx_max = static_cast<int>(A.lin_len) - PB::W;
-        const int q_lo = floor_div(static_cast<int>(m_lo) - static_cast<int>(A.m_star), LR);
-        const int q_hi = floor_div(static_cast<int>(m_hi) - static_cast<int>(A.m_star) + LR - 1, LR);
-        auto win = [&](int q) {
-            const int pb = static_cast<int>(A.p_star) + MR * q;
-            return w.lin + min(max(pb - HLR + lin_off, 0), idx_max);  // clamped windows feed unstored outputs only
-        };
-        float2 y[2][LR], y2[LR];
-        {
-            const float2* xw[2] = {win(q_lo + static_cast<int>(t)), win(q_lo + static_cast<int>(t + TX_THREADS))};
-            PB::template run_multi<2>(xw, w.hpl, y);
-        }
-        const int q2 = q_lo + static_cast<int>(t + 2 * TX_THREADS);
-        if (q2 < q_hi) PB::run(win(q2), w.hpl, y2);
-        float2 hist = make_float2(0.f, 0.f);
-        if (t < A.HP) hist = w.lin[span + t];  // the next group's resampler history
-        lds_barrier();
-        // ---- outputs through LDS (behind the history slots) for contiguous stores
-        float2* ob = w.lin + A.HP;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int q = q_lo + static_cast<int>(t + r * TX_THREADS);
-            if (q < q_hi) {
-                const int mb = static_cast<int>(A.m_star) + LR * q;
-                float2 rot = w.P.do_mix ? phasor(w.P.ph0 + static_cast<double>(mb) * w.P.inc) : make_float2(1.f, 0.f);
-#pragma unroll
-                for (int k = 0; k < LR; ++k) {
-                    const uint32_t m = static_cast<uint32_t>(mb + k);
-                    float2 v = r < 2 ? y[r < 2 ? r : 0][k] : y2[k];
-                    if (w.P.do_mix) {
-                        v = cmul(v, rot);
-                        rot = cmul(rot, step1);
-                    }
-                    if (m - m_lo < m_hi - m_lo) ob[m - m_lo] = v;
-                }
-            }
-        }
-        lds_barrier();
-        // ---- next group's codes / PDC bytes in flight while the outputs leave
-        const bool last = w.last_run, more = g + 1 < A.n_grp;
-        if (more) {
-            set_group(g + 1);
-            load_codes(rc);
-            load_bytes(rb);
-        }
-        const uint32_t n = m_hi - m_lo;
-        const uint32_t head = min(n, (reinterpret_cast<uintptr_t>(out + m_lo) & 15u) ? 1u : 0u);
-        if (t < head) out[m_lo] = ob[0];
-        const uint32_t npair = (n - head) / 2;
-        float4* o4 = reinterpret_cast<float4*>(out + m_lo + head);
-        for (uint32_t i = t; i < npair; i += TX_THREADS) {
-            const float2 a = ob[head + 2 * i], c = ob[head + 2 * i + 1];
-            o4[i] = make_float4(a.x, a.y, c.x, c.y);
-        }
-        if (t == 0 && ((n - head) & 1u)) out[m_hi - 1] = ob[n - 1];
-        if (last)  // GI and slot tail (tx.cpp:706-714)
-            for (uint32_t m = m_hi + t; m < A.S; m += TX_THREADS) out[m] = make_float2(0.f, 0.f);
-        if (t < A.HP) w.lin[t] = hist;
-        if (more) store_bytes(rb);
-        lds_barrier();
-    }
-}
-
 // ---- other FFT sizes: workgroup-wide batched Stockham FFT
 template <int LR, int MR, int HLR>
 __global__ void __launch_bounds__(TX_THREADS) tx_kernel(tx_args A) {
@@ -586,15 +403,15 @@ __global__ void __launch_bounds__(TX_THREADS) tx_kernel(tx_args A) {
     const uint32_t npass = fft_num_passes(A.plan);
     float2* gin = ((npass - 1) % 2 == 0) ? bufB : w.lin;
     float2* gout = (gin == w.lin) ? bufB : w.lin;
-    uint32_t rc[TX_MAX_SLOTS][TX_BIN_REG];
+    uint32_t rc[TX_BLOCK_SLOTS][TX_BIN_REG];
 #pragma unroll
-    for (uint32_t b = 0; b < TX_MAX_SLOTS; ++b)
+    for (uint32_t b = 0; b < TX_BLOCK_SLOTS; ++b)
 #pragma unroll
         for (uint32_t r = 0; r < TX_BIN_REG; ++r)
             rc[b][r] = b < w.nsl ? w.code(w.s0 + b, threadIdx.x + r * TX_THREADS) : 0u;
     __syncthreads();
 #pragma unroll
-    for (uint32_t b = 0; b < TX_MAX_SLOTS; ++b) {
+    for (uint32_t b = 0; b < TX_BLOCK_SLOTS; ++b) {
         if (b >= w.nsl) break;
 #pragma unroll
         for (uint32_t r = 0; r < TX_BIN_REG; ++r) {
@@ -619,23 +436,10 @@ size_t tx_lds_bytes(const tx_args& a) {
 
 hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
     const bool wave = a.plan.N == 1024;
-    if (a.stream) {
-        if (!wave || a.N_bps > 8 || a.npp > 2 * TX_THREADS) return hipErrorInvalidValue;
-        const size_t lds = size_t(a.lin_len + 256 + 98 + 8) * sizeof(float2) + a.npp * sizeof(float) +
-                           ((a.stage_bytes + 15) & ~15u);
-        const dim3 g(n * a.N_TX), b(TX_THREADS);
-        if (a.L == 10 && a.M == 9 && a.hl == 22)
-            hipLaunchKernelGGL((tx_kernel_stream<10, 9, 22>), g, b, lds, st, a);
-        else if (a.L == 10 && a.M == 9 && a.hl == 4)
-            hipLaunchKernelGGL((tx_kernel_stream<10, 9, 4>), g, b, lds, st, a);
-        else
-            return hipErrorInvalidValue;
-        return hipGetLastError();
-    }
-    if (a.K + 1 > TX_MAX_SLOTS || a.plan.N > TX_BIN_REG * TX_THREADS || a.N_bps > 8) return hipErrorInvalidValue;
-    if (wave && (a.K + 1) * 64 > TX_THREADS) return hipErrorInvalidValue;
+    if (a.K + 1 > TX_MAX_SLOTS || a.N_bps > 8) return hipErrorInvalidValue;
+    if (!wave && (a.K + 1 > TX_BLOCK_SLOTS || a.plan.N > TX_BIN_REG * TX_THREADS)) return hipErrorInvalidValue;
     const size_t lds = tx_lds_bytes(a);
-    const dim3 g(n * a.N_TX * a.n_runs), b(TX_THREADS);
+    const dim3 g(n * a.N_TX * a.n_runs), b(wave ? 64 * (a.K + 1) : TX_THREADS);
 #define DNRP_TX_LAUNCH(LR, MR, HLR)                                                      \
     do {                                                                                 \
         if (wave)                                                                        \
