@@ -73,4 +73,56 @@ struct pp_block {
     }
 };
 
+// Output-major form of the same block: the W window inputs are read from LDS into registers once
+// (16-B reads where the window start is even), then every output k accumulates exactly its HL + 1
+// taps h[ph_k + d L] — compile-time indices, no zero taps (the input-major table carries
+// W * L - (HL + 1) * L zeros: 32 % of the FMAs for 9/10, 26 % for 10/9). The taps are read
+// through the constant address space: uniform scalar loads into SGPRs, no LDS traffic at all.
+// Summation order d = HL .. 0 (oldest input first) matches pp_block::run bit for bit.
+typedef const __attribute__((address_space(4))) float* ctap_ptr;
+
+template <int L, int M, int HL>
+struct pp_direct {
+    static constexpr int W = HL + 1 + ((L - 1) * M) / L;
+
+    template <bool EVEN>
+    __device__ static __forceinline__ void load(const float2* xw, float2 (&x)[W]) {
+        if constexpr (EVEN) {
+            const float4* x4 = reinterpret_cast<const float4*>(xw);
+#pragma unroll
+            for (int i = 0; i < W / 2; ++i) {
+                const float4 v = x4[i];
+                x[2 * i] = make_float2(v.x, v.y);
+                x[2 * i + 1] = make_float2(v.z, v.w);
+            }
+            if constexpr (W & 1) x[W - 1] = xw[W - 1];
+        } else {
+#pragma unroll
+            for (int i = 0; i < W; ++i) x[i] = xw[i];
+        }
+    }
+
+    __device__ static __forceinline__ void run(const float2 (&x)[W], ctap_ptr h, float2 (&y)[L]) {
+#pragma unroll
+        for (int k = 0; k < L; ++k) y[k] = make_float2(0.f, 0.f);
+        // tap-row order: the L taps of delay d are contiguous (h[ph_k + d L], ph_k a permutation of
+        // 0..L-1), one short scalar load each, so only ~L taps are live in SGPRs at a time
+        uint64_t hp = reinterpret_cast<uint64_t>(h);
+#pragma unroll
+        for (int d = HL; d >= 0; --d) {
+            // opaque tap pointer per row: stops the compiler from hoisting all (HL + 1) L tap loads
+            // ahead of the FMAs (more SGPRs than a wave has -> spills through VGPR lanes)
+            if ((HL - d) % 2 == 0) asm volatile("" : "+s"(hp));
+            const ctap_ptr hr = reinterpret_cast<ctap_ptr>(hp);
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const int o = (k * M) / L, ph = (k * M) % L;
+                const float t = hr[ph + d * L];
+                y[k].x = fmaf(x[HL + o - d].x, t, y[k].x);
+                y[k].y = fmaf(x[HL + o - d].y, t, y[k].y);
+            }
+        }
+    }
+};
+
 }  // namespace dnrp::dev

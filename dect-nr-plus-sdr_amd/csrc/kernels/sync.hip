@@ -19,6 +19,9 @@
 //                      samples around the coarse peak and cross-correlation with every STF
 //                      template (crosscorrelator.cpp:80-251) as one forward FFT plus one inverse
 //                      FFT per template, argmax over the search range, N_eff_TX, fine peak.
+#include <algorithm>
+#include <cstdlib>
+
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
@@ -240,6 +243,141 @@ __global__ void __launch_bounds__(64 * WPG) sync_steps_wave_kernel(sync_args A) 
             A.P[o] = pw;
             A.Cs[o] = c;
         }
+    }
+}
+
+// ---- streaming path (pp resampler, ring fits): one wavefront walks a segment of steps in chunks
+// of 64 polyphase blocks (64 L outputs), software-pipelined: the next chunk's M * 64 new inputs are
+// loaded into registers (coalesced, 8 B per lane and instruction) while the current chunk is
+// resampled, so every wave keeps its own loads in flight instead of waiting on a staging pass.
+// Per wave LDS: the chunk's input window (carry W - M + M * 64) and a 1024-sample output ring
+// holding the pattern lookback; no workgroup barrier anywhere.
+constexpr uint32_t SS_RING = 1024;
+constexpr uint32_t SS_WPG = 4;
+
+template <int LR, int MR, int HLR>
+__host__ __device__ constexpr uint32_t ss_inbuf() {  // float2 per wave, 16-B multiple
+    return ((HLR + 1 + ((LR - 1) * MR) / LR - MR) + 64 * MR + 1) / 2 * 2;
+}
+
+template <int LR, int MR, int HLR, int SQ>
+__global__ void __launch_bounds__(64 * SS_WPG) sync_steps_stream_kernel(sync_args A, uint32_t seg_steps, uint32_t n_seg) {
+    using PD = pp_direct<LR, MR, HLR>;
+    constexpr int W = PD::W, CARRY = W - MR, NEW = 64 * MR;
+    constexpr uint32_t INB = ss_inbuf<LR, MR, HLR>();
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    float2* inb = smem + wv * (INB + SS_RING);
+    float2* ring = inb + INB;
+    const uint32_t gw = blockIdx.x * SS_WPG + wv;
+    const uint32_t seg = gw % n_seg, a = (gw / n_seg) % A.n_ant, w = gw / (n_seg * A.n_ant);
+    if (w >= A.n_win) return;  // no barriers below: a retired wave stalls nobody
+    const uint32_t s_a = seg * seg_steps, s_b = min(s_a + seg_steps, A.n_steps);
+    if (s_a >= s_b) return;
+    const int64_t step = A.step, P = A.pattern;
+    const int64_t m_lo = max<int64_t>(0, s_a * step - P), m_hi = s_b * step;
+    const int64_t ms = A.m_star;
+    const int64_t qa = floordiv(m_lo - ms, LR), qb = floordiv(m_hi - 1 - ms, LR);
+    const uint32_t nch = static_cast<uint32_t>((qb - qa + 64) / 64);
+    const float2* __restrict__ x = A.iq + w * A.win_stride + a * A.ant_stride;
+    const int64_t S = A.S_win;
+    const float* taps_g = A.taps;
+    auto ld = [&](int64_t q) { return (q >= 0 && q < S) ? x[q] : make_float2(0.f, 0.f); };
+    // chunk c: blocks qa + 64 c + lane, window inputs [ib_c, ib_c + CARRY + NEW), ib_c = p_star + M qc - HL
+    const int64_t ib0 = static_cast<int64_t>(A.p_star) + MR * qa - HLR;
+    float2 pre[MR];
+#pragma unroll
+    for (int j = 0; j < MR; ++j) pre[j] = ld(ib0 + CARRY + j * 64 + lane);
+    if (lane < CARRY) inb[lane] = ld(ib0 + lane);
+    uint32_t s_next = s_a;
+    const uint32_t sq = A.step >> 2;  // samples per lane quarter of a step
+    for (uint32_t c = 0; c < nch; ++c) {
+#pragma unroll
+        for (int j = 0; j < MR; ++j) inb[CARRY + j * 64 + lane] = pre[j];
+        if (c + 1 < nch) {
+            const int64_t ibn = ib0 + static_cast<int64_t>(c + 1) * NEW;
+#pragma unroll
+            for (int j = 0; j < MR; ++j) pre[j] = ld(ibn + CARRY + j * 64 + lane);
+        }
+        __builtin_amdgcn_wave_barrier();
+        float2 xv[W];
+        if constexpr ((MR & 1) == 0) PD::template load<true>(inb + MR * lane, xv);
+        else PD::template load<false>(inb + MR * lane, xv);
+        float2 y[LR];
+        {
+            // opaque per chunk: the taps are re-read (scalar loads, K$ hits) instead of being hoisted
+            // into more SGPRs than a wave has
+            const float* tp = taps_g;
+            asm volatile("" : "+s"(tp));
+            PD::run(xv, (ctap_ptr)(tp), y);
+        }
+        const int64_t mb = ms + LR * (qa + 64 * static_cast<int64_t>(c) + lane);
+        // unconditional: outputs m < 0 (first block only) land in slots that outputs 1024 - L..1023
+        // overwrite before any step reads them, and keeping the stores unconditional keeps the
+        // compiler from sinking the FMAs into per-output branches
+#pragma unroll
+        for (int k = 0; k < LR; ++k) ring[static_cast<uint32_t>(mb + k) & (SS_RING - 1)] = y[k];
+        // carry: the last W - M inputs of this window start the next one (disjoint from the reads)
+        if (lane < CARRY) inb[lane] = inb[NEW + lane];
+        __builtin_amdgcn_wave_barrier();
+        // steps complete in the ring: 4 lanes per step, a quarter each, bank-rotated walk
+        const int64_t m_end = ms + LR * (qa + 64 * static_cast<int64_t>(c) + 64);
+        const uint32_t s_end = static_cast<uint32_t>(min<int64_t>(s_b, m_end >= 0 ? m_end / step : 0));
+        for (uint32_t sb = s_next; sb < s_end; sb += 16) {
+            const uint32_t s = sb + (lane >> 2), part = lane & 3u;
+            const uint32_t rot = (2u * ((lane >> 2) & 7u) + ((part >> 1) & 1u) + (lane >> 5)) % sq;
+            float pw = 0.f;
+            float2 cc = make_float2(0.f, 0.f);
+            if (s < s_end) {
+                const uint32_t n0 = s * A.step + part * sq;
+                const bool corr = static_cast<int64_t>(s) * step >= P;
+                if (SQ > 0) {
+                    // quarter of 16 samples: n0 and the pattern lag are multiples of 16, so the
+                    // quarter never wraps the ring; all 32 reads issue back to back
+                    const float2* rv = ring + (n0 & (SS_RING - 1));
+                    const float2* ru = ring + ((n0 - A.pattern) & (SS_RING - 1));
+                    float2 v[SQ > 0 ? SQ : 1], u[SQ > 0 ? SQ : 1];
+#pragma unroll
+                    for (int j = 0; j < SQ; ++j) {
+                        const uint32_t jj = (j + rot) & (SQ - 1);
+                        v[j] = rv[jj];
+                        u[j] = corr ? ru[jj] : make_float2(0.f, 0.f);
+                    }
+#pragma unroll
+                    for (int j = 0; j < SQ; ++j) {
+                        pw = fmaf(v[j].x, v[j].x, fmaf(v[j].y, v[j].y, pw));
+                        cc.x = fmaf(u[j].x, v[j].x, fmaf(u[j].y, v[j].y, cc.x));
+                        cc.y = fmaf(u[j].y, v[j].x, fmaf(-u[j].x, v[j].y, cc.y));
+                    }
+                } else {
+                    for (uint32_t j = 0; j < sq; ++j) {
+                        uint32_t jj = j + rot;
+                        if (jj >= sq) jj -= sq;
+                        const uint32_t n = n0 + jj;
+                        const float2 v = ring[n & (SS_RING - 1)];
+                        pw = fmaf(v.x, v.x, fmaf(v.y, v.y, pw));
+                        if (corr) {
+                            const float2 u = ring[(n - A.pattern) & (SS_RING - 1)];
+                            cc.x = fmaf(u.x, v.x, fmaf(u.y, v.y, cc.x));
+                            cc.y = fmaf(u.y, v.x, fmaf(-u.x, v.y, cc.y));
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 1; o < 4; o <<= 1) {
+                pw += __shfl_xor(pw, o);
+                cc.x += __shfl_xor(cc.x, o);
+                cc.y += __shfl_xor(cc.y, o);
+            }
+            if (s < s_end && part == 0) {
+                const size_t o = (static_cast<size_t>(w) * A.n_ant + a) * A.n_steps + s;
+                A.P[o] = pw;
+                A.Cs[o] = cc;
+            }
+        }
+        s_next = max(s_next, s_end);
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -744,6 +882,24 @@ size_t sync_detect_lds(const sync_args& a) {
 constexpr int SYNC_WPG = SYNC_WPG_DEF;  // waves per workgroup of the wave kernel
 
 hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
+    static const int ss_env = [] {
+        const char* e = std::getenv("DNRP_SYNC_STREAM");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (ss_env && a.L == 9 && a.M == 10 && a.hl == 24 && a.step % 4 == 0 && a.step >= 4 &&
+        64u * 9u + a.step + a.pattern + 9u <= SS_RING) {
+        // segments of ~32 chunks per (window, antenna): enough waves to fill the chip, little warm-up
+        const uint32_t seg_steps = std::max(1u, (32u * 64u * 9u) / a.step);
+        const uint32_t n_seg = (a.n_steps + seg_steps - 1) / seg_steps;
+        const uint64_t waves = uint64_t(n) * a.n_ant * n_seg;
+        const size_t lds = SS_WPG * size_t(ss_inbuf<9, 10, 24>() + SS_RING) * sizeof(float2);
+        const dim3 g(static_cast<uint32_t>((waves + SS_WPG - 1) / SS_WPG)), b(64 * SS_WPG);
+        if (a.step == 64)
+            hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 16>), g, b, lds, st, a, seg_steps, n_seg);
+        else
+            hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 0>), g, b, lds, st, a, seg_steps, n_seg);
+        return hipGetLastError();
+    }
     if (a.L == 9 && a.M == 10 && a.hl == 24) {
         const uint32_t sw = sync_wave_steps(9, a.step, a.pattern);
         const uint32_t waves = n * a.n_ant * ((a.n_steps + sw - 1) / sw);
