@@ -195,6 +195,33 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         *err = DNRP_EUNSUPPORTED;
         return nullptr;
     }
+    {
+        // streaming TX kernel: cell code per FFT bin (tx.hip tx_wg::code layout, 0 for empty bins)
+        const uint32_t N = t->q.N_b_OCC, Nf = N + 1, Nd = t->dm.Nd;
+        if (Nd == 1024) {
+            std::vector<uint32_t> cb(size_t(t->q.N_DF_symb + 1) * 1024, 0u);
+            for (uint32_t l = 0; l <= t->q.N_DF_symb; ++l)
+                for (uint32_t nn = 0; nn < 1024; ++nn) {
+                    uint32_t k = 0xFFFFFFFFu;
+                    if (nn <= N / 2) k = N / 2 + nn;
+                    else if (nn >= t->dm.off_lower && nn < t->dm.off_lower + N / 2) k = nn - t->dm.off_lower;
+                    if (k != 0xFFFFFFFFu) cb[size_t(l) * 1024 + nn] = code[size_t(l) * Nf + k];
+                }
+            for (uint32_t l = 0; l <= t->q.N_DF_symb; ++l)
+                for (uint32_t k = 0; k < Nf; ++k)
+                    if ((code[size_t(l) * Nf + k] & dev::CODE_MASK) == dev::CODE_PCC) {
+                        if (l >= 32) {
+                            *err = DNRP_EUNSUPPORTED;
+                            return nullptr;
+                        }
+                        t->pcc_syms |= 1u << l;
+                    }
+            if (!t->code_bin.upload(cb)) {
+                *err = DNRP_ENOMEM;
+                return nullptr;
+            }
+        }
+    }
     if (!t->code.upload(code) || !t->stf.upload(stf) || !t->pdc_off.upload(m.pdc_sym_off) || !t->W.upload(W) || !t->taps.upload(t->rs.h) || !t->taps_pp.upload(taps_polyphase(t->rs, &t->npp)) ||
         !t->tw.upload(twiddles(t->dm.Nd)) || !t->qam.upload(constellation(t->q.N_bps)) ||
         !t->qpsk.upload(constellation(2))) {
@@ -615,6 +642,37 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     a.pdc_d = pdc_d;
     a.out = iq_out;
     a.pk = ctx->tx_pk.as<dev::tx_pkt>();
+    // streaming kernel (tx.hip tx_stream_kernel) where its geometry holds; DNRP_TX_STREAM=0 disables
+    static const int stream_env = [] {
+        const char* e = std::getenv("DNRP_TX_STREAM");
+        return e ? std::atoi(e) : 1;
+    }();
+    a.stream = 0;
+    if (stream_env && wave && t->code_bin.p && dev::tx_stream_taps_match(t->rs.h.data(), t->rs.h.size()) && a.L == 10 && a.M == 9 && a.hl == 22 && a.CP == 128 && a.STF_CP == 1280 &&
+        a.pattern_len * 9 == a.STF_CP + 1024 && S % 2 == 0 && (reinterpret_cast<uintptr_t>(iq_out) & 15u) == 0) {
+        // every symbol's PDC bytes (SFBC partners included) within its 1024-byte staging window
+        const uint32_t bpc = t->tm.N_SS * t->q.N_bps;
+        bool fits = true;
+        for (uint32_t l = 1; l <= t->q.N_DF_symb && fits; ++l) {
+            const uint64_t j0 = t->pdc_off_h[l] & ~1u, j1 = (uint64_t(t->pdc_off_h[l + 1]) + 1) & ~1ull;
+            const uint64_t ab = ((j0 * bpc) >> 3) & ~15ull, hi = ((j1 * bpc + 7) >> 3) + 1;
+            fits = hi - ab <= 1024;
+        }
+        const int qlo0 = -static_cast<int>((a.p_star + 8) / 9);
+        const int64_t mfirst0 = int64_t(a.m_star) + 10 * qlo0;
+        if (fits) {
+            a.stream = 1;
+            a.code_bin = t->code_bin.as<uint32_t>();
+            a.pcc_syms = t->pcc_syms;
+            a.n_pieces = static_cast<uint32_t>((int64_t(a.n_keep) - mfirst0 + 1279) / 1280);
+            // enough wavefronts for ~8 rounds of 16 per CU; each extra segment costs one history FFT
+            const uint64_t per = uint64_t(n) * a.N_TX;
+            uint32_t ns = static_cast<uint32_t>(std::min<uint64_t>((32768 + per - 1) / per, std::max(1u, a.n_pieces / 8)));
+            a.n_seg = std::max(1u, ns);
+            a.piece_per_seg = (a.n_pieces + a.n_seg - 1) / a.n_seg;
+            a.n_seg = (a.n_pieces + a.piece_per_seg - 1) / a.piece_per_seg;
+        }
+    }
     ctx->tic("tx", st);
     if (dev::launch_tx(a, n, st) != hipSuccess) return DNRP_EDEVICE;
     ctx->toc("tx", st);

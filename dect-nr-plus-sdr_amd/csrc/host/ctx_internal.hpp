@@ -91,6 +91,8 @@ struct tx_tables {
     dev::fft_plan plan{};
     geo::resampler_t rs;
     dbuf code, stf, W, taps, taps_pp, tw, qam, qpsk, pdc_off;
+    dbuf code_bin;  // [N_DF+1][1024] code per FFT bin (streaming TX kernel, N_b_DFT_os = 1024)
+    uint32_t pcc_syms = 0;  // bit l: symbol l carries PCC cells
     uint32_t npp = 0;  // floats in taps_pp
     std::vector<float> wscale;  // per codebook
     std::vector<uint32_t> pdc_off_h;  // host copy of maps.pdc_sym_off

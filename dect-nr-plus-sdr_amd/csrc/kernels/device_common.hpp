@@ -473,6 +473,72 @@ __device__ __forceinline__ void wave_fft1024(float2 (&v)[16], float2* xb, const 
     for (int m = 0; m < 16; ++m) v[m] = o[m];
 }
 
+// Same transform with two twiddle loads per lane instead of 27: pass 2 needs W^(4 kk r), r = 1..15,
+// = powers of one loaded W^(4 kk) (binary-power products, chain depth <= 4); pass 3 needs W^(j),
+// W^(2j), W^(3j) for j = lane + 64 b, and W^(lane + 64 b) = W^lane * exp(SIGN i pi b / 8) with
+// compile-time constants. Fewer live registers where the FFT sits inside a loop; results differ from
+// wave_fft1024 by a few float ulps of the twiddles (~1e-7 relative).
+template <int SIGN>
+__device__ __forceinline__ void wave_fft1024_rt(float2 (&v)[16], float2* xb, const float2* tw, uint32_t lane) {
+    constexpr float C1 = 0.92387953251128675613f, S1 = 0.38268343236508977173f, R2 = 0.70710678118654752440f;
+    dft16<SIGN>(v);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xb[wfft_pad(16 * lane + k)] = v[k];
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t kk = lane & 15u;
+    const float2 w1 = wfft_tw<SIGN>(tw, 4 * kk);
+    const float2 wl = wfft_tw<SIGN>(tw, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = xb[wfft_pad(lane + 64 * r)];
+    {
+        float2 w[16];
+        w[1] = w1;
+        w[2] = cmul(w1, w1);
+        w[4] = cmul(w[2], w[2]);
+        w[8] = cmul(w[4], w[4]);
+        w[3] = cmul(w[2], w1);
+        w[5] = cmul(w[4], w1);
+        w[6] = cmul(w[4], w[2]);
+        w[7] = cmul(w[4], w[3]);
+        w[9] = cmul(w[8], w1);
+        w[10] = cmul(w[8], w[2]);
+        w[11] = cmul(w[8], w[3]);
+        w[12] = cmul(w[8], w[4]);
+        w[13] = cmul(w[8], w[5]);
+        w[14] = cmul(w[8], w[6]);
+        w[15] = cmul(w[8], w[7]);
+#pragma unroll
+        for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], w[r]);
+    }
+    dft16<SIGN>(v);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t zb = (lane >> 4) * 256 + kk;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xb[wfft_pad(zb + 16 * k)] = v[k];
+    __builtin_amdgcn_wave_barrier();
+    float2 o[16];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t j = lane + 64 * b;
+        const float cb = b == 0 ? 1.f : b == 1 ? C1 : b == 2 ? R2 : S1;
+        const float sb = b == 0 ? 0.f : b == 1 ? S1 : b == 2 ? R2 : C1;
+        const float2 e1 = b == 0 ? wl : cmul(wl, make_float2(cb, SIGN * sb));
+        const float2 e2 = cmul(e1, e1), e3 = cmul(e2, e1);
+        float2 a0 = xb[wfft_pad(j)], a1 = xb[wfft_pad(j + 256)], a2 = xb[wfft_pad(j + 512)], a3 = xb[wfft_pad(j + 768)];
+        a1 = cmul(a1, e1);
+        a2 = cmul(a2, e2);
+        a3 = cmul(a3, e3);
+        dft4<SIGN>(a0, a1, a2, a3);
+        o[b] = a0;
+        o[b + 4] = a1;
+        o[b + 8] = a2;
+        o[b + 12] = a3;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = o[m];
+}
+
 // block-wide sum of a double, result valid in all threads (blockDim.x multiple of 64, <= 1024)
 __device__ __forceinline__ double block_sum(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

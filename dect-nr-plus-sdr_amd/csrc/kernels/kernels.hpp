@@ -56,8 +56,14 @@ struct tx_args {
     const uint8_t* pdc_d;
     float* out;
     const tx_pkt* pk;
+    // streaming kernel (tx_stream_kernel, N_b_DFT_os = 1024, L/M = 10/9, CP 128 / STF CP 1280):
+    // one wavefront per (packet, antenna, segment of 1152-sample input pieces)
+    const uint32_t* code_bin;  // [N_DF+1][1024] cell code of every FFT bin (0: empty)
+    uint32_t n_pieces, n_seg, piece_per_seg, stream;
+    uint32_t pcc_syms;         // bit l: symbol l (< 32) carries PCC cells
 };
 hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st);
+bool tx_stream_taps_match(const float* h, size_t n);  // compiled-in 10/9 taps == run-time taps
 
 // ---------------------------------------------------------------- RX
 struct rx_pkt_in {          // from sync_report_t

@@ -126,3 +126,38 @@ struct pp_direct {
 };
 
 }  // namespace dnrp::dev
+
+namespace dnrp::dev {
+
+// pp_direct with the taps as compile-time constants (TP: a generated taps_* struct, build/gen/
+// taps_gen.hpp): every tap is an immediate materialised into an SGPR next to its FMA, zero taps
+// (the filter's padding to a multiple of L) vanish, and no SGPRs or LDS hold a tap table. The host
+// checks its run-time taps against TP::h bit for bit before choosing a kernel built on this.
+template <class TP>
+struct pp_const {
+    static constexpr int L = TP::L, M = TP::M, HL = TP::HL;
+    static constexpr int W = HL + 1 + ((L - 1) * M) / L;
+
+    __device__ static __forceinline__ void run(const float2 (&x)[W], float2 (&y)[L]) {
+#pragma unroll
+        for (int k = 0; k < L; ++k) y[k] = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int d = HL; d >= 0; --d) {
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const int o = (k * M) / L, ph = (k * M) % L;
+                constexpr_if_nonzero(TP::h[ph + d * L], x[HL + o - d], y[k]);
+            }
+        }
+    }
+
+  private:
+    __device__ static __forceinline__ void constexpr_if_nonzero(const float t, const float2 xv, float2& acc) {
+        if (t != 0.f) {  // compile-time after unrolling: padding taps cost nothing (fma(x, 0, a) == a)
+            acc.x = fmaf(xv.x, t, acc.x);
+            acc.y = fmaf(xv.y, t, acc.y);
+        }
+    }
+};
+
+}  // namespace dnrp::dev

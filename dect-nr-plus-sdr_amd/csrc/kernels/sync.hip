@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(64 * SS_WPG) sync_steps_stream_kernel(sync_arg
     constexpr int W = PD::W, CARRY = W - MR, NEW = 64 * MR;
     constexpr uint32_t INB = ss_inbuf<LR, MR, HLR>();
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;  // uniform
     float2* inb = smem + wv * (INB + SS_RING);
     float2* ring = inb + INB;
     const uint32_t gw = blockIdx.x * SS_WPG + wv;

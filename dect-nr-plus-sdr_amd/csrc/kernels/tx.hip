@@ -18,6 +18,7 @@
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
+#include "taps_gen.hpp"
 
 namespace dnrp::dev {
 
@@ -392,6 +393,283 @@ __global__ void __launch_bounds__(TX_WAVE_MAX) tx_kernel_wave(tx_args A) {
     if (!(A.dbg & 4)) tx_resample<LR, MR, HLR>(w);
 }
 
+// ---- streaming TX: N_b_DFT_os = 1024, L/M = 10/9 (os_min 1), CP 128, STF CP 1280.
+// One wavefront walks one (packet, antenna, segment) through 1152-sample input pieces: the STF is
+// pieces 0 and 1, DF symbol l is piece l + 1, later pieces are the zero flush. Per piece: cell
+// mapping into registers -> wave_fft1024 -> the piece's cyclic-prefixed (STF: covered) samples into
+// the wave's LDS buffer behind the 30-sample resampler carry -> 128 polyphase blocks (two per lane,
+// output-major pp_direct, taps in SGPRs) + phase-continuous mixer -> outputs staged through the
+// same buffer and stored as contiguous 16-B lane stores. The next symbol's PDC bytes (and their
+// Gold sequence) are in flight while a piece is resampled. No workgroup barrier after the
+// constellation load; the carry makes every symbol's history free (no extra FFT per run).
+constexpr uint32_t TXS_WPG = 4;
+constexpr uint32_t TXS_PIECE = 1152;                  // input samples per piece = 128 blocks of 9
+constexpr uint32_t TXS_CARRY = 30;                    // inputs before the piece its first window reads
+constexpr uint32_t TXS_BUF = TXS_CARRY + TXS_PIECE;   // float2 per wave
+constexpr uint32_t TXS_XB = 32;                       // FFT exchange / PDC byte staging offset
+constexpr uint32_t TXS_WROW = 12;                     // beamforming row (8) + descrambled PCC bytes (32 B)
+static_assert(TXS_XB + WFFT_XB <= TXS_BUF, "FFT exchange buffer must fit behind the carry");
+
+__device__ __forceinline__ uint32_t txs_sym(uint32_t r, uint32_t N_DF) {  // symbol of piece r (N_DF+1: none)
+    return r <= 1 ? 0u : (r - 1 <= N_DF ? r - 1 : N_DF + 1);
+}
+
+struct txs_wave {
+    const tx_args* A;
+    tx_pkt P;
+    uint32_t pkt, ant, lane;
+    float2 *buf, *wrow, *qtab;
+    const uint8_t *dpdc, *cpdc;
+    uint32_t pdc_bytes;
+
+    // first staged byte of symbol l (16-B aligned), PDC cells from pdc_off[l] & ~1 (SFBC partners)
+    __device__ uint32_t stage_base(uint32_t l) const {
+        const uint32_t j0 = A->pdc_off[l] & ~1u;
+        return ((j0 * A->N_SS * A->N_bps) >> 3) & ~15u;
+    }
+    // raw 16-B chunk of the descrambled PDC bytes at byte g (zero beyond the packet)
+    __device__ uint4 chunk(uint32_t g) const {
+        if (g + 16 <= pdc_bytes) {
+            // the d-bit rows need not be 16-B aligned (byte stride): one unaligned dwordx4 load
+            uint4 d;
+            __builtin_memcpy(&d, dpdc + g, 16);
+            const uint4 c = *reinterpret_cast<const uint4*>(cpdc + g);
+            return make_uint4(d.x ^ c.x, d.y ^ c.y, d.z ^ c.z, d.w ^ c.w);
+        }
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t i = 0; i < 16; ++i)
+            if (g + i < pdc_bytes) w[i >> 2] |= uint32_t(dpdc[g + i] ^ cpdc[g + i]) << (8 * (i & 3));
+        return make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    // branch-free cell values: every source is read unconditionally at an in-bounds (masked)
+    // index and the code type selects the result, so 16 bins per lane cost no divergent control
+    // flow and no exec-mask SGPRs
+    __device__ float2 pcc_sym(const uint8_t* pcb, uint32_t j) const {  // QPSK (TS 36.211 7.1.2) of PCC bits 2j, 2j+1
+        const uint32_t bo = ((2 * j) >> 3) & 31u;
+        const uint32_t q = (uint32_t(pcb[bo]) >> (6u - ((2 * j) & 7u))) & 3u;
+        return make_float2((q & 2u) ? -0.70710678f : 0.70710678f, (q & 1u) ? -0.70710678f : 0.70710678f);
+    }
+    __device__ float2 pdc_sym(const uint8_t* sb, uint32_t ab, uint32_t s) const {
+        if (A->N_bps == 8) return qtab[sb[(s - ab) & 1023u]];
+        const uint32_t lb = s * A->N_bps - 8 * ab, bo = (lb >> 3) & 1022u;
+        return qtab[bits_of(sb[bo], sb[bo + 1], lb, A->N_bps)];
+    }
+    // value of FFT bin n with cell code c in DF symbol l >= 1, scaled (tx.cpp:944-1116, 729-860, 862-871)
+    template <bool PCC>
+    __device__ float2 bin_df(uint32_t c, const uint8_t* sb, uint32_t ab, const uint8_t* pcb) const {
+        const uint32_t ty = c & CODE_MASK, j = c & CODE_J_MASK, pr = (c >> CODE_PAIR_SHIFT) & 0xFFu;
+        float2 x0 = pdc_sym(sb, ab, j);
+        float2 v;
+        if (A->N_TS == 1) {  // SISO (N_SS = 1): PCC and PDC alike
+            if (PCC && ty == CODE_PCC) x0 = pcc_sym(pcb, j);
+            v = cmul(wrow[0], x0);
+        } else if (A->txdiv || (PCC && ty == CODE_PCC)) {
+            // transmit diversity pair (transmit_diversity_precoding.cpp:37-75): the PCC always,
+            // the PDC in the transmit-diversity modes
+            float2 x1 = pdc_sym(sb, ab, j ^ 1u);
+            if (PCC && ty == CODE_PCC) {
+                x0 = pcc_sym(pcb, j);
+                x1 = pcc_sym(pcb, j ^ 1u);
+            }
+            x1 = (j & 1u) ? make_float2(x1.x, -x1.y) : make_float2(-x1.x, x1.y);
+            v = cadd(cmul(wrow[pr & 0xFu], x0), cmul(wrow[pr >> 4], x1));
+        } else {
+            v = make_float2(0.f, 0.f);
+            for (uint32_t ss = 0; ss < A->N_SS; ++ss) v = cadd(v, cmul(wrow[ss], pdc_sym(sb, ab, j * A->N_SS + ss)));
+        }
+        const float2 d = cscale(wrow[j & 7u], (j & 8u) ? -1.f : 1.f);
+        v = ty == CODE_DRS ? d : v;
+        v = (ty == CODE_PDC || ty == CODE_DRS || (PCC && ty == CODE_PCC)) ? v : make_float2(0.f, 0.f);
+        return cscale(v, P.scale_df);
+    }
+    // STF bin n (stf.cpp:185-285 values, STF scaling)
+    __device__ float2 bin_stf(uint32_t c, uint32_t n) const {
+        const uint32_t N = A->N_occ;
+        const uint32_t k = n <= N / 2 ? N / 2 + n : n - A->off_lower;
+        const float2 v = cmul(wrow[0], A->stf[min(k, N)]);
+        return (c & CODE_MASK) == CODE_STF ? cscale(v, P.scale_stf) : make_float2(0.f, 0.f);
+    }
+};
+
+template <int LR, int MR, int HLR>
+__global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_eu(4))) tx_stream_kernel(tx_args A, uint32_t n) {
+    using PD = pp_direct<LR, MR, HLR>;
+    static_assert(PD::W == TXS_CARRY + 1, "carry = window - 1");
+    static_assert(taps_tx_10_9::L == LR && taps_tx_10_9::M == MR && taps_tx_10_9::HL == HLR, "generated taps");
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    float2* qtab = smem;  // [256] per workgroup
+    // wave index made provably uniform: everything derived from it (packet, segment, loop bounds,
+    // pointers) stays in SGPRs and the piece loop is not divergent control flow
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    {
+        const uint32_t nq = 1u << A.N_bps;
+        for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) qtab[i] = A.qam[i];
+    }
+    txs_wave T;
+    T.A = &A;
+    T.lane = lane;
+    T.qtab = qtab;
+    T.buf = smem + 256 + wv * (TXS_BUF + TXS_WROW);
+    T.wrow = T.buf + TXS_BUF;
+    const uint32_t gw = blockIdx.x * TXS_WPG + wv;
+    T.ant = gw % A.N_TX;
+    const uint32_t seg = (gw / A.N_TX) % A.n_seg;
+    T.pkt = gw / (A.N_TX * A.n_seg);
+    const bool live = T.pkt < n;
+    uint8_t* pcb = reinterpret_cast<uint8_t*>(T.wrow + 8);
+    if (live) {
+        T.P = A.pk[T.pkt];
+        if (lane < A.N_TS) T.wrow[lane] = A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS + lane];
+        if (lane < 32) pcb[lane] = lane < 25 ? static_cast<uint8_t>(A.pcc_d[size_t(T.pkt) * 25 + lane] ^ A.pcc_seq[lane]) : 0u;
+    }
+    __syncthreads();  // the only workgroup barrier: qtab / wrow visible
+    if (!live) return;
+    const uint32_t r_a = seg * A.piece_per_seg, r_b = min(r_a + A.piece_per_seg, A.n_pieces);
+    if (r_a >= r_b) return;
+    T.dpdc = A.pdc_d + size_t(T.pkt) * A.pdc_stride;
+    T.cpdc = T.P.pdc_seq;
+    T.pdc_bytes = (A.G + 7) / 8;
+    float2* buf = T.buf;
+    float2* out = reinterpret_cast<float2*>(A.out) + size_t(T.pkt * A.N_TX + T.ant) * A.S;
+    uint8_t* sb = reinterpret_cast<uint8_t*>(buf + TXS_XB);
+    // block grid: piece r holds blocks q = q0 + 128 r + (lane + 64 b), window at buf[base0 + 9 (lane + 64 b)]
+    const int qlo0 = -static_cast<int>((A.p_star + 8) / MR);  // ceil((0 - p_star - 8) / 9)
+    const uint32_t base0 = static_cast<uint32_t>(static_cast<int>(A.p_star) + MR * qlo0 + 8);
+    const int mfirst0 = static_cast<int>(A.m_star) + LR * qlo0;  // first output of piece 0
+    const float2 step1 = T.P.do_mix ? phasor(T.P.inc) : make_float2(1.f, 0.f);
+    if (seg == 0)  // outputs before piece 0's first block see only zero input
+        for (int m = lane; m < mfirst0; m += 64) out[m] = make_float2(0.f, 0.f);
+    const uint32_t r_start = r_a > 0 ? r_a - 1 : 0;
+    if (r_a == 0 && lane < TXS_CARRY) buf[lane] = make_float2(0.f, 0.f);
+    // PDC bytes of the first symbol
+    const uint32_t l_cur = txs_sym(r_start, A.N_DF);
+    uint4 pre = make_uint4(0u, 0u, 0u, 0u);
+    if (l_cur >= 1 && l_cur <= A.N_DF) pre = T.chunk(T.stage_base(l_cur) + 16 * lane);
+    for (uint32_t r = r_start; r < r_b; ++r) {
+        // lid index opaque per piece: lid-dependent addresses are recomputed in the loop instead of
+        // being hoisted out of it as dozens of 64-bit VGPR pairs (loop-invariant code motion)
+        uint32_t lid = lane;
+        asm volatile("" : "+v"(lid));
+        const uint32_t l = txs_sym(r, A.N_DF);
+        float2 v[16];
+        const bool real = l <= A.N_DF;
+        if (real) {
+            // stage this symbol's bytes, prefetch the next symbol's
+            const uint32_t ab = (l >= 1) ? T.stage_base(l) : 0u;
+            if (l >= 1) reinterpret_cast<uint4*>(sb)[lid] = pre;
+            const uint32_t ln = txs_sym(r + 1, A.N_DF);
+            if (r + 1 < r_b && ln != l && ln >= 1 && ln <= A.N_DF) pre = T.chunk(T.stage_base(ln) + 16 * lid);
+            uint32_t cd[16];
+            const uint32_t* crow = A.code_bin + size_t(l) * 1024;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) cd[m] = crow[lid + 64 * m];
+            __builtin_amdgcn_wave_barrier();
+            if (l == 0) {
+#pragma unroll
+                for (int m = 0; m < 16; ++m) v[m] = T.bin_stf(cd[m], lid + 64 * m);
+            } else if ((l < 32) && ((A.pcc_syms >> l) & 1u)) {
+#pragma unroll
+                for (int m = 0; m < 16; ++m) v[m] = T.bin_df<true>(cd[m], sb, ab, pcb);
+            } else {
+#pragma unroll
+                for (int m = 0; m < 16; ++m) v[m] = T.bin_df<false>(cd[m], sb, ab, pcb);
+            }
+            __builtin_amdgcn_wave_barrier();
+            {
+                // two twiddle loads per lid (27 hoisted twiddles would hold 54 VGPRs over the loop)
+                wave_fft1024_rt<+1>(v, buf + TXS_XB, A.tw, lid);
+            }
+            __builtin_amdgcn_wave_barrier();
+            // piece samples: sample i of the symbol is X[(i - cp) mod 1024] (STF: times the cover)
+            const uint32_t cp = l == 0 ? A.STF_CP : A.CP, len = cp + 1024;
+            const uint32_t i0 = (l == 0 && r == 1) ? TXS_PIECE : 0u;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const uint32_t nn = lid + 64 * m;
+                for (uint32_t i = (nn + cp) & 1023u; i < len; i += 1024)
+                    if (i - i0 < TXS_PIECE) {
+                        float2 x = v[m];
+                        if (l == 0) x = cscale(x, k_cover[min(i / A.pattern_len, 8u)]);
+                        buf[TXS_CARRY + i - i0] = x;
+                    }
+            }
+        } else {
+            for (uint32_t i = lid; i < TXS_PIECE; i += 64) buf[TXS_CARRY + i] = make_float2(0.f, 0.f);
+        }
+        __builtin_amdgcn_wave_barrier();
+        float2 creg = make_float2(0.f, 0.f);
+        if (r >= r_a) {
+            float2 y[2][LR];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                __builtin_amdgcn_sched_barrier(0);  // one window live at a time
+                float2 xv[PD::W];
+                PD::template load<false>(buf + base0 + MR * (lid + 64 * b), xv);
+                pp_const<taps_tx_10_9>::run(xv, y[b]);
+                if (T.P.do_mix) {
+                    const int mb = mfirst0 + static_cast<int>(1280 * r) + LR * static_cast<int>(lid + 64 * b);
+                    float2 rot = phasor(T.P.ph0 + static_cast<double>(mb) * T.P.inc);
+#pragma unroll
+                    for (int k = 0; k < LR; ++k) {
+                        y[b][k] = cmul(y[b][k], rot);
+                        rot = cmul(rot, step1);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lid < TXS_CARRY) creg = buf[TXS_PIECE + lid];
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+#pragma unroll
+                for (int k = 0; k < LR; ++k) buf[LR * lid + k] = y[b][k];
+                __builtin_amdgcn_wave_barrier();
+                const int m0 = mfirst0 + static_cast<int>(1280 * r) + 640 * b;
+                if (m0 >= 0 && m0 + 640 <= static_cast<int>(A.n_keep)) {
+                    // contiguous 16-B lid stores (the row base is 16-B aligned, host-checked)
+                    const uint32_t head = static_cast<uint32_t>(m0) & 1u;
+                    if (lid == 0 && head) out[m0] = buf[0];
+                    float4* o4 = reinterpret_cast<float4*>(out + m0 + head);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        const uint32_t e = lid + 64 * i;
+                        if (e < (640 - head) / 2) {
+                            const float2 p0 = buf[head + 2 * e], p1 = buf[head + 2 * e + 1];
+                            o4[e] = make_float4(p0.x, p0.y, p1.x, p1.y);
+                        }
+                    }
+                    if (lid == 0 && head) out[m0 + 639] = buf[639];
+                } else {
+                    for (int i = lid; i < 640; i += 64) {
+                        const int m = m0 + i;
+                        if (m >= 0 && m < static_cast<int>(A.S))
+                            out[m] = m < static_cast<int>(A.n_keep) ? buf[i] : make_float2(0.f, 0.f);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        } else if (lid < TXS_CARRY) {
+            creg = buf[TXS_PIECE + lid];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lid < TXS_CARRY) buf[lid] = creg;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (r_b == A.n_pieces) {  // slot tail (GI and beyond): zeros
+        const int m_end = mfirst0 + static_cast<int>(1280 * A.n_pieces);
+        for (int m = max(m_end, 0) + static_cast<int>(lane); m < static_cast<int>(A.S); m += 64) out[m] = make_float2(0.f, 0.f);
+    }
+}
+
+bool tx_stream_taps_match(const float* h, size_t n) {  // run-time taps == compiled-in taps, bitwise
+    if (n != static_cast<size_t>(taps_tx_10_9::N)) return false;
+    for (size_t i = 0; i < n; ++i)
+        if (__builtin_bit_cast(uint32_t, h[i]) != __builtin_bit_cast(uint32_t, taps_tx_10_9::h[i])) return false;
+    return true;
+}
+
+size_t tx_stream_lds() { return (256 + TXS_WPG * (TXS_BUF + TXS_WROW)) * sizeof(float2); }
+
 // ---- other FFT sizes: workgroup-wide batched Stockham FFT
 template <int LR, int MR, int HLR>
 __global__ void __launch_bounds__(TX_THREADS) tx_kernel(tx_args A) {
@@ -435,6 +713,12 @@ size_t tx_lds_bytes(const tx_args& a) {
 }
 
 hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
+    if (a.stream) {
+        const uint64_t waves = uint64_t(n) * a.N_TX * a.n_seg;
+        hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22>), dim3(static_cast<uint32_t>((waves + TXS_WPG - 1) / TXS_WPG)),
+                           dim3(64 * TXS_WPG), tx_stream_lds(), st, a, n);
+        return hipGetLastError();
+    }
     const bool wave = a.plan.N == 1024;
     if (a.K + 1 > TX_MAX_SLOTS || a.N_bps > 8) return hipErrorInvalidValue;
     if (!wave && (a.K + 1 > TX_BLOCK_SLOTS || a.plan.N > TX_BIN_REG * TX_THREADS)) return hipErrorInvalidValue;
