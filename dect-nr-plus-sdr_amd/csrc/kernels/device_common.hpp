@@ -478,16 +478,15 @@ __device__ __forceinline__ void wave_fft1024(float2 (&v)[16], float2* xb, const 
 // W^(2j), W^(3j) for j = lane + 64 b, and W^(lane + 64 b) = W^lane * exp(SIGN i pi b / 8) with
 // compile-time constants. Fewer live registers where the FFT sits inside a loop; results differ from
 // wave_fft1024 by a few float ulps of the twiddles (~1e-7 relative).
+// w1 = W^(4 (lane & 15)), wl = W^lane (SIGN-signed): the caller may keep them in registers
 template <int SIGN>
-__device__ __forceinline__ void wave_fft1024_rt(float2 (&v)[16], float2* xb, const float2* tw, uint32_t lane) {
+__device__ __forceinline__ void wave_fft1024_rt(float2 (&v)[16], float2* xb, float2 w1, float2 wl, uint32_t lane) {
     constexpr float C1 = 0.92387953251128675613f, S1 = 0.38268343236508977173f, R2 = 0.70710678118654752440f;
     dft16<SIGN>(v);
 #pragma unroll
     for (int k = 0; k < 16; ++k) xb[wfft_pad(16 * lane + k)] = v[k];
     __builtin_amdgcn_wave_barrier();
     const uint32_t kk = lane & 15u;
-    const float2 w1 = wfft_tw<SIGN>(tw, 4 * kk);
-    const float2 wl = wfft_tw<SIGN>(tw, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = xb[wfft_pad(lane + 64 * r)];
     {
@@ -537,6 +536,11 @@ __device__ __forceinline__ void wave_fft1024_rt(float2 (&v)[16], float2* xb, con
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = o[m];
+}
+
+template <int SIGN>
+__device__ __forceinline__ void wave_fft1024_rt(float2 (&v)[16], float2* xb, const float2* tw, uint32_t lane) {
+    wave_fft1024_rt<SIGN>(v, xb, wfft_tw<SIGN>(tw, 4 * (lane & 15u)), wfft_tw<SIGN>(tw, lane), lane);
 }
 
 // block-wide sum of a double, result valid in all threads (blockDim.x multiple of 64, <= 1024)

@@ -410,6 +410,8 @@ constexpr uint32_t TXS_XB = 32;                       // FFT exchange / PDC byte
 constexpr uint32_t TXS_WROW = 12;                     // beamforming row (8) + descrambled PCC bytes (32 B)
 static_assert(TXS_XB + WFFT_XB <= TXS_BUF, "FFT exchange buffer must fit behind the carry");
 
+enum { TXS_SISO = 0, TXS_TXDIV = 1, TXS_SM = 2 };
+
 __device__ __forceinline__ uint32_t txs_sym(uint32_t r, uint32_t N_DF) {  // symbol of piece r (N_DF+1: none)
     return r <= 1 ? 0u : (r - 1 <= N_DF ? r - 1 : N_DF + 1);
 }
@@ -449,24 +451,26 @@ struct txs_wave {
         const uint32_t q = (uint32_t(pcb[bo]) >> (6u - ((2 * j) & 7u))) & 3u;
         return make_float2((q & 2u) ? -0.70710678f : 0.70710678f, (q & 1u) ? -0.70710678f : 0.70710678f);
     }
+    template <bool Q8>
     __device__ float2 pdc_sym(const uint8_t* sb, uint32_t ab, uint32_t s) const {
-        if (A->N_bps == 8) return qtab[sb[(s - ab) & 1023u]];
+        if (Q8) return qtab[sb[(s - ab) & 1023u]];
         const uint32_t lb = s * A->N_bps - 8 * ab, bo = (lb >> 3) & 1022u;
         return qtab[bits_of(sb[bo], sb[bo + 1], lb, A->N_bps)];
     }
     // value of FFT bin n with cell code c in DF symbol l >= 1, scaled (tx.cpp:944-1116, 729-860, 862-871)
-    template <bool PCC>
+    // MODE: TXS_SISO (N_TS = 1), TXS_TXDIV (transmit diversity), TXS_SM (N_SS streams, PCC paired)
+    template <int MODE, bool Q8, bool PCC>
     __device__ float2 bin_df(uint32_t c, const uint8_t* sb, uint32_t ab, const uint8_t* pcb) const {
         const uint32_t ty = c & CODE_MASK, j = c & CODE_J_MASK, pr = (c >> CODE_PAIR_SHIFT) & 0xFFu;
-        float2 x0 = pdc_sym(sb, ab, j);
+        float2 x0 = pdc_sym<Q8>(sb, ab, j);
         float2 v;
-        if (A->N_TS == 1) {  // SISO (N_SS = 1): PCC and PDC alike
+        if (MODE == TXS_SISO) {  // SISO (N_SS = 1): PCC and PDC alike
             if (PCC && ty == CODE_PCC) x0 = pcc_sym(pcb, j);
             v = cmul(wrow[0], x0);
-        } else if (A->txdiv || (PCC && ty == CODE_PCC)) {
+        } else if (MODE == TXS_TXDIV || (PCC && ty == CODE_PCC)) {
             // transmit diversity pair (transmit_diversity_precoding.cpp:37-75): the PCC always,
             // the PDC in the transmit-diversity modes
-            float2 x1 = pdc_sym(sb, ab, j ^ 1u);
+            float2 x1 = pdc_sym<Q8>(sb, ab, j ^ 1u);
             if (PCC && ty == CODE_PCC) {
                 x0 = pcc_sym(pcb, j);
                 x1 = pcc_sym(pcb, j ^ 1u);
@@ -475,7 +479,7 @@ struct txs_wave {
             v = cadd(cmul(wrow[pr & 0xFu], x0), cmul(wrow[pr >> 4], x1));
         } else {
             v = make_float2(0.f, 0.f);
-            for (uint32_t ss = 0; ss < A->N_SS; ++ss) v = cadd(v, cmul(wrow[ss], pdc_sym(sb, ab, j * A->N_SS + ss)));
+            for (uint32_t ss = 0; ss < A->N_SS; ++ss) v = cadd(v, cmul(wrow[ss], pdc_sym<Q8>(sb, ab, j * A->N_SS + ss)));
         }
         const float2 d = cscale(wrow[j & 7u], (j & 8u) ? -1.f : 1.f);
         v = ty == CODE_DRS ? d : v;
@@ -491,7 +495,7 @@ struct txs_wave {
     }
 };
 
-template <int LR, int MR, int HLR>
+template <int LR, int MR, int HLR, int MODE, bool Q8>
 __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_eu(4))) tx_stream_kernel(tx_args A, uint32_t n) {
     using PD = pp_direct<LR, MR, HLR>;
     static_assert(PD::W == TXS_CARRY + 1, "carry = window - 1");
@@ -537,6 +541,8 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
     const uint32_t base0 = static_cast<uint32_t>(static_cast<int>(A.p_star) + MR * qlo0 + 8);
     const int mfirst0 = static_cast<int>(A.m_star) + LR * qlo0;  // first output of piece 0
     const float2 step1 = T.P.do_mix ? phasor(T.P.inc) : make_float2(1.f, 0.f);
+    // the FFT's two lane twiddles, loaded once (wave_fft1024_rt)
+    const float2 tw1 = wfft_tw<+1>(A.tw, 4 * (lane & 15u)), twl = wfft_tw<+1>(A.tw, lane);
     if (seg == 0)  // outputs before piece 0's first block see only zero input
         for (int m = lane; m < mfirst0; m += 64) out[m] = make_float2(0.f, 0.f);
     const uint32_t r_start = r_a > 0 ? r_a - 1 : 0;
@@ -569,29 +575,35 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
                 for (int m = 0; m < 16; ++m) v[m] = T.bin_stf(cd[m], lid + 64 * m);
             } else if ((l < 32) && ((A.pcc_syms >> l) & 1u)) {
 #pragma unroll
-                for (int m = 0; m < 16; ++m) v[m] = T.bin_df<true>(cd[m], sb, ab, pcb);
+                for (int m = 0; m < 16; ++m) v[m] = T.template bin_df<MODE, Q8, true>(cd[m], sb, ab, pcb);
             } else {
 #pragma unroll
-                for (int m = 0; m < 16; ++m) v[m] = T.bin_df<false>(cd[m], sb, ab, pcb);
+                for (int m = 0; m < 16; ++m) v[m] = T.template bin_df<MODE, Q8, false>(cd[m], sb, ab, pcb);
             }
             __builtin_amdgcn_wave_barrier();
             {
-                // two twiddle loads per lid (27 hoisted twiddles would hold 54 VGPRs over the loop)
-                wave_fft1024_rt<+1>(v, buf + TXS_XB, A.tw, lid);
+                // two lane twiddles held over the loop (27 hoisted ones would cost 54 VGPRs)
+                // laundered: keeps LICM from hoisting the twiddle powers derived from them
+                float2 w1 = tw1, wl = twl;
+                asm volatile("" : "+v"(w1.x), "+v"(w1.y), "+v"(wl.x), "+v"(wl.y));
+                wave_fft1024_rt<+1>(v, buf + TXS_XB, w1, wl, lid);
             }
             __builtin_amdgcn_wave_barrier();
             // piece samples: sample i of the symbol is X[(i - cp) mod 1024] (STF: times the cover)
-            const uint32_t cp = l == 0 ? A.STF_CP : A.CP, len = cp + 1024;
-            const uint32_t i0 = (l == 0 && r == 1) ? TXS_PIECE : 0u;
+            if (l >= 1) {  // DF symbol (CP 128): sample nn + 128, CP copies of the last 128 (m >= 14)
 #pragma unroll
-            for (int m = 0; m < 16; ++m) {
-                const uint32_t nn = lid + 64 * m;
-                for (uint32_t i = (nn + cp) & 1023u; i < len; i += 1024)
-                    if (i - i0 < TXS_PIECE) {
-                        float2 x = v[m];
-                        if (l == 0) x = cscale(x, k_cover[min(i / A.pattern_len, 8u)]);
-                        buf[TXS_CARRY + i - i0] = x;
-                    }
+                for (int m = 0; m < 16; ++m) {
+                    buf[TXS_CARRY + 128 + lid + 64 * m] = v[m];
+                    if (m >= 14) buf[TXS_CARRY + lid + 64 * (m - 14)] = v[m];
+                }
+            } else {  // STF (CP 1280, covered): piece r holds samples [1152 r, 1152 r + 1152)
+                const uint32_t cp = A.STF_CP, len = cp + 1024, i0 = r == 1 ? TXS_PIECE : 0u;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) {
+                    const uint32_t nn = lid + 64 * m;
+                    for (uint32_t i = (nn + cp) & 1023u; i < len; i += 1024)
+                        if (i - i0 < TXS_PIECE) buf[TXS_CARRY + i - i0] = cscale(v[m], k_cover[min(i / A.pattern_len, 8u)]);
+                }
             }
         } else {
             for (uint32_t i = lid; i < TXS_PIECE; i += 64) buf[TXS_CARRY + i] = make_float2(0.f, 0.f);
@@ -715,8 +727,19 @@ size_t tx_lds_bytes(const tx_args& a) {
 hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
     if (a.stream) {
         const uint64_t waves = uint64_t(n) * a.N_TX * a.n_seg;
-        hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22>), dim3(static_cast<uint32_t>((waves + TXS_WPG - 1) / TXS_WPG)),
-                           dim3(64 * TXS_WPG), tx_stream_lds(), st, a, n);
+        const dim3 g(static_cast<uint32_t>((waves + TXS_WPG - 1) / TXS_WPG)), b(64 * TXS_WPG);
+        const int mode = a.N_TS == 1 ? TXS_SISO : a.txdiv ? TXS_TXDIV : TXS_SM;
+#define DNRP_TXS(MODE, Q8) hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8>), g, b, tx_stream_lds(), st, a, n)
+        if (a.N_bps == 8) {
+            if (mode == TXS_SISO) DNRP_TXS(TXS_SISO, true);
+            else if (mode == TXS_TXDIV) DNRP_TXS(TXS_TXDIV, true);
+            else DNRP_TXS(TXS_SM, true);
+        } else {
+            if (mode == TXS_SISO) DNRP_TXS(TXS_SISO, false);
+            else if (mode == TXS_TXDIV) DNRP_TXS(TXS_TXDIV, false);
+            else DNRP_TXS(TXS_SM, false);
+        }
+#undef DNRP_TXS
         return hipGetLastError();
     }
     const bool wave = a.plan.N == 1024;
