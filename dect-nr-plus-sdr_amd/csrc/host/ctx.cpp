@@ -394,6 +394,14 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t) {
     a.pin = ctx->rx_in.as<dev::rx_pkt_in>();
     a.st = ctx->rx_st.as<dev::rx_pkt_state>();
     a.Y = ctx->Y.as<float2>();
+    // streaming FFT front end (rx.hip rx_fft_stream_kernel): opt-in with DNRP_RX_STREAM=1. Parity
+    // green on MI355X but 17.1 ms vs 7.4 ms per 4096-slot PDC launch (52.8 GB HBM traffic per
+    // launch vs 20.3 GB: register spills), so rx_fft_wave_kernel stays the default
+    static const int rx_stream_env = [] {
+        const char* e = std::getenv("DNRP_RX_STREAM");
+        return e ? std::atoi(e) : 0;
+    }();
+    a.stream = (rx_stream_env && dev::rx_stream_taps_match(t->rs.h.data(), t->rs.h.size())) ? 1u : 0u;
     return a;
 }
 

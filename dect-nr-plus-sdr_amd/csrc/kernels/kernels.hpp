@@ -98,8 +98,10 @@ struct rx_front_args {
     const rx_pkt_in* pin;
     rx_pkt_state* st;
     float2* Y;                 // [n][N_RX][n_sym_total][Nf_pad]
+    uint32_t stream;           // rx_fft_stream_kernel allowed (host: compiled-in taps match)
 };
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);
+bool rx_stream_taps_match(const float* h, size_t n);  // compiled-in 9/10 taps == run-time taps
 hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st);
 
 // back end, see geometry.hpp rx_plan_t (identical layouts)
