@@ -362,7 +362,7 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
     return r;
 }
 
-dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t) {
+dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, const uint32_t* sel) {
     dev::rx_front_args a{};
     a.plan = t->plan;
     a.N_occ = t->N_occ;
@@ -390,7 +390,8 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t) {
     a.npp = t->npp;
     a.tw = t->tw.as<float2>();
     a.stf = t->stf.as<float2>();
-    a.iq = reinterpret_cast<const float2*>(ctx->rx_iq);
+    a.iq = reinterpret_cast<const float2*>(iq);
+    a.sel = sel;
     a.pin = ctx->rx_in.as<dev::rx_pkt_in>();
     a.st = ctx->rx_st.as<dev::rx_pkt_state>();
     a.Y = ctx->Y.as<float2>();
@@ -406,10 +407,12 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t) {
 }
 
 // back-end launches of one phase: SNR chain, then cells (rx_back.hip)
-int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t n, bool pdc, uint32_t N_bps,
-                const uint32_t* kk, const uint16_t* pdc_sym, int16_t* llr, uint32_t llr_stride, hipStream_t st) {
+int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t n, const uint32_t* sel, bool pdc,
+                uint32_t N_bps, const uint32_t* kk, const uint16_t* pdc_sym, int16_t* llr, uint32_t llr_stride,
+                hipStream_t st) {
     const char* name = pdc ? "rx_pdc" : "rx_pcc";
-    if (!ctx->lut_d.ensure(size_t(ctx->cfg.max_batch) * std::max(plan.n_dops, 1u))) return DNRP_ENOMEM;
+    if (plan.n_dops > dev::RX_MAX_DOPS) return DNRP_EUNSUPPORTED;
+    if (!ctx->lut_d.ensure(size_t(ctx->cfg.max_batch) * dev::RX_MAX_DOPS)) return DNRP_ENOMEM;
     dev::rx_snr_args s{};
     s.N_RX = ctx->cfg.N_TX_max;
     s.Nf_pad = ctx->rx_Nf_pad;
@@ -425,6 +428,7 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     s.Y = ctx->Y.as<float2>();
     s.st = ctx->rx_st.as<dev::rx_pkt_state>();
     s.lut_d = ctx->lut_d.as<uint8_t>();
+    s.sel = sel;
     dev::rx_cells_args c{};
     c.N_occ = t->N_occ;
     c.N_RX = ctx->cfg.N_TX_max;
@@ -452,6 +456,7 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     c.pdc_seq = static_cast<const uint8_t* const*>(ctx->pdc_seq_ptrs.p);
     c.llr = llr;
     c.llr_stride = llr_stride;
+    c.sel = sel;
     ctx->tic(name, st);
     if (dev::launch_rx_snr(s, n, st) != hipSuccess) return DNRP_EDEVICE;
     if (plan.n_epochs && dev::launch_rx_cells(c, n, st) != hipSuccess) return DNRP_EDEVICE;
@@ -690,50 +695,91 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
 int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, const float* iq_in, uint32_t S_in,
                       int16_t* pcc_llr, dnrp_pcc_report* rep, void* stream) {
     if (!ctx || (n > 0 && (!sr || !iq_in || !pcc_llr))) return DNRP_EINVAL;
+    ctx->rx_valid = false;
     if (n == 0) return DNRP_OK;
     if (n > ctx->cfg.max_batch) return DNRP_ENOMEM;
     (void)hipSetDevice(ctx->cfg.device);
-    for (uint32_t i = 1; i < n; ++i)
-        if (sr[i].u != sr[0].u || sr[i].b != sr[0].b || sr[i].N_eff_TX != sr[0].N_eff_TX) return DNRP_EINVAL;
+    // packets grouped by (u, b, N_eff_TX) of their sync report: one launch set per group, each
+    // packet processed exactly as an independent demoddecod_rx_pcc call (rx_synced.cpp:186-323)
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::vector<uint32_t>> groups;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (sr[i].fine_peak_time >= static_cast<int64_t>(S_in) || sr[i].fine_peak_time <= -static_cast<int64_t>(S_in))
+            return DNRP_EINVAL;
+        groups[std::make_tuple(sr[i].u, sr[i].b, sr[i].N_eff_TX)].push_back(i);
+    }
     int err = DNRP_OK;
-    rx1_tables* t = get_rx1(ctx, sr[0].u, sr[0].b, sr[0].N_eff_TX, &err);
-    if (!t) return err;
+    const uint64_t dect = uint64_t(S_in) * ctx->cfg.M / ctx->cfg.L;  // DECT-rate samples in the window
+    std::vector<std::pair<rx1_tables*, const std::vector<uint32_t>*>> gl;
+    uint32_t cap_max = 0, nf_max = 0;
+    ctx->rx_slot_t.assign(n, nullptr);
+    ctx->rx_slot_cap.assign(n, 0);
+    for (const auto& g : groups) {
+        rx1_tables* t = get_rx1(ctx, std::get<0>(g.first), std::get<1>(g.first), std::get<2>(g.first), &err);
+        if (!t) return err;
+        // symbols that fit into the window: (S_in * M/L - STF) / symbol
+        const uint64_t n_stf = t->STF_CP + t->Nd;
+        if (dect < n_stf + t->CP + t->Nd) return DNRP_EINVAL;
+        const uint32_t cap = static_cast<uint32_t>((dect - n_stf) / (t->CP + t->Nd));
+        if (cap < t->pcc_max) return DNRP_EINVAL;
+        cap_max = std::max(cap_max, cap);
+        nf_max = std::max(nf_max, (t->N_occ + 1 + 63) / 64 * 64);
+        for (uint32_t i : g.second) {
+            ctx->rx_slot_t[i] = t;
+            ctx->rx_slot_cap[i] = cap;
+        }
+        gl.emplace_back(t, &g.second);
+    }
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // symbols that fit into the window: (S_in * M/L - STF) / symbol
-    const uint64_t dect = uint64_t(S_in) * ctx->cfg.M / ctx->cfg.L;
-    const uint64_t n_stf = t->STF_CP + t->Nd;
-    if (dect < n_stf + t->CP + t->Nd) return DNRP_EINVAL;
-    ctx->rx_nsym_cap = static_cast<uint32_t>((dect - n_stf) / (t->CP + t->Nd));
-    if (ctx->rx_nsym_cap < t->pcc_max) return DNRP_EINVAL;
-    ctx->rx_Nf_pad = (t->N_occ + 1 + 63) / 64 * 64;
+    ctx->rx_nsym_cap = cap_max;
+    ctx->rx_Nf_pad = nf_max;
     ctx->rx_S_in = S_in;
-    ctx->rx_iq = iq_in;
     ctx->rx_n = n;
     const size_t ybytes = size_t(n) * ctx->cfg.N_TX_max * (ctx->rx_nsym_cap + 1) * ctx->rx_Nf_pad * sizeof(float2);
     if (!ctx->Y.ensure(ybytes) || !ctx->rx_in.ensure(sizeof(dev::rx_pkt_in) * ctx->cfg.max_batch) ||
-        !ctx->rx_st.ensure(sizeof(dev::rx_pkt_state) * ctx->cfg.max_batch))
+        !ctx->rx_st.ensure(sizeof(dev::rx_pkt_state) * ctx->cfg.max_batch) ||
+        !ctx->rx_sel.ensure(2 * sizeof(uint32_t) * ctx->cfg.max_batch))
         return DNRP_ENOMEM;
     auto* pin = static_cast<dev::rx_pkt_in*>(ctx->st_rxin.get(sizeof(dev::rx_pkt_in) * n));
-    if (!pin) return DNRP_ENOMEM;
+    auto* sel = static_cast<uint32_t*>(ctx->st_sel.get(2 * sizeof(uint32_t) * n));
+    if (!pin || !sel) return DNRP_ENOMEM;
     for (uint32_t i = 0; i < n; ++i) {
         pin[i].fine_peak = sr[i].fine_peak_time;
         pin[i].cfo_rad = sr[i].cfo_fractional_rad + sr[i].cfo_integer_rad;
         pin[i].inc0 = phasor_arg(pin[i].cfo_rad);
     }
+    {
+        uint32_t o = 0;
+        for (const auto& g : gl)
+            for (uint32_t i : *g.second) {
+                sel[2 * o] = i;
+                sel[2 * o + 1] = i;  // PCC LLR row = slot
+                ++o;
+            }
+    }
     HIPCHK(hipMemcpyAsync(ctx->rx_in.p, pin, sizeof(dev::rx_pkt_in) * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ctx->st_rxin.ev, st));
-    auto fa = front_args(ctx, t);
-    ctx->tic("rx_stf", st);
-    if (dev::launch_rx_stf(fa, n, st) != hipSuccess) return DNRP_EDEVICE;
-    ctx->toc("rx_stf", st);
-    fa.sym_first = 1;
-    fa.sym_count = t->pcc_max;
-    ctx->tic("rx_fft_pcc", st);
-    if (dev::launch_rx_fft(fa, n, st) != hipSuccess) return DNRP_EDEVICE;
-    ctx->toc("rx_fft_pcc", st);
-    if ((err = launch_back(ctx, t, t->bplan, n, false, 2, t->pcc_k.as<uint32_t>(), nullptr, pcc_llr, 196, st)) != DNRP_OK)
-        return err;
-    ctx->rx1_last = t;
+    HIPCHK(hipMemcpyAsync(ctx->rx_sel.p, sel, 2 * sizeof(uint32_t) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(ctx->st_sel.ev, st));
+    uint32_t off = 0;
+    for (const auto& g : gl) {
+        rx1_tables* t = g.first;
+        const uint32_t ng = static_cast<uint32_t>(g.second->size());
+        const uint32_t* gsel = ctx->rx_sel.as<uint32_t>() + 2 * off;
+        off += ng;
+        auto fa = front_args(ctx, t, iq_in, gsel);
+        ctx->tic("rx_stf", st);
+        if (dev::launch_rx_stf(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
+        ctx->toc("rx_stf", st);
+        fa.sym_first = 1;
+        fa.sym_count = t->pcc_max;
+        ctx->tic("rx_fft_pcc", st);
+        if (dev::launch_rx_fft(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
+        ctx->toc("rx_fft_pcc", st);
+        if ((err = launch_back(ctx, t, t->bplan, ng, gsel, false, 2, t->pcc_k.as<uint32_t>(), nullptr, pcc_llr, 196,
+                               st)) != DNRP_OK)
+            return err;
+    }
+    ctx->rx_valid = true;
     if (rep) {
         std::vector<dev::rx_pkt_state> S(n);
         HIPCHK(hipMemcpyAsync(S.data(), ctx->rx_st.p, sizeof(dev::rx_pkt_state) * n, hipMemcpyDeviceToHost, st));
@@ -748,75 +794,116 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
     return DNRP_OK;
 }
 
-int dnrp_rx_pdc_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp_pdc_req* req, int16_t* pdc_llr,
-                      uint32_t llr_stride, dnrp_pdc_report* rep, void* stream) {
-    if (!ctx || !psdef || (n > 0 && (!req || !pdc_llr))) return DNRP_EINVAL;
-    if (n == 0) return DNRP_OK;
-    if (!ctx->rx1_last || n != ctx->rx_n) return DNRP_ESTATE;
+int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const float* iq_in, uint32_t S_in,
+                      int16_t* pdc_llr, uint32_t llr_stride, dnrp_pdc_report* rep, void* stream) {
+    if (!ctx || (m > 0 && (!req || !iq_in || !pdc_llr))) return DNRP_EINVAL;
+    if (!ctx->rx_valid) return DNRP_ESTATE;
+    if (m == 0) return DNRP_OK;
+    if (m > ctx->rx_n || S_in != ctx->rx_S_in) return DNRP_EINVAL;
     (void)hipSetDevice(ctx->cfg.device);
     int err = DNRP_OK;
-    rx2_tables* t2 = get_rx2(ctx, *psdef, &err);
-    if (!t2) return err;
-    rx1_tables* t = ctx->rx1_last;
-    if (psdef->u != t->u || psdef->b != t->b || t2->q.N_eff_TX != t->N_eff_TX) return DNRP_EINVAL;
-    if (t2->q.N_DF_symb > ctx->rx_nsym_cap || llr_stride < t2->q.G) return DNRP_EINVAL;
+    // requests grouped by (PCC-phase tables, PLCF-announced psdef) (rx_synced.cpp:325-436 per packet)
+    using key_t = std::tuple<rx1_tables*, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>;
+    std::map<key_t, std::vector<uint32_t>> groups;
+    std::vector<uint8_t> seen(ctx->rx_n, 0);
+    for (uint32_t r = 0; r < m; ++r) {
+        const auto& q = req[r];
+        if (q.pcc_index >= ctx->rx_n || seen[q.pcc_index]) return DNRP_EINVAL;
+        seen[q.pcc_index] = 1;
+        if (q.plcf_type != 1 && q.plcf_type != 2) return DNRP_EINVAL;
+        const auto& d = q.psdef;
+        groups[key_t(ctx->rx_slot_t[q.pcc_index], d.u, d.b, d.PacketLengthType, d.PacketLength, d.tm_mode_index,
+                     d.mcs_index, d.Z)]
+            .push_back(r);
+    }
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (!ctx->pdc_seq_ptrs.ensure(sizeof(void*) * ctx->cfg.max_batch)) return DNRP_ENOMEM;
-    auto** seqp = static_cast<const uint8_t**>(ctx->st_seq.get(sizeof(void*) * n));
-    if (!seqp) return DNRP_ENOMEM;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (req[i].plcf_type != 1 && req[i].plcf_type != 2) return DNRP_EINVAL;
-        auto it = ctx->netid.find(req[i].network_id);
-        if (it == ctx->netid.end()) return DNRP_ENETID;
-        if ((err = ensure_seq(ctx, *it->second, req[i].network_id, t2->q.G)) != DNRP_OK) return err;
-        seqp[i] = (req[i].plcf_type == 1 ? it->second->t1 : it->second->t2).as<uint8_t>();
+    if (!ctx->pdc_seq_ptrs.ensure(sizeof(void*) * ctx->cfg.max_batch) ||
+        !ctx->rx_sel2.ensure(2 * sizeof(uint32_t) * ctx->cfg.max_batch))
+        return DNRP_ENOMEM;
+    auto** seqp = static_cast<const uint8_t**>(ctx->st_seq.get(sizeof(void*) * m));
+    auto* sel = static_cast<uint32_t*>(ctx->st_sel2.get(2 * sizeof(uint32_t) * m));
+    if (!seqp || !sel) return DNRP_ENOMEM;
+    std::vector<std::pair<rx2_tables*, const std::vector<uint32_t>*>> gl;
+    uint32_t o = 0;
+    for (const auto& g : groups) {
+        rx1_tables* t = std::get<0>(g.first);
+        const dnrp_psdef& d = req[g.second.front()].psdef;
+        rx2_tables* t2 = get_rx2(ctx, d, &err);
+        if (!t2) return err;
+        if (d.u != t->u || d.b != t->b || t2->q.N_eff_TX != t->N_eff_TX) return DNRP_EINVAL;
+        if (llr_stride < t2->q.G) return DNRP_EINVAL;
+        for (uint32_t r : g.second) {
+            if (t2->q.N_DF_symb > ctx->rx_slot_cap[req[r].pcc_index]) return DNRP_EINVAL;
+            auto it = ctx->netid.find(req[r].network_id);
+            if (it == ctx->netid.end()) return DNRP_ENETID;
+            if ((err = ensure_seq(ctx, *it->second, req[r].network_id, t2->q.G)) != DNRP_OK) return err;
+            seqp[r] = (req[r].plcf_type == 1 ? it->second->t1 : it->second->t2).as<uint8_t>();
+            sel[2 * o] = req[r].pcc_index;
+            sel[2 * o + 1] = r;
+            ++o;
+        }
+        gl.emplace_back(t2, &g.second);
     }
-    HIPCHK(hipMemcpyAsync(ctx->pdc_seq_ptrs.p, seqp, sizeof(void*) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(ctx->pdc_seq_ptrs.p, seqp, sizeof(void*) * m, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ctx->st_seq.ev, st));
-    auto fa = front_args(ctx, t);
-    fa.sym_first = t->pcc_max + 1;
-    if (t2->q.N_DF_symb > t->pcc_max) {
-        fa.sym_count = t2->q.N_DF_symb - t->pcc_max;
-        ctx->tic("rx_fft_pdc", st);
-        if (dev::launch_rx_fft(fa, n, st) != hipSuccess) return DNRP_EDEVICE;
-        ctx->toc("rx_fft_pdc", st);
+    HIPCHK(hipMemcpyAsync(ctx->rx_sel2.p, sel, 2 * sizeof(uint32_t) * m, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(ctx->st_sel2.ev, st));
+    if (rep && !ctx->mimo_out.ensure(size_t(ctx->cfg.max_batch) * 3 * sizeof(uint32_t))) return DNRP_ENOMEM;
+    uint32_t off = 0;
+    size_t gi = 0;
+    for (const auto& g : groups) {
+        rx1_tables* t = std::get<0>(g.first);
+        rx2_tables* t2 = gl[gi++].first;
+        const uint32_t ng = static_cast<uint32_t>(g.second.size());
+        const uint32_t* gsel = ctx->rx_sel2.as<uint32_t>() + 2 * off;
+        off += ng;
+        auto fa = front_args(ctx, t, iq_in, gsel);
+        fa.sym_first = t->pcc_max + 1;
+        if (t2->q.N_DF_symb > t->pcc_max) {
+            fa.sym_count = t2->q.N_DF_symb - t->pcc_max;
+            ctx->tic("rx_fft_pdc", st);
+            if (dev::launch_rx_fft(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
+            ctx->toc("rx_fft_pdc", st);
+        }
+        if ((err = launch_back(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps, t2->pdc_k.as<uint32_t>(),
+                               t2->pdc_sym.as<uint16_t>(), pdc_llr, llr_stride, st)) != DNRP_OK)
+            return err;
+        if (rep) {
+            // MIMO report at the packet end (rx_synced.cpp:417-436; the reference runs it after a
+            // successful CRC, which is the caller's decision here)
+            dev::rx_mimo_args ma{};
+            ma.N_RX = ctx->cfg.N_TX_max;
+            ma.N_TS = t2->N_TS;
+            ma.Nf_pad = ctx->rx_Nf_pad;
+            ma.n_sym_total = ctx->rx_nsym_cap + 1;
+            ma.ncb_tx = t2->ncb_tx;
+            ma.A_tx = t2->A_tx;
+            ma.ncb_rx = t2->ncb_rx;
+            ma.A_rx = t2->A_rx;
+            ma.cells = t2->mimo_cells.as<uint32_t>();
+            ma.signs = t2->mimo_signs.as<float>();
+            ma.Wtx = t2->Wtx.as<float2>();
+            ma.stx = t2->stx.as<float>();
+            ma.Wrx = t2->Wrx.as<float2>();
+            ma.srx = t2->srx.as<float>();
+            ma.Y = ctx->Y.as<float2>();
+            ma.out = ctx->mimo_out.as<uint32_t>();
+            ma.sel = gsel;
+            if (dev::launch_rx_mimo(ma, ng, st) != hipSuccess) return DNRP_EDEVICE;
+        }
     }
-    if ((err = launch_back(ctx, t, t2->bplan, n, true, t2->q.N_bps, t2->pdc_k.as<uint32_t>(), t2->pdc_sym.as<uint16_t>(),
-                           pdc_llr, llr_stride, st)) != DNRP_OK)
-        return err;
     if (rep) {
-        // MIMO report at the packet end (rx_synced.cpp:417-436; the reference runs it after a
-        // successful CRC, which is the caller's decision here)
-        if (!ctx->mimo_out.ensure(size_t(ctx->cfg.max_batch) * 3 * sizeof(uint32_t))) return DNRP_ENOMEM;
-        dev::rx_mimo_args ma{};
-        ma.N_RX = ctx->cfg.N_TX_max;
-        ma.N_TS = t2->N_TS;
-        ma.Nf_pad = ctx->rx_Nf_pad;
-        ma.n_sym_total = ctx->rx_nsym_cap + 1;
-        ma.ncb_tx = t2->ncb_tx;
-        ma.A_tx = t2->A_tx;
-        ma.ncb_rx = t2->ncb_rx;
-        ma.A_rx = t2->A_rx;
-        ma.cells = t2->mimo_cells.as<uint32_t>();
-        ma.signs = t2->mimo_signs.as<float>();
-        ma.Wtx = t2->Wtx.as<float2>();
-        ma.stx = t2->stx.as<float>();
-        ma.Wrx = t2->Wrx.as<float2>();
-        ma.srx = t2->srx.as<float>();
-        ma.Y = ctx->Y.as<float2>();
-        ma.out = ctx->mimo_out.as<uint32_t>();
-        if (dev::launch_rx_mimo(ma, n, st) != hipSuccess) return DNRP_EDEVICE;
-        std::vector<dev::rx_pkt_state> S(n);
-        std::vector<uint32_t> mo(3 * size_t(n));
-        HIPCHK(hipMemcpyAsync(S.data(), ctx->rx_st.p, sizeof(dev::rx_pkt_state) * n, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(mo.data(), ma.out, mo.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        std::vector<dev::rx_pkt_state> S(ctx->rx_n);
+        std::vector<uint32_t> mo(3 * size_t(m));
+        HIPCHK(hipMemcpyAsync(S.data(), ctx->rx_st.p, sizeof(dev::rx_pkt_state) * ctx->rx_n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(mo.data(), ctx->mimo_out.p, mo.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        for (uint32_t i = 0; i < n; ++i) {
-            rep[i].snr_dB = S[i].snr_pdc;
-            rep[i].mimo_N_RX = ma.N_RX;
-            rep[i].mimo_N_TS_other = mo[3 * i];
-            rep[i].tm_3_7_beamforming_idx = mo[3 * i + 1];
-            rep[i].tm_3_7_beamforming_reciprocal_idx = mo[3 * i + 2];
+        for (uint32_t r = 0; r < m; ++r) {
+            rep[r].snr_dB = S[req[r].pcc_index].snr_pdc;
+            rep[r].mimo_N_RX = ctx->cfg.N_TX_max;
+            rep[r].mimo_N_TS_other = mo[3 * r];
+            rep[r].tm_3_7_beamforming_idx = mo[3 * r + 1];
+            rep[r].tm_3_7_beamforming_reciprocal_idx = mo[3 * r + 2];
         }
     }
     return DNRP_OK;

@@ -167,11 +167,14 @@ struct dnrp_ctx {
     // batch scratch
     dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d, mimo_out;
     pinned st_tx, st_rxin, st_seq, st_rep;
-    // retained RX phase-1 state
-    rx1_tables* rx1_last = nullptr;
+    // retained RX phase-1 state: per PCC-batch slot its (u, b, N_eff_TX) tables and symbol
+    // capacity; Y is laid out with the batch-wide maxima rx_nsym_cap / rx_Nf_pad
+    bool rx_valid = false;
     uint32_t rx_n = 0, rx_S_in = 0, rx_nsym_cap = 0, rx_Nf_pad = 0;
-    const float* rx_iq = nullptr;
-    std::vector<dnrp::dev::rx_pkt_in> rx_pin_host;
+    std::vector<rx1_tables*> rx_slot_t;
+    std::vector<uint32_t> rx_slot_cap;
+    dbuf rx_sel, rx_sel2;  // [max_batch][2] launch packet -> slot / output row (PCC / PDC call), one slice per group
+    pinned st_sel, st_sel2;
     // synchronisation: per (u, b) tables, step sums and reports
     std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<dnrp::host::sync_tables>> synct;
     dbuf sy_P, sy_C, sy_res, sy_cnt;

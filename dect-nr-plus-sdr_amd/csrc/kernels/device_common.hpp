@@ -57,6 +57,17 @@ __device__ __forceinline__ void stage_span(float2* dst, const float2* __restrict
     });
 }
 
+// same with a lower bound: x[q] valid for q in [lo, S) (RX windows whose packet starts before the
+// window, fine_peak < 0: zero history there, never a read before the window row)
+template <int U>
+__device__ __forceinline__ void stage_span_lo(float2* dst, const float2* __restrict__ x, int64_t q0, uint32_t n,
+                                              int64_t lo, int64_t S, uint32_t tid, uint32_t nt) {
+    stage_gen<U>(dst, n, tid, nt, [&](uint32_t i) {
+        const int64_t q = q0 + i;
+        return (q >= lo && q < S) ? x[q] : make_float2(0.f, 0.f);
+    });
+}
+
 template <int U, class T>
 __device__ __forceinline__ void stage_copy(T* dst, const T* __restrict__ src, uint32_t n, uint32_t tid, uint32_t nt) {
     stage_gen<U>(dst, n, tid, nt, [&](uint32_t i) { return src[i]; });

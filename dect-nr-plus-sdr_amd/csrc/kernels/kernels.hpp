@@ -99,10 +99,18 @@ struct rx_front_args {
     rx_pkt_state* st;
     float2* Y;                 // [n][N_RX][n_sym_total][Nf_pad]
     uint32_t stream;           // rx_fft_stream_kernel allowed (host: compiled-in taps match)
+    const uint32_t* sel;       // [launch packets][2]: PCC-batch slot, output row (rx_slot_of / rx_row_of)
 };
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);
 bool rx_stream_taps_match(const float* h, size_t n);  // compiled-in 9/10 taps == run-time taps
 hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st);
+
+// Packet selection of one RX launch: launch-local packet i works on PCC-batch slot sel[2i] (its
+// window, state and Y rows) and writes output row sel[2i+1] (LLRs, reports). The host groups the
+// packets of a batch call by configuration and launches each group with its own sel slice.
+__device__ __forceinline__ uint32_t rx_slot_of(const uint32_t* sel, uint32_t i) { return sel[2 * i]; }
+__device__ __forceinline__ uint32_t rx_row_of(const uint32_t* sel, uint32_t i) { return sel[2 * i + 1]; }
+constexpr uint32_t RX_MAX_DOPS = 64;  // DRS ops per phase; lut_d holds RX_MAX_DOPS bytes per slot
 
 // back end, see geometry.hpp rx_plan_t (identical layouts)
 struct rx_seg {
@@ -122,7 +130,8 @@ struct rx_snr_args {        // DRS zero-forcing SNR chain + LUT profile picks, o
     float prof_snr[3];
     const float2* Y;
     rx_pkt_state* st;
-    uint8_t* lut_d;         // [n][n_dops]: profile picked after each DRS op
+    uint8_t* lut_d;         // [slot][RX_MAX_DOPS]: profile picked after each DRS op
+    const uint32_t* sel;    // launch packet -> slot / output row
 };
 hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st);
 
@@ -147,9 +156,10 @@ struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epo
     const float2* Y;
     const uint8_t* lut_d;
     const uint8_t* pcc_seq;
-    const uint8_t* const* pdc_seq;  // per packet (PDC phase)
-    int16_t* llr;                   // PCC: [n][196], PDC: [n][llr_stride]
+    const uint8_t* const* pdc_seq;  // per output row (PDC phase)
+    int16_t* llr;                   // PCC: [n][196], PDC: [m][llr_stride] (output rows)
     uint32_t llr_stride;
+    const uint32_t* sel;            // launch packet -> slot / output row
 };
 hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st);
 
@@ -163,7 +173,8 @@ struct rx_mimo_args {  // estimator_mimo_t::process_drs at the packet end, one w
     const float2* Wrx;      // [ncb_rx][N_RX]
     const float* srx;
     const float2* Y;
-    uint32_t* out;          // [n][3]: N_TS_other, tm_3_7_beamforming_idx, tm_3_7_beamforming_reciprocal_idx
+    uint32_t* out;          // [row][3]: N_TS_other, tm_3_7_beamforming_idx, tm_3_7_beamforming_reciprocal_idx
+    const uint32_t* sel;    // launch packet -> slot / output row
 };
 hipError_t launch_rx_mimo(const rx_mimo_args& a, uint32_t n, hipStream_t st);
 

@@ -31,15 +31,8 @@ __device__ void resample_block(const rx_front_args& A, const float2* __restrict_
     const uint32_t n_in = static_cast<uint32_t>(p1 - q0 + 1);
     // input index q relative to the fine peak, zero history before it: valid for q in
     // [max(0, -fine_peak), S_in - fine_peak)
-    if (fine_peak >= 0) {
-        stage_span<8>(inbuf, x + fine_peak, q0, n_in, static_cast<int64_t>(A.S_in) - fine_peak, threadIdx.x, blockDim.x);
-    } else {
-        for (uint32_t i = threadIdx.x; i < n_in; i += blockDim.x) {
-            const int64_t q = q0 + i;
-            const int64_t g = fine_peak + q;
-            inbuf[i] = (q >= 0 && g >= 0 && g < static_cast<int64_t>(A.S_in)) ? x[g] : make_float2(0.f, 0.f);
-        }
-    }
+    stage_span_lo<8>(inbuf, x + fine_peak, q0, n_in, fine_peak < 0 ? -fine_peak : 0,
+                     static_cast<int64_t>(A.S_in) - fine_peak, threadIdx.x, blockDim.x);
     __syncthreads();
     const uint32_t dT = blockDim.x * A.M, dp = dT / A.L, dph = dT % A.L;
     if (threadIdx.x < cnt) {
@@ -82,7 +75,7 @@ template <int HL>
 __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     __shared__ double red[16];
-    const uint32_t pkt = blockIdx.x;
+    const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x);
     const uint32_t Nd = A.plan.N, N = A.N_occ, Nf = N + 1;
     const uint32_t n_stf = A.STF_CP + Nd;
     const uint32_t n_in_max = (n_stf * A.M) / A.L + A.hl + 4;
@@ -203,7 +196,7 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
     const uint32_t nblk = (A.sym_count + A.sym_per_block - 1) / A.sym_per_block;
     const uint32_t blk = blockIdx.x % nblk;
     const uint32_t a = (blockIdx.x / nblk) % A.N_RX;
-    const uint32_t pkt = blockIdx.x / (nblk * A.N_RX);
+    const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / (nblk * A.N_RX));
     using PB = pp_block<(LR > 0 ? LR : 1), (LR > 0 ? MR : 1), (LR > 0 ? HLR : 0)>;
     float2* fa = smem;                         // [RX_SYM_PASS][Nd]
     float2* fb = fa + RX_SYM_PASS * Nd;        // [RX_SYM_PASS][Nd]
@@ -228,7 +221,7 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
     const uint32_t l0 = A.sym_first + blk * A.sym_per_block;
     const uint32_t l1 = min(A.sym_first + A.sym_count, l0 + A.sym_per_block);
     // valid input window relative to the fine peak: history is zero before it (rx_synced.cpp:711-740)
-    const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak;
+    const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
     auto m_first = [&](uint32_t l) { return static_cast<int>(n_stf + (l - 1) * (A.CP + Nd) + A.CP); };
     for (uint32_t lp = l0; lp < l1; lp += RX_SYM_PASS) {
         const uint32_t ns = min(RX_SYM_PASS, l1 - lp);
@@ -239,7 +232,7 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
             const int64_t in0 = static_cast<int64_t>(A.p_star) + int64_t(MR) * qb0 - HLR;
             const uint32_t n_in = static_cast<uint32_t>(MR * (qb1 - 1 - qb0) + PB::W);
             const float2* src = x + in.fine_peak + in0;
-            stage_span<8>(inbuf, src - in0, in0, n_in, q_hi, threadIdx.x, RX_THREADS);
+            stage_span_lo<8>(inbuf, src - in0, in0, n_in, q_lo, q_hi, threadIdx.x, RX_THREADS);
             __syncthreads();
             for (int q = qb0 + static_cast<int>(threadIdx.x); q < qb1; q += RX_THREADS) {
                 const int mb = static_cast<int>(A.m_star) + LR * q;
@@ -317,7 +310,7 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     const uint32_t nblk = (A.sym_count + RXW_SYMS - 1) / RXW_SYMS;
     const uint32_t blk = blockIdx.x % nblk;
     const uint32_t a = (blockIdx.x / nblk) % A.N_RX;
-    const uint32_t pkt = blockIdx.x / (nblk * A.N_RX);
+    const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / (nblk * A.N_RX));
     const uint32_t region = rxw_region(LR, MR, PB::W);
     float2* twl = smem;                                  // Nd
     float* taps = reinterpret_cast<float*>(twl + Nd);    // npp
@@ -337,9 +330,9 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     const uint32_t n_in = static_cast<uint32_t>(MR * (qb1 - 1 - qb0) + PB::W);
     float2* R = reg0 + w * region;
     // valid input window relative to the fine peak: history is zero before it (rx_synced.cpp:711-740)
-    const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak;
+    const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
     const float2* src = A.iq + (size_t(pkt) * A.N_RX + a) * A.S_in + in.fine_peak + in0;
-    if (active) stage_span<20>(R, src - in0, in0, n_in, q_hi, lane, 64);
+    if (active) stage_span_lo<20>(R, src - in0, in0, n_in, q_lo, q_hi, lane, 64);
     __syncthreads();  // twiddles / taps (and this wave's own staging)
     if (!active) return;
     // resampling + phase-continuous mixer, outputs in registers
@@ -435,8 +428,9 @@ rx_fft_stream_kernel(rx_front_args A, uint32_t n, uint32_t n_seg) {
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     float2* R = smem + wv * RXS_SPAN;
     const uint32_t gw = blockIdx.x * RXS_WPG + wv;
-    const uint32_t seg = gw % n_seg, a = (gw / n_seg) % A.N_RX, pkt = gw / (n_seg * A.N_RX);
-    if (pkt >= n) return;
+    const uint32_t seg = gw % n_seg, a = (gw / n_seg) % A.N_RX, pl = gw / (n_seg * A.N_RX);
+    if (pl >= n) return;
+    const uint32_t pkt = rx_slot_of(A.sel, pl);
     const uint32_t s_a = seg * RXS_SEG, s_b = min(s_a + RXS_SEG, A.sym_count);
     if (s_a >= s_b) return;
     const rx_pkt_in in = A.pin[pkt];

@@ -104,11 +104,11 @@ __device__ __forceinline__ void emit_cell(float2 x, uint32_t j, uint32_t N_bps, 
 }
 
 // ===================================================================== SNR chain
-constexpr uint32_t SNR_THREADS = 256, MAX_DOPS = 64;
+constexpr uint32_t SNR_THREADS = 256, MAX_DOPS = RX_MAX_DOPS;
 
 __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
     __shared__ double s1s[MAX_DOPS], s2s[MAX_DOPS];
-    const uint32_t pkt = blockIdx.x, nd = A.n_drs;
+    const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x), nd = A.n_drs;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u, nw = SNR_THREADS / 64;
     const float2* Yp = A.Y + size_t(pkt) * A.N_RX * A.n_sym_total * A.Nf_pad;
     for (uint32_t d = wave; d < A.n_dops; d += nw) {
@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
                 pick = i;
             }
         }
-        A.lut_d[size_t(pkt) * A.n_dops + d] = static_cast<uint8_t>(pick);
+        A.lut_d[size_t(pkt) * MAX_DOPS + d] = static_cast<uint8_t>(pick);
     }
     if (A.is_pdc)
         st->snr_pdc = snr_db();
@@ -185,7 +185,8 @@ constexpr uint32_t CELL_WCHUNK = CELL_WCHUNK_DEF;  // interpolation taps per wei
 template <int NRX, int NT>
 __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 zfi[];  // [NRX][NT][2 nd]
-    const uint32_t pkt = blockIdx.x / A.n_epochs, ep = blockIdx.x % A.n_epochs;
+    const uint32_t pl = blockIdx.x / A.n_epochs, ep = blockIdx.x % A.n_epochs;
+    const uint32_t pkt = rx_slot_of(A.sel, pl), row = rx_row_of(A.sel, pl);
     const rx_epoch E = A.epochs[ep];
     const uint32_t nd = A.n_drs, Nf = A.N_occ + 1, nd2 = 2 * nd;
     const float2* Yp = A.Y + size_t(pkt) * NRX * A.n_sym_total * A.Nf_pad;
@@ -203,9 +204,9 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
         zfi[(a * NT + t) * nd2 + 2 * i + o] = v;
     }
     __syncthreads();
-    const uint8_t* __restrict__ seq = A.is_pdc ? A.pdc_seq[pkt] : A.pcc_seq;
-    int16_t* __restrict__ llr = A.llr + size_t(pkt) * A.llr_stride;
-    const uint8_t* lutp = A.lut_d + size_t(pkt) * A.n_dops;
+    const uint8_t* __restrict__ seq = A.is_pdc ? A.pdc_seq[row] : A.pcc_seq;
+    int16_t* __restrict__ llr = A.llr + size_t(row) * A.llr_stride;
+    const uint8_t* lutp = A.lut_d + size_t(pkt) * RX_MAX_DOPS;
     if (E.units == 0) return;
     uint32_t si = E.seg0;
     rx_seg S = A.segs[si];
@@ -392,7 +393,7 @@ __device__ uint32_t mimo_pick(const float2* H, uint32_t N_TX_virt, uint32_t N_RX
 
 __global__ void __launch_bounds__(64) rx_mimo_kernel(rx_mimo_args A) {
     __shared__ float2 H[8 * 8 * 4];
-    const uint32_t pkt = blockIdx.x, lane = threadIdx.x;
+    const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x), row = rx_row_of(A.sel, blockIdx.x), lane = threadIdx.x;
     const float2* Yp = A.Y + size_t(pkt) * A.N_RX * A.n_sym_total * A.Nf_pad;
     for (uint32_t e = lane; e < A.N_RX * A.N_TS * 4; e += 64) {
         const uint32_t rx = e / (A.N_TS * 4), tc = e % (A.N_TS * 4);
@@ -403,9 +404,9 @@ __global__ void __launch_bounds__(64) rx_mimo_kernel(rx_mimo_args A) {
     const uint32_t idx = A.N_TS == 1 ? 0u : mimo_pick(H, A.N_TS, A.N_RX, false, A.N_TS, A.Wtx, A.stx, A.A_tx, A.ncb_tx, lane);
     const uint32_t idr = A.N_RX == 1 ? 0u : mimo_pick(H, A.N_RX, A.N_TS, true, A.N_TS, A.Wrx, A.srx, A.A_rx, A.ncb_rx, lane);
     if (lane == 0) {
-        A.out[3 * pkt] = A.N_TS;
-        A.out[3 * pkt + 1] = idx;
-        A.out[3 * pkt + 2] = idr;
+        A.out[3 * row] = A.N_TS;
+        A.out[3 * row + 1] = idx;
+        A.out[3 * row + 2] = idr;
     }
 }
 

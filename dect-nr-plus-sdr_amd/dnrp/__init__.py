@@ -115,7 +115,8 @@ class PdcReport(C.Structure):
 
 
 class PdcReq(C.Structure):
-    _fields_ = [("network_id", C.c_uint32), ("plcf_type", C.c_uint32)]
+    """dnrp_pdc_req: PLCF-announced psdef, slot in the preceding PCC batch, network ID, PLCF type."""
+    _fields_ = [("psdef", PsDef), ("pcc_index", C.c_uint32), ("network_id", C.c_uint32), ("plcf_type", C.c_uint32)]
 
 
 EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_get_packet_sizes",
@@ -143,7 +144,7 @@ def lib():
                                          P, P, P]
         L.dnrp_rx_pcc_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P,
                                         C.POINTER(PccReport), P]
-        L.dnrp_rx_pdc_batch.argtypes = [P, C.POINTER(PsDef), C.c_uint32, C.POINTER(PdcReq), P, C.c_uint32,
+        L.dnrp_rx_pdc_batch.argtypes = [P, C.c_uint32, C.POINTER(PdcReq), P, C.c_uint32, P, C.c_uint32,
                                         C.POINTER(PdcReport), P]
         L.dnrp_sync.argtypes = [P, P]
         L.dnrp_last_kernel_ms.argtypes = [P, C.c_char_p, C.POINTER(C.c_float)]
@@ -175,6 +176,21 @@ def compute_packet_sizes(ps, u_max=None, b_max=None, os_min=1, L=10, M=9):
     if rc != 0:
         raise DnrpError(rc, "dnrp_compute_packet_sizes")
     return out.as_dict()
+
+
+def _check_tensor(t, what, dtype, ndim, device):
+    """Shapes, dtype, layout and device of a buffer handed to libdnrp.so (the C side trusts them)."""
+    import torch
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{what}: expected a torch tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{what}: dtype {t.dtype}, expected {dtype}")
+    if t.dim() != ndim:
+        raise ValueError(f"{what}: {t.dim()} dimensions, expected {ndim}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: must be contiguous")
+    if t.device.type != "cuda" or (t.device.index or 0) != device:
+        raise ValueError(f"{what}: must live on cuda:{device}, is on {t.device}")
 
 
 def _stream_ptr(stream):
@@ -213,7 +229,19 @@ class Phy:
 
     def tx_batch(self, ps, descs, pcc_d, pdc_d, iq_out, stream=None):
         """pcc_d uint8 [n,25], pdc_d uint8 [n,stride], iq_out float32 [n,N_TX,S,2] (torch, device)."""
+        import torch
         n = len(descs)
+        dev = int(self.cfg.device)
+        _check_tensor(pcc_d, "pcc_d", torch.uint8, 2, dev)
+        _check_tensor(pdc_d, "pdc_d", torch.uint8, 2, dev)
+        _check_tensor(iq_out, "iq_out", torch.float32, 4, dev)
+        sz = self.packet_sizes(ps)
+        if pcc_d.shape[0] < n or pcc_d.shape[1] != 25:
+            raise ValueError(f"pcc_d shape {tuple(pcc_d.shape)}, expected [>={n}, 25]")
+        if pdc_d.shape[0] < n or pdc_d.shape[1] < (sz["G"] + 7) // 8:
+            raise ValueError(f"pdc_d shape {tuple(pdc_d.shape)}, expected [>={n}, >={(sz['G'] + 7) // 8}]")
+        if iq_out.shape[0] < n or iq_out.shape[1] != sz["N_TX"] or iq_out.shape[3] != 2:
+            raise ValueError(f"iq_out shape {tuple(iq_out.shape)}, expected [>={n}, {sz['N_TX']}, S, 2]")
         arr = descs if isinstance(descs, C.Array) else (TxDesc * n)(*descs)
         _chk(lib().dnrp_tx_batch(self._ctx, C.byref(ps), n, arr, C.c_void_p(pcc_d.data_ptr()),
                                  C.c_void_p(pdc_d.data_ptr()), pdc_d.shape[1], C.c_void_p(iq_out.data_ptr()),
@@ -223,19 +251,40 @@ class Phy:
         """sync_chunk_t::search() on n windows of the device cf32 tensor iq (strides in samples).
         res: numpy SYNC_RESULT_DTYPE [n, max_reports] (pinned memory keeps the copy asynchronous);
         valid after sync(). Returns (res, n_found)."""
+        import torch
+        _check_tensor(iq, "iq", torch.float32, iq.dim(), int(self.cfg.device))
+        if iq.shape[-1] != 2:
+            raise ValueError("iq: last dimension must be 2 (interleaved cf32)")
+        if n > 0:
+            last = (n - 1) * win_stride + (sc.N_ant_limited - 1) * ant_stride + S_win
+            if last > iq.numel() // 2:
+                raise ValueError(f"iq holds {iq.numel() // 2} samples, the windows reach {last}")
         if res is None:
             res = np.zeros((n, sc.max_reports), SYNC_RESULT_DTYPE)
         if n_found is None:
             n_found = np.zeros(n, np.uint32)
         assert res.dtype == SYNC_RESULT_DTYPE and res.size >= n * sc.max_reports and res.flags.c_contiguous
+        assert n_found.dtype == np.uint32 and n_found.size >= n
         _chk(lib().dnrp_rx_sync_batch(self._ctx, C.byref(sc), n, C.c_void_p(iq.data_ptr()), win_stride, ant_stride,
                                       S_win, C.c_void_p(res.ctypes.data), C.c_void_p(n_found.ctypes.data),
                                       _stream_ptr(stream)), "dnrp_rx_sync_batch")
         return res, n_found
 
+    def _check_rx_windows(self, iq_in, n):
+        import torch
+        _check_tensor(iq_in, "iq_in", torch.float32, 4, int(self.cfg.device))
+        if iq_in.shape[0] < n or iq_in.shape[1] != self.cfg.N_TX_max or iq_in.shape[3] != 2:
+            raise ValueError(f"iq_in shape {tuple(iq_in.shape)}, expected [>={n}, {self.cfg.N_TX_max}, S_in, 2]")
+
     def rx_pcc_batch(self, reports, iq_in, pcc_llr, want_report=False, stream=None):
-        """reports: list of SyncReport or a numpy SYNC_REPORT_DTYPE array (see sync_reports())."""
+        """reports: list of SyncReport or a numpy SYNC_REPORT_DTYPE array (see sync_reports()).
+        iq_in float32 [n, N_RX, S_in, 2]; pcc_llr int16 [n, 196]."""
+        import torch
         n = len(reports)
+        self._check_rx_windows(iq_in, n)
+        _check_tensor(pcc_llr, "pcc_llr", torch.int16, 2, int(self.cfg.device))
+        if pcc_llr.shape[0] < n or pcc_llr.shape[1] != 196:
+            raise ValueError(f"pcc_llr shape {tuple(pcc_llr.shape)}, expected [>={n}, 196]")
         if isinstance(reports, np.ndarray):
             assert reports.dtype == SYNC_REPORT_DTYPE and reports.flags.c_contiguous
             arr = C.c_void_p(reports.ctypes.data)
@@ -244,14 +293,25 @@ class Phy:
         rep = (PccReport * n)() if want_report else None
         _chk(lib().dnrp_rx_pcc_batch(self._ctx, n, arr, C.c_void_p(iq_in.data_ptr()), iq_in.shape[2],
                                      C.c_void_p(pcc_llr.data_ptr()), rep, _stream_ptr(stream)), "dnrp_rx_pcc_batch")
+        self._pcc_n = n
         return rep
 
-    def rx_pdc_batch(self, ps, reqs, pdc_llr, want_report=False, stream=None):
-        n = len(reqs)
-        arr = reqs if isinstance(reqs, C.Array) else (PdcReq * n)(*reqs)
-        rep = (PdcReport * n)() if want_report else None
-        _chk(lib().dnrp_rx_pdc_batch(self._ctx, C.byref(ps), n, arr, C.c_void_p(pdc_llr.data_ptr()),
-                                     pdc_llr.shape[1], rep, _stream_ptr(stream)), "dnrp_rx_pdc_batch")
+    def rx_pdc_batch(self, reqs, iq_in, pdc_llr, want_report=False, stream=None):
+        """reqs: PdcReq per packet the MAC continues with (psdef, pcc_index, network_id, plcf_type);
+        iq_in: the windows of the preceding rx_pcc_batch; pdc_llr int16 [m, >= max G] (row r = reqs[r])."""
+        import torch
+        m = len(reqs)
+        self._check_rx_windows(iq_in, getattr(self, "_pcc_n", 0))
+        _check_tensor(pdc_llr, "pdc_llr", torch.int16, 2, int(self.cfg.device))
+        arr = reqs if isinstance(reqs, C.Array) else (PdcReq * m)(*reqs)
+        keys = {tuple(getattr(r.psdef, f) for f, _ in PsDef._fields_) for r in arr}
+        g_max = max((self.packet_sizes(PsDef(*k))["G"] for k in keys), default=0)
+        if pdc_llr.shape[0] < m or pdc_llr.shape[1] < g_max:
+            raise ValueError(f"pdc_llr shape {tuple(pdc_llr.shape)}, expected [>={m}, >={g_max}]")
+        rep = (PdcReport * m)() if want_report else None
+        _chk(lib().dnrp_rx_pdc_batch(self._ctx, m, arr, C.c_void_p(iq_in.data_ptr()), iq_in.shape[2],
+                                     C.c_void_p(pdc_llr.data_ptr()), pdc_llr.shape[1], rep, _stream_ptr(stream)),
+             "dnrp_rx_pdc_batch")
         return rep
 
     def sync(self, stream=None):

@@ -151,10 +151,17 @@ typedef struct {
     uint32_t tm_3_7_beamforming_reciprocal_idx;  /* codebook index for this side if reciprocal */
 } dnrp_pdc_report;
 
-/* per-packet PDC request = what maclow_phy_t / the HARQ process provide (interfaces/maclow_phy.hpp) */
+/* Per-packet PDC request = what maclow_phy_t carries once the MAC has decided from the decoded PLCF
+ * to continue with the PDC (phy/interfaces/maclow_phy.hpp: continue_with_pdc, hp_rx): the HARQ
+ * process' packet configuration (harq::process_rx_t::get_packet_sizes -> psdef), network ID and
+ * PLCF type (rx_synced.cpp:325-350), plus the packet's slot in the preceding dnrp_rx_pcc_batch
+ * (the rx_synced_t state the reference keeps between demoddecod_rx_pcc and demoddecod_rx_pdc).
+ * Packets the MAC rejected (continue_with_pdc = false) are simply not requested. */
 typedef struct {
+    dnrp_psdef psdef;     /* u, b and N_eff_TX (tm_mode_index) must match the PCC slot's sync report */
+    uint32_t pcc_index;   /* slot index i of sr[i] in the preceding dnrp_rx_pcc_batch, each at most once */
     uint32_t network_id;
-    uint32_t plcf_type;
+    uint32_t plcf_type;   /* 1 or 2: selects the PDC descrambling sequence (scrambling_pdc.cpp:41-48) */
 } dnrp_pdc_req;
 
 int dnrp_ctx_create(const dnrp_cfg* cfg, dnrp_ctx** out);
@@ -191,23 +198,34 @@ int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32_t n, const
                        uint64_t ant_stride, uint32_t S_win, dnrp_sync_result* res, uint32_t* n_found, void* stream);
 
 /*
- * RX phase 1: synchronised PCC demodulation of n packets (same u, b, N_eff_TX).
+ * RX phase 1: synchronised PCC demodulation of n packets. Each packet is processed with the
+ * (u, b, N_eff_TX) of its own sync report (packets are grouped internally, like independent
+ * demoddecod_rx_pcc calls).
+ *   sr       host [n]; fine_peak_time may be negative (zero history before the window start)
  *   iq_in    device [n][N_RX][S_in] cf32 slot windows, N_RX = cfg.N_TX_max
  *   pcc_llr  device [n][196] int16, descrambled
  *   rep      host [n] (optional)
- * Device state for phase 2 is kept in the context until the next dnrp_rx_pcc_batch.
+ * Device state for phase 2 (STF estimates, PCC-phase channel estimates) is kept in the context
+ * until the next dnrp_rx_pcc_batch.
  */
 int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, const float* iq_in,
                       uint32_t S_in, int16_t* pcc_llr, dnrp_pcc_report* rep, void* stream);
 
 /*
- * RX phase 2: PDC demodulation of the packets of the preceding dnrp_rx_pcc_batch (the MAC has
- * decided from the decoded PLCF; psdef is the packet configuration the PLCF announced).
- *   req      host [n] network ID / PLCF type per packet
- *   pdc_llr  device [n][llr_stride] int16, G descrambled LLRs per packet
- *   rep      host [n] (optional)
+ * RX phase 2: PDC demodulation of any subset of the packets of the preceding dnrp_rx_pcc_batch,
+ * each with its own PLCF-announced configuration (mixed MCS / PacketLength / network IDs are
+ * grouped internally).
+ *   req      host [m], m <= n of the PCC batch, distinct pcc_index values
+ *   iq_in    device windows holding the same samples as the PCC call's iq_in ([n][N_RX][S_in]
+ *            cf32, same S_in): the PDC symbols are read from here, so the windows must stay valid
+ *            and unchanged until this call's work has completed on the stream
+ *   pdc_llr  device [m][llr_stride] int16: row r = the G descrambled LLRs of req[r]
+ *   rep      host [m] (optional)
+ * Returns DNRP_ESTATE without a preceding PCC batch, DNRP_EINVAL for a pcc_index out of range or
+ * repeated, a psdef whose u/b/N_eff_TX differ from the slot's sync report, S_in different from
+ * the PCC call, or llr_stride < G.
  */
-int dnrp_rx_pdc_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp_pdc_req* req,
+int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const float* iq_in, uint32_t S_in,
                       int16_t* pdc_llr, uint32_t llr_stride, dnrp_pdc_report* rep, void* stream);
 
 int dnrp_sync(dnrp_ctx* ctx, void* stream);

@@ -13,6 +13,34 @@ CONFIGS = {
     "C4": ((8, 16, 1, 1, 5, 8), (8, 16, 4, 1, 10, 9)),
 }
 
+# GPU parity configurations (tests/test_gpu_parity.py; the oracle loopback runs all of them on the
+# CPU in tests/test_oracle_loopback.py). The bench configurations C2/C3/C4 plus every mode the
+# reference RX supports that the bench does not exercise.
+# name: psdef (u, b, PLT, PL, tm, mcs), ctx (u_max, b_max, N_TX_max, os_min, L, M), chestim lr,
+#       per-packet SNRs (dB), TX codebook
+PARITY_CASES = {
+    "C2": ((1, 1, 1, 1, 0, 1), (1, 1, 1, 1, 10, 9), 1, (10.0, 10.0, 10.0), 0),
+    "C3": ((8, 16, 1, 1, 0, 8), (8, 16, 1, 1, 10, 9), 1, (30.0, 30.0, 30.0), 0),
+    "C4": ((8, 16, 1, 1, 5, 8), (8, 16, 4, 1, 10, 9), 1, (30.0, 30.0, 30.0), 0),
+    **{f"C1_mcs{m}": ((1, 1, 1, 1, 0, m), (1, 1, 1, 1, 10, 9), 1, (-2.0, 5.0, 20.0), 0) for m in (0, 2, 3, 4, 5, 6, 7)},
+    "mrc2_64qam": ((1, 2, 1, 2, 0, 6), (1, 2, 2, 1, 10, 9), 1, (12.0, 25.0), 0),
+    "mrc4_16qam": ((2, 4, 1, 1, 0, 4), (2, 4, 4, 1, 10, 9), 1, (8.0, 20.0), 0),
+    "tm1_txdiv2": ((4, 8, 1, 1, 1, 5), (4, 8, 2, 1, 10, 9), 1, (15.0, 28.0), 0),
+    "tm5_u2b4": ((2, 4, 1, 2, 5, 6), (2, 4, 4, 1, 10, 9), 1, (18.0, 30.0), 0),
+    "tm3_codebook3": ((2, 2, 1, 2, 3, 6), (2, 2, 2, 1, 10, 9), 1, (20.0, 30.0), 3),
+    "tm7_codebook9": ((1, 4, 1, 1, 7, 3), (1, 4, 4, 1, 10, 9), 1, (10.0, 20.0), 9),
+    "lmode_siso": ((1, 1, 1, 2, 0, 3), (1, 1, 1, 1, 10, 9), 0, (6.0, 15.0), 0),
+    "lmode_C4": ((8, 16, 1, 1, 5, 8), (8, 16, 4, 1, 10, 9), 0, (30.0, 30.0), 0),
+    "lmode_txdiv2": ((2, 2, 1, 3, 1, 4), (2, 2, 2, 1, 10, 9), 0, (12.0, 25.0), 0),
+    "lm40_27_b12": ((1, 12, 1, 1, 0, 4), (1, 12, 1, 1, 40, 27), 1, (15.0, 25.0), 0),
+    "lm40_27_u8b12_tm5": ((8, 12, 1, 1, 5, 6), (8, 12, 4, 1, 40, 27), 1, (25.0, 30.0), 0),
+    "lm1_1_tm1": ((2, 2, 1, 1, 1, 3), (2, 2, 2, 1, 1, 1), 1, (10.0, 25.0), 0),
+    "lm1_1_u8b16": ((8, 16, 1, 1, 0, 8), (8, 16, 1, 1, 1, 1), 1, (30.0, 30.0), 0),
+    "os2": ((1, 1, 1, 1, 0, 2), (1, 1, 1, 2, 10, 9), 1, (5.0, 20.0), 0),
+    "os2_u2b2_tm1": ((2, 2, 1, 1, 1, 4), (2, 2, 2, 2, 10, 9), 1, (15.0, 25.0), 0),
+    "subslot_tm5": ((1, 2, 0, 3, 5, 7), (1, 2, 4, 1, 10, 9), 1, (22.0, 30.0), 0),
+}
+
 
 def random_bits(rng, n_bits):
     return rng.integers(0, 2, n_bits, dtype=np.uint8)

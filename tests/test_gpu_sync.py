@@ -134,7 +134,7 @@ def test_sync_then_demodulate_c4():
     pcc_llr = torch.zeros((2, 196), dtype=torch.int16, device=dev)
     pdc_llr = torch.zeros((2, sz["G"]), dtype=torch.int16, device=dev)
     phy.rx_pcc_batch(reps, iq, pcc_llr)
-    phy.rx_pdc_batch(ps, [dnrp.PdcReq(m[2], m[3]) for m in metas], pdc_llr)
+    phy.rx_pdc_batch([dnrp.PdcReq(ps, i, m[2], m[3]) for i, m in enumerate(metas)], iq, pdc_llr)
     phy.sync()
     g_pcc, g_pdc = pcc_llr.cpu().numpy(), pdc_llr.cpu().numpy()
     ocf = O.cfg(cfgt[0], cfgt[1], os_min=cfgt[3], L=cfgt[4], M=cfgt[5])

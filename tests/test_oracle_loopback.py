@@ -83,3 +83,22 @@ def test_mimo_report_codebook_search():
     r = O.rx(cf, ps, (H @ x).astype(np.complex64))
     assert r["mimo_N_TS_other"] == 4
     assert r["mimo_idx"] == 17
+
+
+@pytest.mark.parametrize("name", sorted(F.PARITY_CASES))
+def test_loopback_parity_cases(name):
+    """Every GPU parity configuration (phy_fixtures.PARITY_CASES) round-trips through the oracle on
+    the CPU at 30 dB: the checker itself supports the mode before the HIP path is compared with it."""
+    psd, cf_t, lr, _, cb = F.PARITY_CASES[name]
+    u_max, b_max, n_ant, os_min, L, M = cf_t
+    cf, ps = O.cfg(u_max, b_max, os_min, L, M, lr=lr), O.psdef(*psd)
+    sz = O.packet_sizes(ps)
+    S = O.dims(cf, ps)["N_packet_os_rs"]
+    rng = np.random.default_rng(1)
+    pcc_bits, pdc_bits = F.random_bits(rng, 196), F.random_bits(rng, sz["G"])
+    x, _ = O.tx(cf, ps, O.pack_bits(pcc_bits), O.pack_bits(pdc_bits), S, codebook=cb)
+    assert x.shape[0] == sz["N_TX"]
+    win = F.channel(rng, x, n_ant, S, 5, 0.0, 30.0)
+    r = O.rx(cf, ps, win, 5, 0.0, 100, 1)
+    assert np.array_equal((r["pcc_llr"] > 0).astype(np.uint8), pcc_bits)
+    assert np.mean((r["pdc_llr"] > 0).astype(np.uint8) != pdc_bits) < 5e-3
