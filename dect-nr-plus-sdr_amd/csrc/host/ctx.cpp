@@ -746,6 +746,7 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         pin[i].fine_peak = sr[i].fine_peak_time;
         pin[i].cfo_rad = sr[i].cfo_fractional_rad + sr[i].cfo_integer_rad;
         pin[i].inc0 = phasor_arg(pin[i].cfo_rad);
+        pin[i].win = sr[i].window;
     }
     {
         uint32_t o = 0;

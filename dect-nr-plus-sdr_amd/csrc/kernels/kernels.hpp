@@ -70,6 +70,7 @@ struct rx_pkt_in {          // from sync_report_t
     int64_t fine_peak;
     double inc0;            // effective CFO phasor increment (float phasor emulated)
     float cfo_rad;          // sync CFO (fractional + integer)
+    uint32_t win;           // window of iq_in holding the packet (dnrp_sync_report::window)
 };
 
 struct rx_pkt_state {       // written by rx_stf_kernel, read by the later RX kernels
@@ -94,7 +95,7 @@ struct rx_front_args {
     uint32_t npp;              // floats in taps_pp
     const float2* tw;
     const float2* stf;         // STF values for (b, N_eff_TX)
-    const float2* iq;          // [n][N_RX][S_in]
+    const float2* iq;          // [windows][N_RX][S_in]
     const rx_pkt_in* pin;
     rx_pkt_state* st;
     float2* Y;                 // [n][N_RX][n_sym_total][Nf_pad]

@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
     rx_pkt_state S;
 
     for (uint32_t a = 0; a < A.N_RX; ++a) {
-        const float2* x = A.iq + (size_t(pkt) * A.N_RX + a) * A.S_in;
+        const float2* x = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in;
         resample_block<HL>(A, x, in.fine_peak, 0, n_stf, inbuf, sbuf, taps, 0.0, in.inc0);
         double e = 0.0, pr = 0.0, pi = 0.0;
         for (uint32_t i = threadIdx.x; i < n_stf; i += blockDim.x) e += cnorm(sbuf[i]);
@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
     const uint32_t n_stf = A.STF_CP + Nd;
     for (uint32_t k = threadIdx.x; k < Nf; k += RX_THREADS)
         rot[k] = phasor(-S.sto_inc * static_cast<double>(N / 2) + S.sto_inc * static_cast<double>(k));
-    const float2* x = A.iq + (size_t(pkt) * A.N_RX + a) * A.S_in;
+    const float2* x = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in;
     const double phi_stf = static_cast<double>(n_stf) * in.inc0;  // mixer phase at the first data sample
     const float2 step1 = phasor(S.inc1);
     const uint32_t l0 = A.sym_first + blk * A.sym_per_block;
@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     float2* R = reg0 + w * region;
     // valid input window relative to the fine peak: history is zero before it (rx_synced.cpp:711-740)
     const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
-    const float2* src = A.iq + (size_t(pkt) * A.N_RX + a) * A.S_in + in.fine_peak + in0;
+    const float2* src = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in + in.fine_peak + in0;
     if (active) stage_span_lo<20>(R, src - in0, in0, n_in, q_lo, q_hi, lane, 64);
     __syncthreads();  // twiddles / taps (and this wave's own staging)
     if (!active) return;
@@ -439,7 +439,7 @@ rx_fft_stream_kernel(rx_front_args A, uint32_t n, uint32_t n_seg) {
     const int n_stf = static_cast<int>(A.STF_CP + Nd);
     // input q (relative to the fine peak) valid in [q_lo, q_hi): zero history before the window
     const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
-    const float2* __restrict__ xa = A.iq + (size_t(pkt) * A.N_RX + a) * A.S_in + in.fine_peak;
+    const float2* __restrict__ xa = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in + in.fine_peak;
     const double phi_stf = static_cast<double>(n_stf) * in.inc0;  // mixer phase at the first data sample
     const float2 step1 = phasor(S.inc1);
     const float2 s64 = phasor(64.0 * S.sto_inc);

@@ -62,7 +62,16 @@ class TxDesc(C.Structure):
 
 class SyncReport(C.Structure):
     _fields_ = [("fine_peak_time", C.c_int64), ("cfo_fractional_rad", C.c_float), ("cfo_integer_rad", C.c_float),
-                ("u", C.c_uint32), ("b", C.c_uint32), ("N_eff_TX", C.c_uint32)]
+                ("u", C.c_uint32), ("b", C.c_uint32), ("N_eff_TX", C.c_uint32), ("window", C.c_uint32)]
+
+    AUTO_WINDOW = 0xFFFFFFFF
+
+    def __init__(self, fine_peak_time=0, cfo_fractional_rad=0.0, cfo_integer_rad=0.0, u=0, b=0, N_eff_TX=0,
+                 window=None):
+        # window omitted: the report's own index in the batch (one packet per window, resolved by
+        # Phy.rx_pcc_batch)
+        super().__init__(fine_peak_time, cfo_fractional_rad, cfo_integer_rad, u, b, N_eff_TX,
+                         SyncReport.AUTO_WINDOW if window is None else window)
 
 
 class SyncCfg(C.Structure):
@@ -96,12 +105,23 @@ SYNC_RESULT_DTYPE = _np_dtype(SyncResult)
 SYNC_REPORT_DTYPE = _np_dtype(SyncReport)
 
 
-def sync_reports(results):
-    """dnrp_sync_result rows -> dnrp_sync_report array for rx_pcc_batch (vectorised)."""
+def sync_reports(results, windows=None):
+    """dnrp_sync_result rows -> dnrp_sync_report array for rx_pcc_batch (vectorised). windows: the
+    sync window of each row (default: row i was found in window i)."""
     r = np.zeros(len(results), SYNC_REPORT_DTYPE)
     for k in ("fine_peak_time", "cfo_fractional_rad", "cfo_integer_rad", "u", "b", "N_eff_TX"):
         r[k] = results[k]
+    r["window"] = np.arange(len(results)) if windows is None else windows
     return r
+
+
+def found_reports(res, n_found):
+    """All packets a sync batch found: res [n_win, max_reports] + n_found [n_win] -> the
+    dnrp_sync_report array of the found packets in window order (window = its sync window)."""
+    n_found = np.asarray(n_found).astype(np.int64)
+    win = np.repeat(np.arange(len(n_found)), n_found)
+    k = np.concatenate([np.arange(c) for c in n_found]) if len(n_found) else np.zeros(0, np.int64)
+    return sync_reports(res[win, k], win)
 
 
 class PccReport(C.Structure):
@@ -270,30 +290,38 @@ class Phy:
                                       _stream_ptr(stream)), "dnrp_rx_sync_batch")
         return res, n_found
 
-    def _check_rx_windows(self, iq_in, n):
+    def _check_rx_windows(self, iq_in):
         import torch
         _check_tensor(iq_in, "iq_in", torch.float32, 4, int(self.cfg.device))
-        if iq_in.shape[0] < n or iq_in.shape[1] != self.cfg.N_TX_max or iq_in.shape[3] != 2:
-            raise ValueError(f"iq_in shape {tuple(iq_in.shape)}, expected [>={n}, {self.cfg.N_TX_max}, S_in, 2]")
+        if iq_in.shape[1] != self.cfg.N_TX_max or iq_in.shape[3] != 2:
+            raise ValueError(f"iq_in shape {tuple(iq_in.shape)}, expected [windows, {self.cfg.N_TX_max}, S_in, 2]")
 
     def rx_pcc_batch(self, reports, iq_in, pcc_llr, want_report=False, stream=None):
         """reports: list of SyncReport or a numpy SYNC_REPORT_DTYPE array (see sync_reports()).
         iq_in float32 [n, N_RX, S_in, 2]; pcc_llr int16 [n, 196]."""
         import torch
         n = len(reports)
-        self._check_rx_windows(iq_in, n)
+        self._check_rx_windows(iq_in)
         _check_tensor(pcc_llr, "pcc_llr", torch.int16, 2, int(self.cfg.device))
         if pcc_llr.shape[0] < n or pcc_llr.shape[1] != 196:
             raise ValueError(f"pcc_llr shape {tuple(pcc_llr.shape)}, expected [>={n}, 196]")
         if isinstance(reports, np.ndarray):
             assert reports.dtype == SYNC_REPORT_DTYPE and reports.flags.c_contiguous
+            wins = reports["window"]
             arr = C.c_void_p(reports.ctypes.data)
         else:
-            arr = C.cast((SyncReport * n)(*reports), C.c_void_p)
+            arr_s = (SyncReport * n)(*reports)
+            for i in range(n):  # SyncReport(...) without a window: its own index
+                if arr_s[i].window == SyncReport.AUTO_WINDOW:
+                    arr_s[i].window = i
+            wins = np.array([r.window for r in arr_s], np.int64)
+            arr = C.cast(arr_s, C.c_void_p)
+        if n and (wins.max() >= iq_in.shape[0] or wins.min() < 0):
+            raise ValueError(f"sync report window {int(wins.max())} outside iq_in ({iq_in.shape[0]} windows)")
         rep = (PccReport * n)() if want_report else None
         _chk(lib().dnrp_rx_pcc_batch(self._ctx, n, arr, C.c_void_p(iq_in.data_ptr()), iq_in.shape[2],
                                      C.c_void_p(pcc_llr.data_ptr()), rep, _stream_ptr(stream)), "dnrp_rx_pcc_batch")
-        self._pcc_n = n
+        self._pcc_windows = int(wins.max()) + 1 if n else 0
         return rep
 
     def rx_pdc_batch(self, reqs, iq_in, pdc_llr, want_report=False, stream=None):
@@ -301,7 +329,9 @@ class Phy:
         iq_in: the windows of the preceding rx_pcc_batch; pdc_llr int16 [m, >= max G] (row r = reqs[r])."""
         import torch
         m = len(reqs)
-        self._check_rx_windows(iq_in, getattr(self, "_pcc_n", 0))
+        self._check_rx_windows(iq_in)
+        if iq_in.shape[0] < getattr(self, "_pcc_windows", 0):
+            raise ValueError(f"iq_in holds {iq_in.shape[0]} windows, the PCC batch used {self._pcc_windows}")
         _check_tensor(pdc_llr, "pdc_llr", torch.int16, 2, int(self.cfg.device))
         arr = reqs if isinstance(reqs, C.Array) else (PdcReq * m)(*reqs)
         keys = {tuple(getattr(r.psdef, f) for f, _ in PsDef._fields_) for r in arr}

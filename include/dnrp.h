@@ -97,10 +97,12 @@ typedef struct {
 
 /* sync_report_t fields consumed by rx_synced_t (phy/rx/sync/sync_report.hpp) */
 typedef struct {
-    int64_t fine_peak_time;   /* hw-rate sample index of the packet start inside this packet's window */
+    int64_t fine_peak_time;   /* hw-rate sample index of the packet start inside its window */
     float cfo_fractional_rad; /* per DECT-rate sample */
     float cfo_integer_rad;
     uint32_t u, b, N_eff_TX;
+    uint32_t window;          /* window of iq_in holding the packet (the sync window it was found in:
+                                 several packets of one window share it) */
 } dnrp_sync_report;
 
 /* Synchronisation of one batch of windows (sync_chunk_t, worker_pool_config_t subset) */
@@ -201,8 +203,10 @@ int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32_t n, const
  * RX phase 1: synchronised PCC demodulation of n packets. Each packet is processed with the
  * (u, b, N_eff_TX) of its own sync report (packets are grouped internally, like independent
  * demoddecod_rx_pcc calls).
- *   sr       host [n]; fine_peak_time may be negative (zero history before the window start)
- *   iq_in    device [n][N_RX][S_in] cf32 slot windows, N_RX = cfg.N_TX_max
+ *   sr       host [n]; packet i lies in window sr[i].window of iq_in at sr[i].fine_peak_time (may
+ *            be negative: zero history before the window start)
+ *   iq_in    device [windows][N_RX][S_in] cf32, N_RX = cfg.N_TX_max; every sr[i].window must
+ *            index a window of it
  *   pcc_llr  device [n][196] int16, descrambled
  *   rep      host [n] (optional)
  * Device state for phase 2 (STF estimates, PCC-phase channel estimates) is kept in the context

@@ -96,8 +96,9 @@ def test_sync_two_packets_per_window():
     import dnrp
     rng = np.random.default_rng(23)
     phy = _phy("C2")
-    windows = [F.sync_window(rng, O, "C2", 3000, [300 + 7 * i, 1650 - 5 * i], 0.4 * (i - 1) * 2 * np.pi / 64)[0]
-               for i in range(3)]
+    made = [F.sync_window(rng, O, "C2", 3000, [300 + 7 * i, 1650 - 5 * i], 0.4 * (i - 1) * 2 * np.pi / 64)
+            for i in range(3)]
+    windows = [m[0] for m in made]
     sc = dnrp.SyncCfg(1, 1, 1, 3000, 4)
     res, cnt = _run(phy, sc, windows, 4)
     osc = O.sync_cfg(1, 1, n_ant=1, chunk_len=3000)
@@ -106,6 +107,26 @@ def test_sync_two_packets_per_window():
         assert len(ref) == 2 and int(cnt[w]) == 2
         for k, o in enumerate(ref):
             _compare(res[w, k], o, (w, k))
+    # both packets of every window demodulated from the shared window (dnrp_sync_report::window)
+    reps = dnrp.found_reports(res, cnt)
+    assert list(reps["window"]) == [0, 0, 1, 1, 2, 2]
+    dev = torch.device("cuda:0")
+    iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(3, 1, 3000, 2)).to(dev)
+    ps = dnrp.psdef(*F.CONFIGS["C2"][0])
+    G = phy.packet_sizes(ps)["G"]
+    pcc_llr = torch.zeros((6, 196), dtype=torch.int16, device=dev)
+    pdc_llr = torch.zeros((6, G), dtype=torch.int16, device=dev)
+    phy.rx_pcc_batch(reps, iq, pcc_llr)
+    meta = [m for _, ms in made for m in ms]
+    phy.rx_pdc_batch([dnrp.PdcReq(ps, i, meta[i][2], meta[i][3]) for i in range(6)], iq, pdc_llr)
+    phy.sync()
+    ocf, ops = O.cfg(1, 1), O.psdef(*F.CONFIGS["C2"][0])
+    for i in range(6):
+        r = O.rx(ocf, ops, windows[int(reps["window"][i])], int(reps["fine_peak_time"][i]),
+                 float(reps["cfo_fractional_rad"][i]), meta[i][2], meta[i][3])
+        assert np.abs(pcc_llr[i].cpu().numpy().astype(int) - r["pcc_llr"]).max() <= 1, i
+        assert np.abs(pdc_llr[i].cpu().numpy().astype(int) - r["pdc_llr"]).max() <= 1, i
+        assert np.array_equal(np.unpackbits(meta[i][1])[:G], (r["pdc_llr"] > 0).astype(np.uint8)), i
 
 
 def test_sync_then_demodulate_c4():
