@@ -163,7 +163,7 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
     }
     t->dm = geo::make_dims(c, d, t->q);
     t->plan = make_plan(t->dm.Nd);
-    t->rs = geo::make_resampler(c.L, c.M, c.os_min);
+    t->rs = geo::make_resampler(c.L, c.M, c.os_min, prm::RS_TX);
     const auto m = geo::build_maps(d.b, t->tm.N_TS, t->tm.N_eff_TX, t->q.N_DF_symb);
     std::vector<float2> stf(m.Nf);
     for (uint32_t k = 0; k < m.Nf; ++k) stf[k] = make_float2(m.stf[k].real(), m.stf[k].imag());
@@ -260,7 +260,7 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
     t->n_pattern = u == 1 ? 7 : 9;
     t->pattern_len = 16 * b * t->Nd / (64 * b);
     t->plan = make_plan(t->Nd);
-    t->rs = geo::make_resampler(c.M, c.L, c.os_min);  // RX swaps L and M (rx_synced.cpp:65-73)
+    t->rs = geo::make_resampler(c.M, c.L, c.os_min, prm::RS_RX_SYNCED);  // RX swaps L and M (rx_synced.cpp:65-73)
     t->maps = geo::build_maps(b, N_eff_TX, N_eff_TX, 20);
     std::vector<geo::op_t> pcc_ops, dummy;
     geo::build_rx_ops(t->maps, N_eff_TX, 20, c.chestim_mode_lr != 0, std::max(1u, c.chestim_lr_stride), pcc_ops, dummy,
@@ -322,18 +322,21 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
     // MIMO report tables (estimator_mimo.cpp:80-160): per TS the latest DRS symbol carrying it, its
     // cells at offset step/2 + c*step (step = N_DRS_cells_b / 4) and their DRS values
     {
-        const uint32_t NTS = tm.N_eff_TX, nd = t->maps.drs_v.size() / 8, step = nd / 4, off = step / 2;
-        std::vector<uint32_t> cells(NTS * 4, 0);
-        std::vector<float> signs(NTS * 4, 1.f);
+        const uint32_t NTS = tm.N_eff_TX, nd = t->maps.drs_v.size() / 8, step = nd / prm::RX_MIMO_WIDEBAND_CELLS,
+                       off = step / 2;
+        constexpr uint32_t NW = prm::RX_MIMO_WIDEBAND_CELLS;
+        static_assert(NW == 4, "rx_mimo_kernel sums 4 wideband cells");
+        std::vector<uint32_t> cells(NTS * NW, 0);
+        std::vector<float> signs(NTS * NW, 1.f);
         for (uint32_t ts = 0; ts < NTS; ++ts) {
             const geo::drs_sym_t* last = nullptr;
             for (const auto& d : t->maps.drs)
                 if (d.ts_first <= ts && ts <= d.ts_last) last = &d;
             if (!last) continue;
-            for (uint32_t c = 0; c < 4; ++c) {
+            for (uint32_t c = 0; c < NW; ++c) {
                 const uint32_t i = off + c * step;
-                cells[ts * 4 + c] = (last->l << 16) | t->maps.drs_k[(last->parity * 4 + ts % 4) * nd + i];
-                signs[ts * 4 + c] = t->maps.drs_v[ts * nd + i];
+                cells[ts * NW + c] = (last->l << 16) | t->maps.drs_k[(last->parity * 4 + ts % 4) * nd + i];
+                signs[ts * NW + c] = t->maps.drs_v[ts * nd + i];
             }
         }
         static const uint32_t A_nonzero[9] = {0, 0, 2, 0, 12, 0, 0, 0, 0};  // beamforming_...mapping.hpp:110-119, N_TS = 1
@@ -789,7 +792,9 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
             rep[i].snr_dB = S[i].snr_pcc;
             rep[i].cfo_fractional_rad = sr[i].cfo_fractional_rad + (S[i].cfo_fine - pin[i].cfo_rad);
             rep[i].sto_fractional = S[i].sto_frac;
-            for (int a = 0; a < 8; ++a) rep[i].rms[a] = S[i].rms[a];
+            // run_stf_rms_estimation (rx_synced.cpp:620-655): sync's RMS kept where it is > 0
+            for (int a = 0; a < 8; ++a)
+                rep[i].rms[a] = (prm::RX_RMS_KEEP_SYNC && sr[i].rms[a] > 0.0f) ? sr[i].rms[a] : S[i].rms[a];
         }
     }
     return DNRP_OK;

@@ -441,7 +441,7 @@ static std::vector<float> kaiser_lpf(float fp, float fs, float ripple_dB, float 
     return h;
 }
 
-resampler_t make_resampler(uint32_t L, uint32_t M, uint32_t os_min) {  // resampler.cpp:56-160
+resampler_t make_resampler(uint32_t L, uint32_t M, uint32_t os_min, uint32_t user) {  // resampler.cpp:56-160
     resampler_t r;
     r.L = L;
     r.M = M;
@@ -449,10 +449,11 @@ resampler_t make_resampler(uint32_t L, uint32_t M, uint32_t os_min) {  // resamp
         r.h = {1.0f};
         return r;
     }
-    const float fpn = os_min == 1 ? 0.48f : os_min == 2 ? 0.30f : os_min == 4 ? 0.20f : 0.15f;
-    const float att = os_min == 1 ? 14.0f : 20.0f;  // resampler_param.hpp:77-88
+    // resampler_param.hpp:77-88 filter of this user and oversampling (resampler.cpp:74-95)
+    const uint32_t o = prm::rs_os_index(os_min);
     const float LM = static_cast<float>(std::max(L, M));
-    auto h = kaiser_lpf(fpn / LM, 0.499f / LM, 100.0f, att);
+    auto h = kaiser_lpf(prm::RS_F_PASS[user][o] / LM, prm::RS_F_STOP[user][o] / LM, prm::RS_RIPPLE_DONT_CARE,
+                        prm::RS_ATT_DB[user][o]);
     r.delay = static_cast<uint32_t>((h.size() - 1) / 2);
     for (auto& x : h) x *= static_cast<float>(L);
     const uint32_t padded = static_cast<uint32_t>((h.size() + L - 1) / L * L);
@@ -465,8 +466,7 @@ resampler_t make_resampler(uint32_t L, uint32_t M, uint32_t os_min) {  // resamp
 
 // ------------------------------------------------------------ Wiener LUTs (channel_lut.cpp, wiener.hpp)
 float lut_profile_snr_db(uint32_t p) {
-    static const float s[3] = {-5.0f, 15.0f, 35.0f};  // rx_synced_param.hpp:216-232
-    return s[p];
+    return static_cast<float>(prm::RX_SNR_DB[p]);  // RX_SYNCED_PARAM_SNR_DB_VEC (rx_synced_param.hpp:216-232)
 }
 
 namespace {
@@ -549,7 +549,7 @@ void lut_fill(uint32_t Nsv, uint32_t b, const stats_t& st, uint32_t n, lut_t* ou
                         best = s;
                         opt = i;
                     }
-                    if (s > best * 1.1) break;
+                    if (s > best * prm::RX_LUT_SEARCH_ABORT) break;
                 }
                 if (f == 0 || opt != prev)
                     for (uint32_t r = 0; r < n; ++r)
@@ -587,11 +587,9 @@ void lut_fill(uint32_t Nsv, uint32_t b, const stats_t& st, uint32_t n, lut_t* ou
 }  // namespace
 
 lut_t build_lut(uint32_t Nsv, uint32_t b, uint32_t b_max, uint32_t u_max, uint32_t profile) {
-    static const double nu[3] = {100.0, 100.0, 500.0}, tau[3] = {0.1e-6, 0.1e-6, 1.0e-6};
-    static const uint32_t nlr[3] = {14, 8, 3}, nl[3] = {7, 4, 2};
-    stats_t st{27000.0 * u_max, 72.0 / 64.0 / (27000.0 * u_max), nu[profile], tau[profile],
+    stats_t st{27000.0 * u_max, 72.0 / 64.0 / (27000.0 * u_max), prm::RX_NU_MAX_HZ[profile], prm::RX_TAU_RMS_SEC[profile],
                1.0 / std::pow(10.0, static_cast<double>(lut_profile_snr_db(profile)) / 10.0)};
-    const uint32_t n = Nsv > 0 ? nlr[profile] : nl[profile];
+    const uint32_t n = Nsv > 0 ? prm::RX_N_INTERP_LR[profile] : prm::RX_N_INTERP_L[profile];
     std::vector<std::vector<float>> vecs;
     if (b != b_max) lut_fill(Nsv, b_max, st, n, nullptr, vecs);
     lut_t L;

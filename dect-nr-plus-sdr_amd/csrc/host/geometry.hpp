@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "dnrp.h"
+#include "../params.hpp"
 
 namespace dnrp::geo {
 
@@ -71,7 +72,7 @@ struct resampler_t {
     uint32_t L = 1, M = 1, delay = 0, hl = 0, taps = 1;
     std::vector<float> h;
 };
-resampler_t make_resampler(uint32_t L, uint32_t M, uint32_t os_min);
+resampler_t make_resampler(uint32_t L, uint32_t M, uint32_t os_min, uint32_t user);  // user: prm::rs_user
 
 // Wiener LUT for one (N_step_virtual, b, SNR profile) — channel_lut.cpp:168-620
 struct lut_t {

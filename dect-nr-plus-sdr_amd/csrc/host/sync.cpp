@@ -88,15 +88,16 @@ sync_tables* get_sync(dnrp_ctx* ctx, uint32_t u, uint32_t b, int* err) {
     auto t = std::make_unique<sync_tables>();
     t->u = u;
     t->b = b;
-    t->n_pattern = u == 1 ? 7 : 9;  // stf.hpp:91-97
+    t->n_pattern = u == 1 ? prm::N_STF_PATTERN_U1 : prm::N_STF_PATTERN_U248;  // stf.hpp:91-97
     t->bos = b * c.os_min;
-    t->stf_len = 16 * t->n_pattern * t->bos;
-    t->pattern = 16 * t->bos;
-    t->step = t->pattern / 4;                          // RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_STEP_DIVIDER
-    t->D = static_cast<uint32_t>(1.0 * t->stf_len);    // ..._PEAK_MAX_SEARCH_LENGTH_IN_STFS_DP
-    t->rms_min = static_cast<float>(0.005f * std::sqrt(static_cast<double>(u) * b * 1728000.0 / 30.72e6));
-    t->xc_l = 16 * b * c.os_min * c.L / c.M;          // crosscorrelator.cpp:53-56
-    t->xc_len = 2 * t->xc_l + 1;
+    t->stf_len = prm::N_SAMPLES_STF_PATTERN * t->n_pattern * t->bos;
+    t->pattern = prm::N_SAMPLES_STF_PATTERN * t->bos;
+    t->step = t->pattern / prm::SYNC_STEP_DIVIDER;  // autocorrelator_detection.cpp:49
+    t->D = static_cast<uint32_t>(prm::SYNC_PEAK_MAX_SEARCH_STFS * t->stf_len);  // sync_chunk.cpp:68
+    t->rms_min = static_cast<float>(prm::SYNC_RMS_MIN * std::sqrt(static_cast<double>(u) * b * prm::SAMP_RATE_MIN_U_B /
+                                                                  prm::SYNC_RMS_MIN_REF_RATE));
+    t->xc_l = prm::SYNC_XC_SEARCH_LEFT * b * c.os_min * c.L / c.M;  // crosscorrelator.cpp:53-56
+    t->xc_len = t->xc_l + prm::SYNC_XC_SEARCH_RIGHT * b * c.os_min * c.L / c.M + 1;
     t->tmpl_len = t->stf_len * c.L / c.M;
     t->n_templates = c.N_TX_max >= 8 ? 4 : c.N_TX_max >= 4 ? 3 : c.N_TX_max >= 2 ? 2 : 1;  // physical_resources.hpp:44
     uint32_t lg = 0;
@@ -104,12 +105,12 @@ sync_tables* get_sync(dnrp_ctx* ctx, uint32_t u, uint32_t b, int* err) {
     t->log2_fft = lg;
     const uint32_t nf = 1u << lg;
     // sync resampler: RX direction, L and M swapped (sync_chunk.cpp:40-48)
-    t->rs = geo::make_resampler(c.M, c.L, c.os_min);
+    t->rs = geo::make_resampler(c.M, c.L, c.os_min, prm::RS_SYNC);
     if (!(c.L == 1 && c.M == 1)) {
         while ((t->rs.delay + t->m_star * t->rs.M) % t->rs.L) ++t->m_star;
         t->p_star = (t->rs.delay + t->m_star * t->rs.M) / t->rs.L;
     }
-    const auto rs_tx = geo::make_resampler(c.L, c.M, c.os_min);
+    const auto rs_tx = geo::make_resampler(c.L, c.M, c.os_min, prm::RS_TX);  // stf_template.cpp: TX filter
     std::vector<float2> tf(size_t(t->n_templates) * nf);
     for (uint32_t k = 0; k < t->n_templates; ++k) {
         auto tm = stf_template(u, b, c.os_min, rs_tx, 1u << k);
@@ -142,7 +143,8 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     const bool uok = sc->u == 1 || sc->u == 2 || sc->u == 4 || sc->u == 8;
     const bool bok = sc->b == 1 || sc->b == 2 || sc->b == 4 || sc->b == 8 || sc->b == 12 || sc->b == 16;
     if (!uok || !bok || sc->u > ctx->cfg.u_max || sc->b > ctx->cfg.b_max) return DNRP_EINVAL;
-    if (sc->N_ant_limited == 0 || sc->N_ant_limited > ctx->cfg.N_TX_max || sc->N_ant_limited > 8) return DNRP_EINVAL;
+    if (sc->N_ant_limited == 0 || sc->N_ant_limited > ctx->cfg.N_TX_max || sc->N_ant_limited > prm::SYNC_ANTENNA_LIMIT)
+        return DNRP_EINVAL;
     if (sc->max_reports == 0 || S_win == 0 || sc->chunk_len < ctx->cfg.L) return DNRP_EINVAL;
     (void)hipSetDevice(ctx->cfg.device);
     int err = DNRP_OK;

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "device_common.hpp"
+#include "../params.hpp"
 
 namespace dnrp::dev {
 

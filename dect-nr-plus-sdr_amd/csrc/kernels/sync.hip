@@ -396,10 +396,11 @@ __device__ bool detect_eval(const sync_args& A, const float* __restrict__ P, con
     double pw = 0.0;
     for (uint32_t i = 0; i < np; ++i) pw += P[s - (np - 1) + i];
     const double rms = sqrt(pw / static_cast<double>(A.stf_len));
-    if (rms < static_cast<double>(A.rms_min) || 2.0 < rms) return false;
+    static_assert(prm::SYNC_RMS_FRONT_STEPS == 2 && prm::SYNC_RMS_BACK_STEPS == 2, "front/back register pairs");
+    if (rms < static_cast<double>(A.rms_min) || static_cast<double>(prm::SYNC_RMS_MAX) < rms) return false;
     const double back = static_cast<double>(P[s - (np - 2)]) + P[s - (np - 3)];
     const double front = static_cast<double>(P[s - (np - 1)]) + P[s];
-    if (sqrt(back) * 0.5 >= sqrt(front)) return false;
+    if (sqrt(back) * prm::SYNC_RMS_FRONT_TO_BACK_RATIO >= sqrt(front)) return false;
     double cr = 0.0, ci = 0.0;
     for (uint32_t g = 0; g < A.n_uw; ++g) {
         double gr = 0.0, gi = 0.0;
@@ -413,8 +414,10 @@ __device__ bool detect_eval(const sync_args& A, const float* __restrict__ P, con
     }
     const double q = static_cast<double>(A.prefactor) * sqrt(cr * cr + ci * ci) / pw;
     const double metric = q * q;
-    if (metric < static_cast<double>(0.18f) || static_cast<double>(1.5f) < metric) return false;
-    if (!(static_cast<double>(0.18f) < metric)) return false;  // streak_t(0.18, 0, 1)::check
+    static_assert(prm::SYNC_METRIC_STREAK == 1 && prm::SYNC_METRIC_STREAK_GAIN == 0.0f, "single-step streak");
+    if (metric < static_cast<double>(prm::SYNC_METRIC_MIN) || static_cast<double>(prm::SYNC_METRIC_MAX) < metric)
+        return false;
+    if (!(static_cast<double>(prm::SYNC_METRIC_MIN) < metric)) return false;  // streak_t(0.18, 0, 1)::check
     out.rms = static_cast<float>(rms);
     out.metric = static_cast<float>(metric);
     return true;
@@ -558,7 +561,7 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
     }
     __syncthreads();
     // smoother (length 2 bos + 1, zero history) and last-maximum argmax
-    const uint32_t ns = 2 * A.bos + 1;
+    const uint32_t ns = (prm::SYNC_PEAK_SMOOTH_LEFT + prm::SYNC_PEAK_SMOOTH_RIGHT) * A.bos + 1;
     double best = -1.0;
     uint32_t bidx = 0;
     if (xb < xe) {
@@ -602,7 +605,7 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
             }
         }
         pk_metric = static_cast<float>(best);
-        pk_idx = r0 + bidx - A.bos;  // metric_smoother_bos_offset_to_center_samples
+        pk_idx = r0 + bidx - prm::SYNC_PEAK_SMOOTH_RIGHT * A.bos;  // metric_smoother_bos_offset_to_center_samples
     }
     __syncthreads();
 }
@@ -681,7 +684,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
         }
         __syncthreads();
         s_cur = static_cast<uint32_t>(sd) + 1;
-        const uint32_t det_time = s_cur * A.step, r0 = det_time - A.pattern;
+        const uint32_t det_time = s_cur * A.step, r0 = det_time - prm::SYNC_JUMP_BACK_PATTERNS * A.pattern;
         const float det_metric = s_metric;
         // ---------------- coarse peak search over one STF on every antenna
         const int64_t yb = static_cast<int64_t>(r0) - A.stf_len - SYNC_PAD_PEAK;
@@ -697,8 +700,9 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
         for (uint32_t a = 0; a < A.n_ant; ++a) {
             cm[a] = 0.f;
             const float m = s_pk_metric[a];
-            if (det_metric + (-0.25f) >= m) continue;
-            if (static_cast<int64_t>(det_time) + static_cast<int64_t>(-0.3 * static_cast<double>(A.stf_len)) >=
+            if (det_metric + prm::SYNC_PEAK_ABOVE_DETECTION >= m) continue;
+            if (static_cast<int64_t>(det_time) +
+                    static_cast<int64_t>(prm::SYNC_PEAK_DETECTION2PEAK_STFS * static_cast<double>(A.stf_len)) >=
                 static_cast<int64_t>(s_pk_idx[a]))
                 continue;
             cm[a] = m;
@@ -759,7 +763,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
             r.b = A.b;  // coarse_peak_f_domain.cpp:75-120: b of the radio device class
             out[nrep] = r;
         }
-        ignore = cpl + static_cast<uint32_t>(2.0 * static_cast<double>(A.stf_len));  // skip_after_peak
+        ignore = cpl + static_cast<uint32_t>(prm::SYNC_SKIP_AFTER_PEAK_STFS * static_cast<double>(A.stf_len));  // skip_after_peak
         ++nrep;
         __syncthreads();
     }

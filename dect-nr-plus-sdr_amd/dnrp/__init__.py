@@ -62,16 +62,18 @@ class TxDesc(C.Structure):
 
 class SyncReport(C.Structure):
     _fields_ = [("fine_peak_time", C.c_int64), ("cfo_fractional_rad", C.c_float), ("cfo_integer_rad", C.c_float),
-                ("u", C.c_uint32), ("b", C.c_uint32), ("N_eff_TX", C.c_uint32), ("window", C.c_uint32)]
+                ("u", C.c_uint32), ("b", C.c_uint32), ("N_eff_TX", C.c_uint32), ("window", C.c_uint32),
+                ("rms", C.c_float * 8)]
 
     AUTO_WINDOW = 0xFFFFFFFF
 
     def __init__(self, fine_peak_time=0, cfo_fractional_rad=0.0, cfo_integer_rad=0.0, u=0, b=0, N_eff_TX=0,
-                 window=None):
+                 window=None, rms=None):
         # window omitted: the report's own index in the batch (one packet per window, resolved by
-        # Phy.rx_pcc_batch)
+        # Phy.rx_pcc_batch); rms omitted: no sync RMS, the RX estimates every antenna's
         super().__init__(fine_peak_time, cfo_fractional_rad, cfo_integer_rad, u, b, N_eff_TX,
-                         SyncReport.AUTO_WINDOW if window is None else window)
+                         SyncReport.AUTO_WINDOW if window is None else window,
+                         (C.c_float * 8)(*(list(rms or []) + [0.0] * 8)[:8]))
 
 
 class SyncCfg(C.Structure):
@@ -111,6 +113,7 @@ def sync_reports(results, windows=None):
     r = np.zeros(len(results), SYNC_REPORT_DTYPE)
     for k in ("fine_peak_time", "cfo_fractional_rad", "cfo_integer_rad", "u", "b", "N_eff_TX"):
         r[k] = results[k]
+    r["rms"] = results["rms_array"]
     r["window"] = np.arange(len(results)) if windows is None else windows
     return r
 
@@ -141,7 +144,8 @@ class PdcReq(C.Structure):
 
 EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_get_packet_sizes",
            "dnrp_compute_packet_sizes", "dnrp_tx_batch", "dnrp_rx_sync_batch",
-           "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_kernel_time_total", "dnrp_strerror"]
+           "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_kernel_time_total",
+           "dnrp_strerror", "dnrp_get_radio_device_class", "dnrp_query_param", "dnrp_param_name"]
 
 _lib = None
 

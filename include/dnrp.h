@@ -103,6 +103,9 @@ typedef struct {
     uint32_t u, b, N_eff_TX;
     uint32_t window;          /* window of iq_in holding the packet (the sync window it was found in:
                                  several packets of one window share it) */
+    float rms[8];             /* sync_report_t::rms_array (dnrp_sync_result::rms_array): the RX keeps
+                                 the values > 0 and estimates the others over the STF
+                                 (RX_SYNCED_PARAM_RMS_KEEP_VALUES_PROVIDED_BY_SYNC, rx_synced.cpp:620-655) */
 } dnrp_sync_report;
 
 /* Synchronisation of one batch of windows (sync_chunk_t, worker_pool_config_t subset) */
@@ -140,7 +143,7 @@ typedef struct {
     float snr_dB;             /* estimator_snr after STF + DRS of the PCC symbols */
     float cfo_fractional_rad; /* sync value + STF re-estimate */
     float sto_fractional;     /* samples, estimator_sto on the STF */
-    float rms[8];             /* per RX antenna, over the STF */
+    float rms[8];             /* per RX antenna: the sync report's value where > 0, else the STF estimate */
 } dnrp_pcc_report;
 
 /* PHY part of pdc_report_t (rx_synced.cpp:432-435) with its mimo_report_t
@@ -233,6 +236,23 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
                       int16_t* pdc_llr, uint32_t llr_stride, dnrp_pdc_report* rep, void* stream);
 
 int dnrp_sync(dnrp_ctx* ctx, void* stream);
+
+/* sp3::radio_device_class_t (sections_part3/radio_device_class.hpp): the capabilities of a device
+ * class string such as "8.16.8.A"; a worker pool sizes itself from them (dnrp_cfg.u_max = u_min,
+ * b_max = b_min, N_TX_max = N_TX_min, as worker_pool_config_t does). Host only. DNRP_ECONFIG for a
+ * class the reference does not list (radio_device_class.cpp:26-150). */
+typedef struct {
+    uint32_t u_min, b_min, N_TX_min, mcs_index_min, M_DL_HARQ_min, M_connection_DL_HARQ_min, N_soft_min, Z_min;
+    uint32_t PacketLength_min;
+} dnrp_radio_device_class;
+int dnrp_get_radio_device_class(const char* name, dnrp_radio_device_class* out);
+
+/* The reference parameters the library is built with, by the reference's own names (sync_param.hpp
+ * RX_SYNC_PARAM_*, rx_synced_param.hpp RX_SYNCED_PARAM_* incl. "NAME[i]" vector entries, flags as
+ * 1 = defined / 0 = not defined, resampler_param_t::f_pass_norm[user][os] etc., constants::*).
+ * Host only: DNRP_EINVAL for an unknown name. dnrp_param_name(i) enumerates them (NULL past the end). */
+int dnrp_query_param(const char* name, double* value);
+const char* dnrp_param_name(uint32_t index);
 
 /* Kernel timing (only when the environment has DNRP_TIMING=1 at dnrp_ctx_create): HIP events
  * recorded on the caller's stream around each launch. Names: "tx", "sync_steps", "sync_detect",

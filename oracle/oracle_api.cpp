@@ -5,10 +5,12 @@
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <string>
 #include <thread>
 
 #include "oracle.hpp"
 #include "oracle_dsp.hpp"
+#include "oracle_params.hpp"
 
 using namespace orc;
 
@@ -26,6 +28,73 @@ static cfg_t to_cfg(const uint32_t* c) {
 }
 
 extern "C" {
+
+// ---- the reference parameters the restatement uses, by the reference's names (oracle_params.hpp);
+// compared with the reference-compiled values in tests/test_oracle_pins.py. -1: unknown name.
+int oracle_query_param(const char* name, double* v) {
+    using namespace orc::prm;
+    const std::string n(name);
+    struct kv {
+        const char* k;
+        double v;
+    };
+    static const kv T[] = {
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_ANTENNA_LIMIT", ANTENNA_LIMIT},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_OVERLAP_LENGTH_IN_STFS_DP", OVERLAP_STFS},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_STEP_DIVIDER", STEP_DIVIDER},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_RESUM_PERIODICITY_IN_STEPS", DET_RESUM},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_RMS_THRESHOLD_MIN_REFERENCE_SAMPLE_RATE_DP", RMS_MIN_REF_RATE},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_RMS_THRESHOLD_MIN_SP", RMS_MIN},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_RMS_THRESHOLD_MAX_SP", RMS_MAX},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_RMS_FRONT_STEPS", RMS_FRONT_STEPS},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_RMS_BACK_STEPS", RMS_BACK_STEPS},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_RMS_FRONT_TO_BACK_RATIO", RMS_FRONT_TO_BACK},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_METRIC_THRESHOLD_MIN_SP", METRIC_MIN},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_METRIC_THRESHOLD_MAX_SP", METRIC_MAX},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_METRIC_STREAK_RELATIVE_GAIN_SP", STREAK_GAIN},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_METRIC_STREAK", STREAK},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_JUMP_BACK_IN_PATTERNS", JUMP_BACK_PATTERNS},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_SKIP_AFTER_PEAK_IN_STFS_DP", SKIP_AFTER_PEAK_STFS},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_PEAK_SAMPLES_REQUEST_IN_PATTERNS", PEAK_REQUEST_PATTERNS},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_PEAK_RESUM_PERIODICITY_IN_STEPS", PEAK_RESUM},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_PEAK_MAX_SEARCH_LENGTH_IN_STFS_DP", PEAK_MAX_SEARCH_STFS},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_PEAK_MOVMEAN_SMOOTH_LEFT", SMOOTH_LEFT},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_PEAK_MOVMEAN_SMOOTH_RIGHT", SMOOTH_RIGHT},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_PEAK_METRIC_ABOVE_DETECTION_THRESHOLD_SP", PEAK_ABOVE_DETECTION},
+        {"RX_SYNC_PARAM_AUTOCORRELATOR_PEAK_DETECTION2PEAK_IN_STFS_DP", DETECTION2PEAK_STFS},
+        {"RX_SYNC_PARAM_CROSSCORRELATOR_SEARCH_LEFT_SAMPLES", XC_SEARCH_LEFT},
+        {"RX_SYNC_PARAM_CROSSCORRELATOR_SEARCH_RIGHT_SAMPLES", XC_SEARCH_RIGHT},
+        {"RX_SYNCED_PARAM_CHANNEL_LUT_SEARCH_ABORT_THRESHOLD", LUT_SEARCH_ABORT},
+        {"RX_SYNCED_PARAM_MIMO_N_WIDEBAND_CELLS", MIMO_WIDEBAND_CELLS},
+        {"RX_SYNCED_PARAM_RMS_PERCENTAGE_OF_STF_USED_FOR_RMS_ESTIMATION", RMS_STF_PERCENT},
+        {"RX_SYNCED_PARAM_RMS_KEEP_VALUES_PROVIDED_BY_SYNC", RMS_KEEP_SYNC},
+        {"resampler_param_t::PASSBAND_RIPPLE_DONT_CARE", RS_RIPPLE},
+    };
+    for (const auto& e : T)
+        if (n == e.k) {
+            *v = e.v;
+            return 0;
+        }
+    const char* vec[5] = {"RX_SYNCED_PARAM_NU_MAX_HZ_VEC[", "RX_SYNCED_PARAM_TAU_RMS_SEC_VEC[", "RX_SYNCED_PARAM_SNR_DB_VEC[",
+                          "RX_SYNCED_PARAM_NOF_DRS_INTERP_LR_VEC[", "RX_SYNCED_PARAM_NOF_DRS_INTERP_L_VEC["};
+    for (int k = 0; k < 5; ++k)
+        for (int i = 0; i < 3; ++i)
+            if (n == std::string(vec[k]) + std::to_string(i) + "]") {
+                const double vals[5] = {NU_MAX_HZ[i], TAU_RMS_SEC[i], SNR_DB[i], double(N_INTERP_LR[i]),
+                                        double(N_INTERP_L[i])};
+                *v = vals[k];
+                return 0;
+            }
+    const int osv[4] = {1, 2, 4, 8};
+    for (int u = 0; u < 3; ++u)
+        for (int o = 0; o < 4; ++o) {
+            const std::string k = "[" + std::to_string(u) + "][" + std::to_string(osv[o]) + "]";
+            if (n == "resampler_param_t::f_pass_norm" + k) return *v = RS_F_PASS[o], 0;
+            if (n == "resampler_param_t::f_stop_norm" + k) return *v = RS_F_STOP[o], 0;
+            if (n == "resampler_param_t::f_stop_att_dB" + k) return *v = RS_ATT_DB[o], 0;
+        }
+    return -1;
+}
 
 // out: N_PACKET_symb, N_DF_symb, N_PDC_subc, N_DRS_subc, G, N_PDC_bits, N_TB_bits, C,
 //      N_samples_STF, N_samples_STF_CP_only, N_samples_DF, N_samples_GI, N_samples_packet_no_GI,
@@ -221,11 +290,11 @@ int oracle_tx(const uint32_t* cfg, const uint32_t* psdef, const uint32_t* desc_u
 //           12 mimo N_TS_other, 13 tm_3_7_beamforming_idx, 14 tm_3_7_beamforming_reciprocal_idx
 int oracle_rx(const uint32_t* cfg, const uint32_t* psdef, uint32_t N_RX, const float* iq, uint32_t S_in,
               int64_t fine_peak, double cfo_rad, uint32_t network_id, uint32_t plcf_type, int16_t* pcc_llr,
-              int16_t* pdc_llr, float* pcc_llr_f, float* pdc_llr_f, float* meta, int use_float) {
+              int16_t* pdc_llr, float* pcc_llr_f, float* pdc_llr_f, float* meta, int use_float, const float* sync_rms) {
     try {
         packet_sizes_t q;
         if (!get_packet_sizes(to_psdef(psdef), q)) return -1;
-        rx_in_t in{iq, N_RX, S_in, fine_peak, cfo_rad, network_id, plcf_type};
+        rx_in_t in{iq, N_RX, S_in, fine_peak, cfo_rad, network_id, plcf_type, sync_rms};
         rx_out_t o;
         if (use_float)
             rx_packet<float>(to_cfg(cfg), q, in, o);

@@ -14,6 +14,7 @@
 
 #include "oracle.hpp"
 #include "oracle_dsp.hpp"
+#include "oracle_params.hpp"
 
 namespace orc {
 
@@ -502,7 +503,11 @@ struct rx_state_t {
         for (uint32_t a = 0; a < N_RX; ++a) {
             double e = 0;
             for (uint32_t i = 0; i < len; ++i) e += std::norm(std::complex<double>(s[a][i].real(), s[a][i].imag()));
+            // run_stf_rms_estimation (rx_synced.cpp:620-655): over RMS_STF_PERCENT of the STF, the
+            // sync report's value kept where it is > 0
+            static_assert(prm::RMS_STF_PERCENT == 100, "whole STF");
             out.rms[a] = static_cast<float>(std::sqrt(e / len));
+            if (prm::RMS_KEEP_SYNC && in.sync_rms && a < 8 && in.sync_rms[a] > 0.0f) out.rms[a] = in.sync_rms[a];
             for (uint32_t i = 0; i < len; ++i) s[a][i] *= static_cast<R>(COVER[std::min<uint32_t>(i / dm.pattern_len, 8)]);
         }
         std::complex<double> sum{0, 0};

@@ -28,6 +28,7 @@ struct rx_in_t {  // sync_report_t subset + HARQ scrambling parameters
     int64_t fine_peak;  // sync_report_t::fine_peak_time_64 relative to iq[0]
     double cfo_rad;     // cfo_fractional_rad + cfo_integer_rad
     uint32_t network_id, plcf_type;
+    const float* sync_rms = nullptr;  // sync_report_t::rms_array[8] (nullable)
 };
 
 struct rx_out_t {

@@ -14,6 +14,7 @@
 
 #include "oracle.hpp"
 #include "oracle_dsp.hpp"
+#include "oracle_params.hpp"
 
 namespace orc {
 
@@ -112,18 +113,18 @@ sync_geom_t sync_geometry(const sync_cfg_t& c) {
     g.bos = c.b * c.os_min;
     g.stf_len = 16 * g.n_pattern * g.bos;
     g.pattern = g.stf_len / g.n_pattern;
-    g.step = g.pattern / 4;                                           // STEP_DIVIDER 4
+    g.step = g.pattern / prm::STEP_DIVIDER;                          // autocorrelator_detection.cpp:49
     g.A = c.chunk_len / c.L * c.M;                                    // sync_chunk.cpp:63-64
-    g.B = static_cast<uint32_t>(4.0 * g.stf_len);                     // OVERLAP_LENGTH_IN_STFS 4
-    g.C = g.pattern;
-    g.D = static_cast<uint32_t>(1.0 * g.stf_len);                     // PEAK_MAX_SEARCH_LENGTH 1
+    g.B = static_cast<uint32_t>(prm::OVERLAP_STFS * g.stf_len);      // sync_chunk.cpp:63-66
+    g.C = prm::PEAK_REQUEST_PATTERNS * g.pattern;
+    g.D = static_cast<uint32_t>(prm::PEAK_MAX_SEARCH_STFS * g.stf_len);  // sync_chunk.cpp:68
     g.search_len = g.A + g.B;
     g.lb_len = g.A + g.B + g.C + g.D;
-    g.xc_l = 16 * c.b * c.os_min * c.L / c.M;                          // crosscorrelator.cpp:53-56
-    g.xc_len = 2 * g.xc_l + 1;
+    g.xc_l = prm::XC_SEARCH_LEFT * c.b * c.os_min * c.L / c.M;        // crosscorrelator.cpp:53-56
+    g.xc_len = g.xc_l + prm::XC_SEARCH_RIGHT * c.b * c.os_min * c.L / c.M + 1;
     g.tmpl_len = g.stf_len * c.L / c.M;                                // stf_template.cpp:33
     g.n_templates = c.N_ant >= 8 ? 4 : c.N_ant >= 4 ? 3 : c.N_ant >= 2 ? 2 : 1;
-    g.rms_min = static_cast<float>(0.005f * std::sqrt(static_cast<double>(c.u) * c.b * 1728000.0 / 30.72e6));
+    g.rms_min = static_cast<float>(prm::RMS_MIN * std::sqrt(static_cast<double>(c.u) * c.b * 1728000.0 / prm::RMS_MIN_REF_RATE));
     return g;
 }
 
@@ -232,11 +233,11 @@ std::vector<sync_out_t> sync_search(const sync_cfg_t& c, const float* iq, uint32
     // ---- peak search state (autocorrelator_peak.cpp:37-81)
     std::vector<movsum_uw_t<C>> pcorr(NA);
     std::vector<movsum_t<R>> ppow(NA), smooth(NA);
-    const uint32_t smooth_right = 1 * g.bos;
+    const uint32_t smooth_right = prm::SMOOTH_RIGHT * g.bos;
     for (uint32_t a = 0; a < NA; ++a) {
         pcorr[a].init_uw(uw, g.pattern);
         ppow[a].init(g.stf_len);
-        smooth[a].init(1 * g.bos + 1 + smooth_right);
+        smooth[a].init(prm::SMOOTH_LEFT * g.bos + 1 + smooth_right);
     }
     auto set_initial_movsums = [&](uint32_t start) {  // autocorrelator_peak.cpp:266-309
         for (uint32_t a = 0; a < NA; ++a) {
@@ -268,7 +269,7 @@ std::vector<sync_out_t> sync_search(const sync_cfg_t& c, const float* iq, uint32
             dcorr[a].pop_push(cs);
             dpow[a].pop_push(ps);
         }
-        if (resum_cnt++ == 16) {
+        if (resum_cnt++ == prm::DET_RESUM) {
             for (uint32_t a = 0; a < NA; ++a) {
                 dcorr[a].resum();
                 dpow[a].resum();
@@ -282,14 +283,15 @@ std::vector<sync_out_t> sync_search(const sync_cfg_t& c, const float* iq, uint32
         for (uint32_t a = 0; a < NA && det < 0; ++a) {
             const R power = dpow[a].sum;
             const R rms = std::sqrt(power / static_cast<R>(g.stf_len));
-            if (rms < static_cast<R>(g.rms_min) || static_cast<R>(2.0f) < rms) continue;
-            const R rms_back = std::sqrt(dpow[a].sum_back(2));
-            const R rms_front = std::sqrt(dpow[a].sum_front(2));
-            if (rms_back * static_cast<R>(0.5) >= rms_front) continue;
+            if (rms < static_cast<R>(g.rms_min) || static_cast<R>(prm::RMS_MAX) < rms) continue;
+            const R rms_back = std::sqrt(dpow[a].sum_back(prm::RMS_BACK_STEPS));
+            const R rms_front = std::sqrt(dpow[a].sum_front(prm::RMS_FRONT_STEPS));
+            if (rms_back * static_cast<R>(prm::RMS_FRONT_TO_BACK) >= rms_front) continue;
             const R q = prefactor * std::abs(dcorr[a].sum) / power;
             const R metric = q * q;
-            if (metric < static_cast<R>(0.18f) || static_cast<R>(1.5f) < metric) continue;  // streak reset
-            if (!(static_cast<R>(0.18f) < metric)) continue;  // streak_t(0.18, 0, 1)::check
+            static_assert(prm::STREAK == 1 && prm::STREAK_GAIN == 0.0f, "single-step streak");
+            if (metric < static_cast<R>(prm::METRIC_MIN) || static_cast<R>(prm::METRIC_MAX) < metric) continue;  // streak reset
+            if (!(static_cast<R>(prm::METRIC_MIN) < metric)) continue;  // streak_t(0.18, 0, 1)::check
             det = static_cast<int>(a);
             det_rms = rms;
             det_metric = metric;
@@ -302,7 +304,7 @@ std::vector<sync_out_t> sync_search(const sync_cfg_t& c, const float* iq, uint32
         o.det_rms = static_cast<float>(det_rms);
         o.det_metric = static_cast<float>(det_metric);
         o.det_time = r;
-        o.det_time_jb = r - g.pattern;
+        o.det_time_jb = r - prm::JUMP_BACK_PATTERNS * g.pattern;
         o.u = c.u;
         const uint32_t r0 = o.det_time_jb, r_max = r0 + g.D;
         set_initial_movsums(r0 - g.stf_len);
@@ -323,7 +325,7 @@ std::vector<sync_out_t> sync_search(const sync_cfg_t& c, const float* iq, uint32
                         pk_metric[a] = sm;
                         pk_idx[a] = x - smooth_right;
                     }
-                    if (presum++ == 64) {
+                    if (presum++ == prm::PEAK_RESUM) {
                         for (uint32_t b2 = 0; b2 < NA; ++b2) {
                             pcorr[b2].resum();
                             ppow[b2].resum();
@@ -340,8 +342,9 @@ std::vector<sync_out_t> sync_search(const sync_cfg_t& c, const float* iq, uint32
         uint32_t nvalid = 0;
         for (uint32_t a = 0; a < NA; ++a) {
             const float m = static_cast<float>(pk_metric[a]);
-            if (o.det_metric + (-0.25f) >= m) continue;
-            if (static_cast<int64_t>(o.det_time) + static_cast<int64_t>(-0.3 * g.stf_len) >= static_cast<int64_t>(pk_idx[a]))
+            if (o.det_metric + prm::PEAK_ABOVE_DETECTION >= m) continue;
+            if (static_cast<int64_t>(o.det_time) + static_cast<int64_t>(prm::DETECTION2PEAK_STFS * g.stf_len) >=
+                static_cast<int64_t>(pk_idx[a]))
                 continue;
             o.coarse_metric[a] = m;
             wsum += m * static_cast<float>(pk_idx[a]);
@@ -369,7 +372,7 @@ std::vector<sync_out_t> sync_search(const sync_cfg_t& c, const float* iq, uint32
         o.cfo_frac = cfo_w / msum2;
         o.b = c.b;  // coarse_peak_f_domain: b of the radio device class, integer CFO 0
         // skip_after_peak (autocorrelator_detection.cpp:130-138)
-        ignore_before = cpl + static_cast<uint32_t>(2.0 * g.stf_len);
+        ignore_before = cpl + static_cast<uint32_t>(prm::SKIP_AFTER_PEAK_STFS * g.stf_len);
         // coarse peak to hw time (rx_pacer.cpp:306-313, sync resampler L=M_tx, M=L_tx)
         double gt = static_cast<double>(cpl);
         gt *= static_cast<double>(c.L);

@@ -8,6 +8,7 @@
 #include <stdexcept>
 
 #include "oracle.hpp"
+#include "oracle_params.hpp"
 
 namespace orc {
 
@@ -613,16 +614,16 @@ void resampler_t::design(uint32_t L_, uint32_t M_, uint32_t os_min) {
         h = {1.0f};
         return;
     }
-    float fpn = 0, att = 0;
+    int oi = -1;
     switch (os_min) {
-        case 1: fpn = 0.48f; att = 14.0f; break;
-        case 2: fpn = 0.30f; att = 20.0f; break;
-        case 4: fpn = 0.20f; att = 20.0f; break;
-        case 8: fpn = 0.15f; att = 20.0f; break;
+        case 1: oi = 0; break;
+        case 2: oi = 1; break;
+        case 4: oi = 2; break;
+        case 8: oi = 3; break;
         default: throw std::runtime_error("os_min undefined");
     }
     const float LM = std::max(static_cast<float>(L), static_cast<float>(M));
-    auto taps = kaiser(fpn / LM, 0.499f / LM, 100.0f, att, 1.0f, true);
+    auto taps = kaiser(prm::RS_F_PASS[oi] / LM, prm::RS_F_STOP[oi] / LM, prm::RS_RIPPLE, prm::RS_ATT_DB[oi], 1.0f, true);
     filter_length = static_cast<uint32_t>(taps.size());
     delay = (filter_length - 1) / 2;
     for (auto& t : taps) t *= static_cast<float>(L);
@@ -642,10 +643,10 @@ uint64_t resampler_t::n_out_no_flush(uint64_t N) const {
 // ---------------------------------------------------------------- channel_lut.cpp / wiener.hpp
 std::vector<chest_stats_t> chest_profiles(uint32_t u_max) {
     const auto nm = get_numerology(u_max, 1);
-    const double nu[3] = {100.0, 100.0, 500.0f};
-    const double tau[3] = {0.1e-6, 0.1e-6, 1.0e-6};
-    const double snr[3] = {-5.0, 15.0, 35.0};
-    const uint32_t nlr[3] = {14, 8, 3}, nl[3] = {7, 4, 2};
+    const double* nu = prm::NU_MAX_HZ;
+    const double* tau = prm::TAU_RMS_SEC;
+    const double* snr = prm::SNR_DB;
+    const uint32_t *nlr = prm::N_INTERP_LR, *nl = prm::N_INTERP_L;
     std::vector<chest_stats_t> v;
     for (int i = 0; i < 3; ++i) {
         chest_stats_t s{};
@@ -741,7 +742,7 @@ void fill_lut(uint32_t Nsv, uint32_t b, const chest_stats_t& st, chest_lut_t& lu
                         best = s;
                         opt = i;
                     }
-                    if (s > best * 1.1) break;
+                    if (s > best * prm::LUT_SEARCH_ABORT) break;
                 }
                 if (f == 0 || opt != prev)  // channel_lut.cpp:399-437 refresh rule
                     for (uint32_t r = 0; r < n; ++r)
