@@ -149,6 +149,10 @@ def test_rx_parity(name):
     S = sz["N_samples_packet_os_rs"]
     windows, reports, nids, types, _, pdc = _rx_windows(rng, name, phy, ps, ops, ocf, snrs, cb)
     n, n_rx = len(windows), phy.cfg.N_TX_max
+    # packet 0's sync report carries an RMS for antenna 0 only: kept, the others estimated
+    # (RX_SYNCED_PARAM_RMS_KEEP_VALUES_PROVIDED_BY_SYNC, rx_synced.cpp:620-655)
+    reports[0].rms[0] = 0.123
+    sync_rms = [[0.123] + [0.0] * 7] + [None] * (n - 1)
     dev = torch.device("cuda:0")
     iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(n, n_rx, S, 2)).to(dev)
     pcc_llr = torch.zeros((n, 196), dtype=torch.int16, device=dev)
@@ -159,8 +163,11 @@ def test_rx_parity(name):
     phy.sync()
     g_pcc, g_pdc = pcc_llr.cpu().numpy(), pdc_llr.cpu().numpy()
     for i in range(n):
-        r = _oracle_rx(ocf, ops, windows[i], reports[i], nids[i], types[i])
+        r = O.rx(ocf, ops, windows[i], reports[i].fine_peak_time, float(np.float32(reports[i].cfo_fractional_rad)),
+                 nids[i], types[i], sync_rms=sync_rms[i])
         _check_rx((name, i), g_pcc[i], g_pdc[i], rep1[i], rep2[i], r)
+        if i == 0:
+            assert rep1[0].rms[0] == np.float32(0.123) and r["rms"][0] == np.float32(0.123)
         if snrs[i] >= 20.0:  # uncoded hard decisions well above the demapping noise floor
             bits = np.unpackbits(pdc[i])[: sz["G"]]
             assert np.mean(bits != (g_pdc[i] > 0)) < 2e-2, (name, i)
