@@ -398,14 +398,13 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, con
     a.pin = ctx->rx_in.as<dev::rx_pkt_in>();
     a.st = ctx->rx_st.as<dev::rx_pkt_state>();
     a.Y = ctx->Y.as<float2>();
-    // streaming FFT front end (rx.hip rx_fft_stream_kernel): opt-in with DNRP_RX_STREAM=1. Parity
-    // green on MI355X but 17.1 ms vs 7.4 ms per 4096-slot PDC launch (52.8 GB HBM traffic per
-    // launch vs 20.3 GB: register spills), so rx_fft_wave_kernel stays the default
-    static const int rx_stream_env = [] {
-        const char* e = std::getenv("DNRP_RX_STREAM");
-        return e ? std::atoi(e) : 0;
+    // compile-time-tap front end (rx.hip rx_fft_wave_kernel<.., true>) where the run-time taps are
+    // the generated ones bit for bit; DNRP_RX_CT=0 forces the tap-table variant (A/B)
+    static const int ct_env = [] {
+        const char* e = std::getenv("DNRP_RX_CT");
+        return e ? std::atoi(e) : 1;
     }();
-    a.stream = (rx_stream_env && dev::rx_stream_taps_match(t->rs.h.data(), t->rs.h.size())) ? 1u : 0u;
+    a.stream = (ct_env && dev::rx_stream_taps_match(t->rs.h.data(), t->rs.h.size())) ? 1u : 0u;
     return a;
 }
 

@@ -100,7 +100,7 @@ struct rx_front_args {
     const rx_pkt_in* pin;
     rx_pkt_state* st;
     float2* Y;                 // [n][N_RX][n_sym_total][Nf_pad]
-    uint32_t stream;           // rx_fft_stream_kernel allowed (host: compiled-in taps match)
+    uint32_t stream;           // compile-time-tap front end allowed (host: compiled-in taps match)
     const uint32_t* sel;       // [launch packets][2]: PCC-batch slot, output row (rx_slot_of / rx_row_of)
 };
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);

@@ -300,8 +300,8 @@ __host__ __device__ inline uint32_t rxw_region(uint32_t L, uint32_t M, uint32_t 
     return (r + 15) / 16 * 16;
 }
 
-template <int LR, int MR, int HLR>
-__global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A) {
+template <int LR, int MR, int HLR, bool CT>
+__global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu(4))) rx_fft_wave_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     using PB = pp_block<LR, MR, HLR>;
     constexpr uint32_t Nd = 1024;
@@ -312,11 +312,15 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     const uint32_t a = (blockIdx.x / nblk) % A.N_RX;
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / (nblk * A.N_RX));
     const uint32_t region = rxw_region(LR, MR, PB::W);
-    float2* twl = smem;                                  // Nd
-    float* taps = reinterpret_cast<float*>(twl + Nd);    // npp
-    float2* reg0 = twl + Nd + (A.npp + 1) / 2;           // RXW_SYMS regions
-    stage_copy<4>(twl, A.tw, Nd, threadIdx.x, RX_THREADS);
-    stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, RX_THREADS);
+    // CT (compile-time taps, pp_const): no tap table and register twiddles, only the wave regions
+    // live in LDS (4 workgroups per CU instead of 3); otherwise LDS twiddles + tap table
+    float2* twl = smem;                                              // Nd (table path)
+    float* taps = reinterpret_cast<float*>(twl + Nd);                // npp (table path)
+    float2* reg0 = CT ? smem : twl + Nd + (A.npp + 1) / 2;           // RXW_SYMS regions
+    if constexpr (!CT) {
+        stage_copy<4>(twl, A.tw, Nd, threadIdx.x, RX_THREADS);
+        stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, RX_THREADS);
+    }
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t l = A.sym_first + blk * RXW_SYMS + w;
     const bool active = l < A.sym_first + A.sym_count;
@@ -333,52 +337,75 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
     const float2* src = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in + in.fine_peak + in0;
     if (active) stage_span_lo<20>(R, src - in0, in0, n_in, q_lo, q_hi, lane, 64);
-    __syncthreads();  // twiddles / taps (and this wave's own staging)
+    if constexpr (CT)
+        __builtin_amdgcn_wave_barrier();  // only the wave's own staging
+    else
+        __syncthreads();  // twiddles / taps (and this wave's own staging)
     if (!active) return;
-    // resampling + phase-continuous mixer, outputs in registers
+    // resampling + phase-continuous mixer
     const double phi_stf = static_cast<double>(n_stf) * in.inc0;  // mixer phase at the first data sample
     const float2 step1 = phasor(S.inc1);
-    float2 ys[BR][LR];
-    {
+    auto mix = [&](int q, float2 (&y)[LR]) {
+        const int mb = static_cast<int>(A.m_star) + LR * q;
+        float2 r = phasor(phi_stf + static_cast<double>(mb - static_cast<int>(n_stf)) * S.inc1);
+#pragma unroll
+        for (int k = 0; k < LR; ++k) {
+            y[k] = cmul(y[k], r);
+            r = cmul(r, step1);
+        }
+    };
+    auto put = [&](int q, const float2 (&y)[LR]) {
+        const int mb = static_cast<int>(A.m_star) + LR * q;
+#pragma unroll
+        for (int k = 0; k < LR; ++k) {
+            const uint32_t idx = static_cast<uint32_t>(mb + k - m0);
+            if (idx < Nd) R[idx] = y[k];
+        }
+    };
+    if constexpr (CT) {
+        // output-major blocks with compile-time taps (no zero taps), one round of blocks at a time:
+        // the outputs of round rd land below every input a later round reads (block q writes
+        // R[< LR (q + 1)] and later blocks read from R[MR q'] with q' >= q + 64 > LR (q + 1) / MR),
+        // so each round stores its outputs before the next round loads its windows
+        using PD = pp_direct<LR, MR, HLR>;
+        static_assert(taps_rx_9_10::L == LR && taps_rx_9_10::M == MR && taps_rx_9_10::HL == HLR, "generated taps");
+        static_assert(LR * (64 + 1) <= MR * 64, "round outputs stay below the next round's windows");
+#pragma unroll
+        for (int rd = 0; rd < BR; ++rd) {
+            const int qr = static_cast<int>(lane) + 64 * rd;
+            const int q = qb0 + qr;
+            float2 xv[PD::W], y[LR];
+            PD::template load<(MR % 2) == 0>(R + MR * min(qr, qb1 - 1 - qb0), xv);
+            pp_const<taps_rx_9_10>::run(xv, y);
+            __builtin_amdgcn_wave_barrier();
+            if (q < qb1) {
+                mix(q, y);
+                put(q, y);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    } else {
+        float2 ys[BR][LR];
         // all rounds of the lane in one pass over the tap rows (pp_block::run_multi); rounds past
         // the symbol's last block read a valid window and are discarded
         const float2* xw[BR];
 #pragma unroll
         for (int rd = 0; rd < BR; ++rd) xw[rd] = R + MR * min(static_cast<int>(lane) + 64 * rd, qb1 - 1 - qb0);
         PB::template run_multi<BR>(xw, taps, ys);
-    }
 #pragma unroll
-    for (int rd = 0; rd < BR; ++rd) {
-        const int q = qb0 + static_cast<int>(lane) + 64 * rd;
-        if (q < qb1) {
-            const int mb = static_cast<int>(A.m_star) + LR * q;
-            float2 r = phasor(phi_stf + static_cast<double>(mb - static_cast<int>(n_stf)) * S.inc1);
+        for (int rd = 0; rd < BR; ++rd)
+            if (qb0 + static_cast<int>(lane) + 64 * rd < qb1) mix(qb0 + static_cast<int>(lane) + 64 * rd, ys[rd]);
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int k = 0; k < LR; ++k) {
-                ys[rd][k] = cmul(ys[rd][k], r);
-                r = cmul(r, step1);
-            }
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int rd = 0; rd < BR; ++rd) {
-        const int q = qb0 + static_cast<int>(lane) + 64 * rd;
-        if (q < qb1) {
-            const int mb = static_cast<int>(A.m_star) + LR * q;
-#pragma unroll
-            for (int k = 0; k < LR; ++k) {
-                const uint32_t idx = static_cast<uint32_t>(mb + k - m0);
-                if (idx < Nd) R[idx] = ys[rd][k];
-            }
-        }
+        for (int rd = 0; rd < BR; ++rd)
+            if (qb0 + static_cast<int>(lane) + 64 * rd < qb1) put(qb0 + static_cast<int>(lane) + 64 * rd, ys[rd]);
     }
     __builtin_amdgcn_wave_barrier();
     float2 v[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = R[lane + 64 * m];
     __builtin_amdgcn_wave_barrier();
-    wave_fft1024<-1>(v, R, twl, lane);
+    wave_fft1024<-1>(v, R, CT ? A.tw : twl, lane);  // CT: twiddles through the L1 (8 KB, every wave)
     // occupied bins: FFT bin n -> subcarrier index k (extract_bins), amplitude, STO derotation
     float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
     // STO derotation exp(j sto_inc (k - N/2)) is linear in m on each half: two running phasors
@@ -404,132 +431,6 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_wave_kernel(rx_front_args A
     }
 }
 
-// ---- streaming front end: N_b_DFT_os = 1024, 9/10 polyphase with compile-time taps (os_min 1).
-// One wavefront walks one (packet, antenna, segment of symbols). Per symbol: the hw-rate span of
-// its 1024 useful outputs (the CP's outputs are skipped) moves from registers into the wave's LDS
-// buffer and the next symbol's span is loaded into the same registers at once, so its loads are
-// in flight during this symbol's resampling, FFT and bin stores; two polyphase blocks per lane
-// (pp_const) + phase-continuous mixer; outputs into the same buffer; wave FFT; occupied bins,
-// amplitude-scaled and STO-derotated, to Y. No workgroup barrier.
-constexpr uint32_t RXS_WPG = 4;
-constexpr uint32_t RXS_SPAN = 1184;                 // >= M (blocks - 1) + W = 10 * 114 + 33
-constexpr uint32_t RXS_PRE = (RXS_SPAN + 63) / 64;  // prefetched samples per lane
-constexpr uint32_t RXS_SEG = 8;                     // symbols per wavefront
-static_assert(WFFT_XB <= RXS_SPAN, "FFT exchange buffer fits the span buffer");
-
-template <int LR, int MR, int HLR>
-__global__ void __launch_bounds__(64 * RXS_WPG) __attribute__((amdgpu_waves_per_eu(3)))
-rx_fft_stream_kernel(rx_front_args A, uint32_t n, uint32_t n_seg) {
-    using PD = pp_direct<LR, MR, HLR>;
-    static_assert(taps_rx_9_10::L == LR && taps_rx_9_10::M == MR && taps_rx_9_10::HL == HLR, "generated taps");
-    static_assert(2 * 64 * LR >= 1024 + 2 * LR, "two blocks per lane cover a symbol");
-    constexpr uint32_t Nd = 1024;
-    extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    float2* R = smem + wv * RXS_SPAN;
-    const uint32_t gw = blockIdx.x * RXS_WPG + wv;
-    const uint32_t seg = gw % n_seg, a = (gw / n_seg) % A.N_RX, pl = gw / (n_seg * A.N_RX);
-    if (pl >= n) return;
-    const uint32_t pkt = rx_slot_of(A.sel, pl);
-    const uint32_t s_a = seg * RXS_SEG, s_b = min(s_a + RXS_SEG, A.sym_count);
-    if (s_a >= s_b) return;
-    const rx_pkt_in in = A.pin[pkt];
-    const rx_pkt_state S = A.st[pkt];
-    const uint32_t N = A.N_occ;
-    const int n_stf = static_cast<int>(A.STF_CP + Nd);
-    // input q (relative to the fine peak) valid in [q_lo, q_hi): zero history before the window
-    const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
-    const float2* __restrict__ xa = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in + in.fine_peak;
-    const double phi_stf = static_cast<double>(n_stf) * in.inc0;  // mixer phase at the first data sample
-    const float2 step1 = phasor(S.inc1);
-    const float2 s64 = phasor(64.0 * S.sto_inc);
-    const float2 tw1 = wfft_tw<-1>(A.tw, 4 * (lane & 15u)), twl = wfft_tw<-1>(A.tw, lane);
-    auto m0_of = [&](uint32_t l) { return n_stf + static_cast<int>((l - 1) * (A.CP + Nd) + A.CP); };
-    auto qb0_of = [&](int m0) { return (m0 - static_cast<int>(A.m_star)) / LR; };  // m0 >= m_star
-    float2 pre[RXS_PRE];
-    auto fetch = [&](uint32_t l, uint32_t lid) {
-        const int64_t i0 = static_cast<int64_t>(A.p_star) + int64_t(MR) * qb0_of(m0_of(l)) - HLR;
-#pragma unroll
-        for (uint32_t j = 0; j < RXS_PRE; ++j) {
-            const int64_t q = i0 + lid + 64 * j;
-            pre[j] = (q >= q_lo && q < q_hi) ? xa[q] : make_float2(0.f, 0.f);
-        }
-    };
-    fetch(A.sym_first + s_a, lane);
-    for (uint32_t si = s_a; si < s_b; ++si) {
-        uint32_t lid = lane;  // opaque per symbol: no hoisted lane-dependent addresses
-        asm volatile("" : "+v"(lid));
-        const uint32_t l = A.sym_first + si;
-        const int m0 = m0_of(l), qb0 = qb0_of(m0);
-        const int nblk = (m0 + static_cast<int>(Nd) - static_cast<int>(A.m_star) + LR - 1) / LR - qb0;
-#pragma unroll
-        for (uint32_t j = 0; j < RXS_PRE; ++j)
-            if (lid + 64 * j < RXS_SPAN) R[lid + 64 * j] = pre[j];
-        if (si + 1 < s_b) fetch(l + 1, lid);
-        __builtin_amdgcn_wave_barrier();
-        float2 y[2][LR];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            __builtin_amdgcn_sched_barrier(0);  // one window live at a time
-            const int qr = min(static_cast<int>(lid) + 64 * b, nblk - 1);  // clamped: window inside the span
-            float2 xv[PD::W];
-            PD::template load<(MR % 2) == 0>(R + MR * qr, xv);
-            pp_const<taps_rx_9_10>::run(xv, y[b]);
-            const int mb = static_cast<int>(A.m_star) + LR * (qb0 + static_cast<int>(lid) + 64 * b);
-            float2 r = phasor(phi_stf + static_cast<double>(mb - n_stf) * S.inc1);
-#pragma unroll
-            for (int k = 0; k < LR; ++k) {
-                y[b][k] = cmul(y[b][k], r);
-                r = cmul(r, step1);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int qr = static_cast<int>(lid) + 64 * b;
-            const int mb = static_cast<int>(A.m_star) + LR * (qb0 + qr);
-            if (qr < nblk) {
-#pragma unroll
-                for (int k = 0; k < LR; ++k) {
-                    const uint32_t idx = static_cast<uint32_t>(mb + k - m0);
-                    if (idx < Nd) R[idx] = y[b][k];
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        float2 v[16];
-#pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = R[lid + 64 * m];
-        __builtin_amdgcn_wave_barrier();
-        {
-            float2 w1 = tw1, wl = twl;  // laundered: the twiddle powers stay inside the loop
-            asm volatile("" : "+v"(w1.x), "+v"(w1.y), "+v"(wl.x), "+v"(wl.y));
-            wave_fft1024_rt<-1>(v, R, w1, wl, lid);
-        }
-        // occupied bins: FFT bin n -> subcarrier index k, amplitude, STO derotation by two running
-        // phasors (one per FFT half) stepped by 64 bins
-        float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
-        float2 pa = phasor(S.sto_inc * static_cast<double>(lid));
-        float2 pb = phasor(S.sto_inc * (static_cast<double>(lid) - static_cast<double>(A.off_lower) - static_cast<double>(N / 2)));
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            const uint32_t nn = lid + 64 * m;
-            uint32_t k = 0xFFFFFFFFu;
-            float2 rot = pa;
-            if (nn <= N / 2) {
-                k = nn + N / 2;
-            } else if (nn >= A.off_lower && nn < A.off_lower + N / 2) {
-                k = nn - A.off_lower;
-                rot = pb;
-            }
-            if (k != 0xFFFFFFFFu) Yrow[k] = cmul(cscale(v[m], A.amp_scale), rot);
-            pa = cmul(pa, s64);
-            pb = cmul(pb, s64);
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
 bool rx_stream_taps_match(const float* h, size_t n) {  // run-time RX taps == compiled-in taps, bitwise
     if (n != static_cast<size_t>(taps_rx_9_10::N)) return false;
     for (size_t i = 0; i < n; ++i)
@@ -546,17 +447,15 @@ hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
         const size_t lds = base + rx_in_cap(Nd, a.CP, a.L, a.M, W) * sizeof(float2) + a.npp * sizeof(float);
         hipLaunchKernelGGL(kern, g, b, lds, st, a);
     };
-    if (a.stream && Nd == 1024 && a.L == 9 && a.M == 10 && a.hl == 24 && a.CP + Nd <= RXS_SPAN) {
-        const uint32_t n_seg = (a.sym_count + RXS_SEG - 1) / RXS_SEG;
-        const uint64_t waves = uint64_t(n) * a.N_RX * n_seg;
-        hipLaunchKernelGGL((rx_fft_stream_kernel<9, 10, 24>), dim3(static_cast<uint32_t>((waves + RXS_WPG - 1) / RXS_WPG)),
-                           dim3(64 * RXS_WPG), RXS_WPG * RXS_SPAN * sizeof(float2), st, a, n, n_seg);
-        return hipGetLastError();
-    }
     if (Nd == 1024 && a.L == 9 && a.M == 10 && a.hl == 24 && a.sym_per_block == RXW_SYMS) {  // os_min 1
         const uint32_t W = pp_block<9, 10, 24>::W;
-        const size_t lds = (Nd + (a.npp + 1) / 2 + RXW_SYMS * size_t(rxw_region(9, 10, W))) * sizeof(float2);
-        hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24>), g, b, lds, st, a);
+        if (a.stream) {  // host: run-time taps == compiled-in taps bit for bit
+            const size_t lds = RXW_SYMS * size_t(rxw_region(9, 10, W)) * sizeof(float2);
+            hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true>), g, b, lds, st, a);
+        } else {
+            const size_t lds = (Nd + (a.npp + 1) / 2 + RXW_SYMS * size_t(rxw_region(9, 10, W))) * sizeof(float2);
+            hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, false>), g, b, lds, st, a);
+        }
     } else if (a.L == 9 && a.M == 10 && a.hl == 24)  // os_min 1 (225 taps)
         fast(rx_fft_kernel<9, 10, 24>, pp_block<9, 10, 24>::W);
     else if (a.L == 9 && a.M == 10 && a.hl == 4)  // os_min 2

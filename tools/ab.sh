@@ -1,0 +1,12 @@
+#!/bin/bash
+# A/B of environment switches on the bench: tools/ab.sh "VAR=a" "VAR=b" ... -> per-kernel ms per 4096-slot chunk
+mkdir -p gpurun_out
+for v in "$@"; do
+  env $v timeout -k 10 200 python bench.py --steps 3 --no-cpu-baseline > gpurun_out/ab.log 2>&1 || { tail -5 gpurun_out/ab.log; exit 1; }
+  python3 - "$v" <<'PY'
+import json, sys
+d = json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1])
+n = d['steps'] * d['config']['slots_per_gpu_per_step'] // d['config']['chunk']
+print(sys.argv[1], d['value'], {k: round(v / n, 2) for k, v in d['kernels_ms_total'].items()}, 'ber', round(d['check']['pdc_hard_ber'], 6))
+PY
+done

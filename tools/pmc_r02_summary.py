@@ -1,0 +1,31 @@
+"""Summarise the PMC passes of tools/profile_r02.sh: per libdnrp kernel dispatch (grid size tells the
+PCC / PDC launches apart) the SQ counters per wave and FETCH_SIZE (x2, gfx950 wide-read correction,
+MI355X_MICROARCH.md §HBM) + WRITE_SIZE in GB per launch."""
+import collections
+import csv
+import glob
+import os
+import sys
+
+out = sys.argv[1]
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+cnt = collections.defaultdict(set)
+for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        name = r["Kernel_Name"]
+        if "dnrp" not in name:
+            continue
+        k = name.split("(")[0].replace("void dnrp::dev::", "").replace("dnrp::dev::", "") + "@" + r["Grid_Size"]
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        cnt[k].add((f, r["Dispatch_Id"]))
+lines = []
+for k, c in sorted(agg.items()):
+    n_disp = max(1, len({d for _, d in cnt[k]}) // max(1, len({f for f, _ in cnt[k]})))
+    w = c.get("SQ_WAVES", 0) / 2 or 1  # SQ_WAVES is collected in both SQ passes
+    per_wave = " ".join(f"{n}={v / w:.0f}" for n, v in sorted(c.items())
+                        if n.startswith("SQ_") and n != "SQ_WAVES")
+    fetch = 2 * c.get("FETCH_SIZE", 0) * 1024 / 1e9 / n_disp
+    write = c.get("WRITE_SIZE", 0) * 1024 / 1e9 / n_disp
+    lines.append(f"{k}  launches={n_disp} waves/launch={w / n_disp:.0f}  fetch={fetch:.3f}GB write={write:.3f}GB  "
+                 f"per-wave: {per_wave}")
+print("\n".join(lines))
