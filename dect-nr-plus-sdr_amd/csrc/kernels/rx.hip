@@ -11,6 +11,7 @@
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
+#include "rx_front.hpp"
 #include "taps_gen.hpp"
 
 namespace dnrp::dev {
@@ -305,15 +306,13 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     using PB = pp_block<LR, MR, HLR>;
     constexpr uint32_t Nd = 1024;
-    constexpr int BR = (Nd + 2 * LR) / LR / 64 + 1;  // block rounds per lane
-    const uint32_t N = A.N_occ;
     const uint32_t nblk = (A.sym_count + RXW_SYMS - 1) / RXW_SYMS;
     const uint32_t blk = blockIdx.x % nblk;
     const uint32_t a = (blockIdx.x / nblk) % A.N_RX;
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / (nblk * A.N_RX));
     const uint32_t region = rxw_region(LR, MR, PB::W);
-    // CT (compile-time taps, pp_const): no tap table and register twiddles, only the wave regions
-    // live in LDS (4 workgroups per CU instead of 3); otherwise LDS twiddles + tap table
+    // CT (compile-time taps, pp_const): no tap table, twiddles through the L1, only the wave
+    // regions live in LDS (4 workgroups per CU instead of 3); otherwise LDS twiddles + tap table
     float2* twl = smem;                                              // Nd (table path)
     float* taps = reinterpret_cast<float*>(twl + Nd);                // npp (table path)
     float2* reg0 = CT ? smem : twl + Nd + (A.npp + 1) / 2;           // RXW_SYMS regions
@@ -326,108 +325,54 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
     const bool active = l < A.sym_first + A.sym_count;
     const rx_pkt_in in = A.pin[pkt];
     const rx_pkt_state S = A.st[pkt];
-    const uint32_t n_stf = A.STF_CP + Nd;
-    const int m0 = static_cast<int>(n_stf + (l - 1) * (A.CP + Nd) + A.CP);  // first output of symbol l
-    const int qb0 = (m0 - static_cast<int>(A.m_star)) / LR;                  // m0 >= m_star
-    const int qb1 = (m0 + static_cast<int>(Nd) - static_cast<int>(A.m_star) + LR - 1) / LR;
-    const int64_t in0 = static_cast<int64_t>(A.p_star) + int64_t(MR) * qb0 - HLR;
-    const uint32_t n_in = static_cast<uint32_t>(MR * (qb1 - 1 - qb0) + PB::W);
+    const rx_span_t sp = rx_span<LR, MR, HLR>(A, l);
     float2* R = reg0 + w * region;
     // valid input window relative to the fine peak: history is zero before it (rx_synced.cpp:711-740)
     const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
-    const float2* src = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in + in.fine_peak + in0;
-    if (active) stage_span_lo<20>(R, src - in0, in0, n_in, q_lo, q_hi, lane, 64);
+    const float2* src = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in + in.fine_peak;
+    if (active) stage_span_lo<20>(R, src, sp.in0, sp.n_in, q_lo, q_hi, lane, 64);
     if constexpr (CT)
         __builtin_amdgcn_wave_barrier();  // only the wave's own staging
     else
         __syncthreads();  // twiddles / taps (and this wave's own staging)
     if (!active) return;
-    // resampling + phase-continuous mixer
-    const double phi_stf = static_cast<double>(n_stf) * in.inc0;  // mixer phase at the first data sample
-    const float2 step1 = phasor(S.inc1);
-    auto mix = [&](int q, float2 (&y)[LR]) {
-        const int mb = static_cast<int>(A.m_star) + LR * q;
-        float2 r = phasor(phi_stf + static_cast<double>(mb - static_cast<int>(n_stf)) * S.inc1);
-#pragma unroll
-        for (int k = 0; k < LR; ++k) {
-            y[k] = cmul(y[k], r);
-            r = cmul(r, step1);
-        }
-    };
-    auto put = [&](int q, const float2 (&y)[LR]) {
-        const int mb = static_cast<int>(A.m_star) + LR * q;
-#pragma unroll
-        for (int k = 0; k < LR; ++k) {
-            const uint32_t idx = static_cast<uint32_t>(mb + k - m0);
-            if (idx < Nd) R[idx] = y[k];
-        }
-    };
+    float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
     if constexpr (CT) {
-        // output-major blocks with compile-time taps (no zero taps), one round of blocks at a time:
-        // the outputs of round rd land below every input a later round reads (block q writes
-        // R[< LR (q + 1)] and later blocks read from R[MR q'] with q' >= q + 64 > LR (q + 1) / MR),
-        // so each round stores its outputs before the next round loads its windows
-        using PD = pp_direct<LR, MR, HLR>;
-        static_assert(taps_rx_9_10::L == LR && taps_rx_9_10::M == MR && taps_rx_9_10::HL == HLR, "generated taps");
-        static_assert(LR * (64 + 1) <= MR * 64, "round outputs stay below the next round's windows");
-#pragma unroll
-        for (int rd = 0; rd < BR; ++rd) {
-            const int qr = static_cast<int>(lane) + 64 * rd;
-            const int q = qb0 + qr;
-            float2 xv[PD::W], y[LR];
-            PD::template load<(MR % 2) == 0>(R + MR * min(qr, qb1 - 1 - qb0), xv);
-            pp_const<taps_rx_9_10>::run(xv, y);
-            __builtin_amdgcn_wave_barrier();
-            if (q < qb1) {
-                mix(q, y);
-                put(q, y);
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
+        rx_resample_ct<LR, MR, HLR>(A, in, S, sp, R, lane);
+        rx_fft_bins(A, S, R, lane, [&](uint32_t k, float2 v) { Yrow[k] = v; });
+        return;
     } else {
+        constexpr int BR = (Nd + 2 * LR) / LR / 64 + 1;  // block rounds per lane
+        const int n_stf = static_cast<int>(A.STF_CP + Nd);
+        const double phi_stf = static_cast<double>(n_stf) * in.inc0;  // mixer phase at the first data sample
+        const float2 step1 = phasor(S.inc1);
         float2 ys[BR][LR];
         // all rounds of the lane in one pass over the tap rows (pp_block::run_multi); rounds past
         // the symbol's last block read a valid window and are discarded
         const float2* xw[BR];
 #pragma unroll
-        for (int rd = 0; rd < BR; ++rd) xw[rd] = R + MR * min(static_cast<int>(lane) + 64 * rd, qb1 - 1 - qb0);
+        for (int rd = 0; rd < BR; ++rd) xw[rd] = R + MR * min(static_cast<int>(lane) + 64 * rd, sp.qb1 - 1 - sp.qb0);
         PB::template run_multi<BR>(xw, taps, ys);
-#pragma unroll
-        for (int rd = 0; rd < BR; ++rd)
-            if (qb0 + static_cast<int>(lane) + 64 * rd < qb1) mix(qb0 + static_cast<int>(lane) + 64 * rd, ys[rd]);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int rd = 0; rd < BR; ++rd)
-            if (qb0 + static_cast<int>(lane) + 64 * rd < qb1) put(qb0 + static_cast<int>(lane) + 64 * rd, ys[rd]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    float2 v[16];
+        for (int rd = 0; rd < BR; ++rd) {
+            const int q = sp.qb0 + static_cast<int>(lane) + 64 * rd;
+            if (q < sp.qb1) {
+                const int mb = static_cast<int>(A.m_star) + LR * q;
+                float2 r = phasor(phi_stf + static_cast<double>(mb - n_stf) * S.inc1);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) v[m] = R[lane + 64 * m];
-    __builtin_amdgcn_wave_barrier();
-    wave_fft1024<-1>(v, R, CT ? A.tw : twl, lane);  // CT: twiddles through the L1 (8 KB, every wave)
-    // occupied bins: FFT bin n -> subcarrier index k (extract_bins), amplitude, STO derotation
-    float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
-    // STO derotation exp(j sto_inc (k - N/2)) is linear in m on each half: two running phasors
-    // stepped by 64 bins instead of one sin/cos per bin
-    const float2 s64 = phasor(64.0 * S.sto_inc);
-    float2 pa = phasor(S.sto_inc * static_cast<double>(lane));  // n <= N/2: k - N/2 = n
-    float2 pb = phasor(S.sto_inc * (static_cast<double>(lane) - static_cast<double>(A.off_lower) -
-                                    static_cast<double>(N / 2)));  // upper FFT half: k - N/2 = n - off_lower - N/2
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const uint32_t n = lane + 64 * m;
-        uint32_t k = 0xFFFFFFFFu;
-        float2 rot = pa;
-        if (n <= N / 2) {
-            k = n + N / 2;
-        } else if (n >= A.off_lower && n < A.off_lower + N / 2) {
-            k = n - A.off_lower;
-            rot = pb;
+                for (int k = 0; k < LR; ++k) {
+                    const uint32_t idx = static_cast<uint32_t>(mb + k - sp.m0);
+                    if (idx < Nd) R[idx] = cmul(ys[rd][k], r);
+                    r = cmul(r, step1);
+                }
+            }
         }
-        if (k != 0xFFFFFFFFu) Yrow[k] = cmul(cscale(v[m], A.amp_scale), rot);
-        pa = cmul(pa, s64);
-        pb = cmul(pb, s64);
+        __builtin_amdgcn_wave_barrier();
+        // table path: twiddles from LDS (rx_fft_bins reads them through A.tw)
+        rx_front_args B = A;
+        B.tw = twl;
+        rx_fft_bins(B, S, R, lane, [&](uint32_t k, float2 v) { Yrow[k] = v; });
     }
 }
 

@@ -1,0 +1,109 @@
+// One-wavefront RX front end for N_b_DFT_os = 1024 with the compile-time 9/10 resampler taps
+// (rx_synced.cpp:711-771: run_mix_resample + run_cp_fft_scale) of rx_fft_wave_kernel (rx.hip). The
+// bins go to a caller-given store functor (Y in HBM).
+//
+// Symbol l (1-based data symbol) yields the DECT-rate outputs m0 .. m0+1023 (the CP outputs are
+// skipped); the polyphase blocks q in [qb0, qb1) cover them, reading hw-rate inputs in0 .. in0+n_in
+// relative to the fine peak. A wave stages that span in its LDS region R, resamples it there with
+// pp_const (output-major, no zero taps), applies the phase-continuous mixer, runs wave_fft1024 and
+// hands every occupied bin, amplitude-scaled and STO-derotated, to a store functor.
+#pragma once
+
+#include "kernels.hpp"
+#include "polyphase.hpp"
+#include "taps_gen.hpp"
+
+namespace dnrp::dev {
+
+struct rx_span_t {
+    int m0, qb0, qb1;
+    int64_t in0;
+    uint32_t n_in;
+};
+
+template <int LR, int MR, int HLR>
+__device__ __forceinline__ rx_span_t rx_span(const rx_front_args& A, uint32_t l) {
+    constexpr int W = pp_direct<LR, MR, HLR>::W;
+    rx_span_t s;
+    const uint32_t n_stf = A.STF_CP + 1024;
+    s.m0 = static_cast<int>(n_stf + (l - 1) * (A.CP + 1024) + A.CP);  // first output of symbol l
+    s.qb0 = (s.m0 - static_cast<int>(A.m_star)) / LR;                  // m0 >= m_star
+    s.qb1 = (s.m0 + 1024 - static_cast<int>(A.m_star) + LR - 1) / LR;
+    s.in0 = static_cast<int64_t>(A.p_star) + int64_t(MR) * s.qb0 - HLR;
+    s.n_in = static_cast<uint32_t>(MR * (s.qb1 - 1 - s.qb0) + W);
+    return s;
+}
+
+// R[i] = input in0 + i (staged), i < n_in  ->  R[j] = mixed output m0 + j, j < 1024
+template <int LR, int MR, int HLR>
+__device__ __forceinline__ void rx_resample_ct(const rx_front_args& A, const rx_pkt_in& in, const rx_pkt_state& S,
+                                               const rx_span_t& sp, float2* R, uint32_t lane) {
+    using PD = pp_direct<LR, MR, HLR>;
+    static_assert(taps_rx_9_10::L == LR && taps_rx_9_10::M == MR && taps_rx_9_10::HL == HLR, "generated taps");
+    constexpr int BR = (1024 + 2 * LR) / LR / 64 + 1;  // block rounds per lane
+    // the outputs of round rd land below every input a later round reads (block q writes
+    // R[< LR (q + 1)] and later blocks read from R[MR q'] with q' >= q + 64), so each round stores
+    // its outputs before the next round loads its windows
+    static_assert(LR * (64 + 1) <= MR * 64, "round outputs stay below the next round's windows");
+    const int n_stf = static_cast<int>(A.STF_CP + 1024);
+    const double phi_stf = static_cast<double>(n_stf) * in.inc0;  // mixer phase at the first data sample
+    const float2 step1 = phasor(S.inc1);
+#pragma unroll
+    for (int rd = 0; rd < BR; ++rd) {
+        const int qr = static_cast<int>(lane) + 64 * rd;
+        const int q = sp.qb0 + qr;
+        float2 xv[PD::W], y[LR];
+        PD::template load<(MR % 2) == 0>(R + MR * min(qr, sp.qb1 - 1 - sp.qb0), xv);
+        pp_const<taps_rx_9_10>::run(xv, y);
+        __builtin_amdgcn_wave_barrier();
+        if (q < sp.qb1) {
+            const int mb = static_cast<int>(A.m_star) + LR * q;
+            float2 r = phasor(phi_stf + static_cast<double>(mb - n_stf) * S.inc1);
+#pragma unroll
+            for (int k = 0; k < LR; ++k) {
+                const uint32_t idx = static_cast<uint32_t>(mb + k - sp.m0);
+                if (idx < 1024) R[idx] = cmul(y[k], r);
+                r = cmul(r, step1);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// wave FFT of R[0..1024) (R also serves as the exchange buffer, >= WFFT_XB float2) and the occupied
+// bins: FFT bin n -> subcarrier index k (n <= N/2: k = n + N/2; upper half: k = n - off_lower),
+// amplitude sqrt(N_b_OCC)/N_b_DFT_os, STO derotation exp(j sto_inc (k - N/2)) by two running
+// phasors stepped by 64 bins. put(k, value) for every k in [0, N_b_OCC]; R is free again when
+// put is called (all exchange reads have completed).
+template <class Put>
+__device__ __forceinline__ void rx_fft_bins(const rx_front_args& A, const rx_pkt_state& S, float2* R, uint32_t lane,
+                                            Put&& put) {
+    float2 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = R[lane + 64 * m];
+    __builtin_amdgcn_wave_barrier();
+    wave_fft1024<-1>(v, R, A.tw, lane);  // twiddles through the L1 (8 KB, every wave)
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t N = A.N_occ;
+    const float2 s64 = phasor(64.0 * S.sto_inc);
+    float2 pa = phasor(S.sto_inc * static_cast<double>(lane));
+    float2 pb = phasor(S.sto_inc * (static_cast<double>(lane) - static_cast<double>(A.off_lower) -
+                                    static_cast<double>(N / 2)));
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const uint32_t n = lane + 64 * m;
+        uint32_t k = 0xFFFFFFFFu;
+        float2 rot = pa;
+        if (n <= N / 2) {
+            k = n + N / 2;
+        } else if (n >= A.off_lower && n < A.off_lower + N / 2) {
+            k = n - A.off_lower;
+            rot = pb;
+        }
+        if (k != 0xFFFFFFFFu) put(k, cmul(cscale(v[m], A.amp_scale), rot));
+        pa = cmul(pa, s64);
+        pb = cmul(pb, s64);
+    }
+}
+
+}  // namespace dnrp::dev
