@@ -277,6 +277,7 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
             const auto L = geo::build_lut(mode ? Nsv : 0, b, c.b_max, c.u_max, p);
             ok = t->lut_pw[mode][p].upload(L.pilot_weight) && t->lut_w[mode][p].upload(L.weights);
             t->lut_n[mode][p] = L.n;
+            ok = ok && L.n < (1u << 15);  // eq_work packs the tap count into 15 bits
             t->lut_T[mode] = L.T;
         }
     std::vector<dev::rx_lut> luts(6);

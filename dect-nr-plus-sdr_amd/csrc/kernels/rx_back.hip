@@ -22,23 +22,45 @@ namespace dnrp::dev {
 // ===================================================================== SNR chain
 constexpr uint32_t SNR_THREADS = 256, MAX_DOPS = RX_MAX_DOPS;
 
+template <int NRX>
 __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
     __shared__ double s1s[MAX_DOPS], s2s[MAX_DOPS];
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x), nd = A.n_drs;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u, nw = SNR_THREADS / 64;
-    const float2* Yp = A.Y + size_t(pkt) * A.N_RX * A.n_sym_total * A.Nf_pad;
+    const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
+    const float2* Yp = A.Y + size_t(pkt) * NRX * ast;
     for (uint32_t d = wave; d < A.n_dops; d += nw) {
-        const uint32_t meta = A.dmeta[d], l = A.dl[d];
-        const uint32_t tf = meta & 0xFFu, tl = (meta >> 8) & 0xFFu, par = (meta >> 16) & 0xFFu, nts = tl - tf + 1;
+        const uint32_t meta = __builtin_amdgcn_readfirstlane(A.dmeta[d]);
+        const uint32_t l = __builtin_amdgcn_readfirstlane(A.dl[d]);
+        const uint32_t tf = meta & 0xFFu, tl = (meta >> 8) & 0xFFu, par = (meta >> 16) & 0xFFu;
+        const float2* rows = Yp + size_t(l) * A.Nf_pad;
         double s1 = 0.0, s2 = 0.0;
-        for (uint32_t e = lane; e < A.N_RX * nts * nd; e += 64) {
-            const uint32_t i = e % nd, t = tf + (e / nd) % nts, a = e / (nd * nts);
-            const uint32_t* kb = A.drs_k + (par * 4 + (t & 3u)) * nd;
-            const float* vv = A.drs_v + t * nd;
-            const float2* row = Yp + (size_t(a) * A.n_sym_total + l) * A.Nf_pad;
-            const float2 v = cscale(row[kb[i]], vv[i]);
-            s1 += cnorm(v);
-            if (i + 1 < nd) s2 += cnorm(csub(v, cscale(row[kb[i + 1]], vv[i + 1])));
+        // lanes take 64 consecutive DRS cells of one transmit stream for every RX antenna at once
+        // (the subcarrier index and DRS value are shared by the antennas); the right neighbour of
+        // the noise difference comes from the next lane, lane 63 fetches its own
+        for (uint32_t t = tf; t <= tl; ++t) {
+            const uint32_t* __restrict__ kb = A.drs_k + (par * 4 + (t & 3u)) * nd;
+            const float* __restrict__ vv = A.drs_v + t * nd;
+            for (uint32_t i0 = 0; i0 < nd; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const bool in = i < nd, nx = lane == 63 && i + 1 < nd;
+                const uint32_t k = in ? kb[i] : 0u, k1 = nx ? kb[i + 1] : 0u;
+                const float w = in ? vv[i] : 0.f, w1 = nx ? vv[i + 1] : 0.f;
+                float2 y[NRX], y1[NRX];
+#pragma unroll
+                for (int a = 0; a < NRX; ++a) {
+                    y[a] = in ? rows[a * ast + k] : make_float2(0.f, 0.f);
+                    y1[a] = nx ? rows[a * ast + k1] : make_float2(0.f, 0.f);
+                }
+#pragma unroll
+                for (int a = 0; a < NRX; ++a) {
+                    const float2 v = cscale(y[a], w);
+                    float2 vn = make_float2(__shfl_down(v.x, 1), __shfl_down(v.y, 1));
+                    if (lane == 63) vn = cscale(y1[a], w1);
+                    if (in) s1 += cnorm(v);
+                    if (i + 1 < nd) s2 += cnorm(csub(v, vn));
+                }
+            }
         }
         for (int o = 32; o > 0; o >>= 1) {
             s1 += __shfl_xor(s1, o);
@@ -87,7 +109,13 @@ __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
 
 hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st) {
     if (a.n_dops > MAX_DOPS) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(rx_snr_kernel, dim3(n), dim3(SNR_THREADS), 0, st, a);
+    switch (a.N_RX) {
+        case 1: hipLaunchKernelGGL(rx_snr_kernel<1>, dim3(n), dim3(SNR_THREADS), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(rx_snr_kernel<2>, dim3(n), dim3(SNR_THREADS), 0, st, a); break;
+        case 4: hipLaunchKernelGGL(rx_snr_kernel<4>, dim3(n), dim3(SNR_THREADS), 0, st, a); break;
+        case 8: hipLaunchKernelGGL(rx_snr_kernel<8>, dim3(n), dim3(SNR_THREADS), 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -108,21 +136,31 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
     int16_t* __restrict__ llr = A.llr + size_t(row) * A.llr_stride;
     const uint8_t* lutp = A.lut_d + size_t(pkt) * RX_MAX_DOPS;
     if (E.units == 0) return;
+    // software pipeline over the thread's units: the index loads (segment, kk, LUT pilot | weight
+    // indices) of unit u + CELL_THREADS are in flight while unit u is equalised
     uint32_t si = E.seg0;
-    rx_seg S = A.segs[si];
     uint32_t seg_end = si + 1 < E.seg1 ? A.segs[si + 1].u0 : E.units;
-    for (uint32_t u = threadIdx.x; u < E.units; u += CELL_THREADS) {
+    auto gather = [&](uint32_t u, eq_work<NT>& w) {
         while (u >= seg_end) {
             ++si;
-            S = A.segs[si];
             seg_end = si + 1 < E.seg1 ? A.segs[si + 1].u0 : E.units;
         }
+        const rx_seg S = A.segs[si];
         const uint32_t lut = S.drs_cnt ? lutp[S.drs_cnt - 1] : 0u;
         const uint32_t jj = S.j0 + (NT == 1 ? 1u : 2u) * (u - S.u0);
         const uint32_t l = A.is_pdc ? static_cast<uint32_t>(A.pdc_sym[jj]) : S.l;
-        eq_unit<NRX, NT>(A, S, zfi, nd2, lut, jj,
-                         [&](uint32_t a, uint32_t k) { return Yp[(size_t(a) * A.n_sym_total + l) * A.Nf_pad + k]; },
-                         seq, llr);
+        eq_gather<NT>(A, S, lut, jj, l * A.Nf_pad, w);
+    };
+    uint32_t u = threadIdx.x;
+    if (u >= E.units) return;
+    eq_work<NT> cur;
+    gather(u, cur);
+    for (; u < E.units; u += CELL_THREADS) {
+        eq_work<NT> nxt;
+        const bool more = u + CELL_THREADS < E.units;
+        if (more) gather(u + CELL_THREADS, nxt);
+        eq_finish<NRX, NT>(A, cur, Yp, zfi, nd2, seq, llr);
+        if (more) cur = nxt;
     }
 }
 
