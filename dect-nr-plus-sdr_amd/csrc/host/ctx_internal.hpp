@@ -178,6 +178,9 @@ struct dnrp_ctx {
     // synchronisation: per (u, b) tables, step sums and reports
     std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<dnrp::host::sync_tables>> synct;
     dbuf sy_P, sy_C, sy_res, sy_cnt;
+    // ring-buffer gather / continuous-stream synchronisation (stream.cpp)
+    dbuf ring_start, ring_win;
+    pinned st_ring, st_stream;
     // timing: HIP events recorded on the caller's stream around every launch (DNRP_TIMING=1)
     bool timing = false;
     struct ev_pool {

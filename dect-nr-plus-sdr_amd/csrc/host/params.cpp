@@ -24,7 +24,10 @@ std::vector<entry> build_table() {
     auto add = [&](const char* n, double v) { t.push_back({n, v}); };
     add("SECTIONS_PART_3_STF_COVER_SEQUENCE_ACTIVE", STF_COVER_SEQUENCE_ACTIVE);
     // sync_param.hpp
+    add("RX_SYNC_PARAM_MAX_NOF_BUFFERABLE_SYNC_BEFORE_ACQUIRING_BATON", SYNC_MAX_BUFFERABLE);
     add("RX_SYNC_PARAM_AUTOCORRELATOR_ANTENNA_LIMIT", SYNC_ANTENNA_LIMIT);
+    add("RX_SYNC_PARAM_SYNC_TIME_UNIQUE_LIMIT_IN_STF_PATTERNS_DP", SYNC_TIME_UNIQUE_LIMIT_PATTERNS);
+    add("RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_OVERLAP_LENGTH_IN_STFS_DP", SYNC_OVERLAP_STFS);
     add("RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_STEP_DIVIDER", SYNC_STEP_DIVIDER);
     add("RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_RMS_THRESHOLD_MIN_REFERENCE_SAMPLE_RATE_DP", SYNC_RMS_MIN_REF_RATE);
     add("RX_SYNC_PARAM_AUTOCORRELATOR_DETECTION_RMS_THRESHOLD_MIN_SP", SYNC_RMS_MIN);

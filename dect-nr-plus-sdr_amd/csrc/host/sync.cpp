@@ -158,7 +158,7 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     a.pattern = t->pattern;
     a.step = t->step;
     const uint64_t A_len = uint64_t(sc->chunk_len) / c.L * c.M;  // sync_chunk.cpp:63-64
-    const uint64_t search = A_len + static_cast<uint32_t>(4.0 * t->stf_len);
+    const uint64_t search = A_len + static_cast<uint32_t>(prm::SYNC_OVERLAP_STFS * t->stf_len);
     if (search > (1u << 30)) return DNRP_EINVAL;
     a.search_len = static_cast<uint32_t>(search);
     a.D = t->D;

@@ -181,6 +181,17 @@ struct rx_mimo_args {  // estimator_mimo_t::process_drs at the packet end, one w
 hipError_t launch_rx_mimo(const rx_mimo_args& a, uint32_t n, hipStream_t st);
 
 
+// ---- ring-buffer window gather (ring.hip): buffer_rx_t ring -> linear windows (rx_pacer.cpp:106-143)
+constexpr int RING_PAIRS = 4;  // sample pairs per thread
+struct ring_args {
+    const float2* ring;     // antenna a at ring + a * ant_stride, ring_len samples each
+    uint64_t ring_len, ant_stride;
+    const int64_t* start;   // [n] global start time of each window (>= 0), device
+    float2* out;            // [n][n_ant][S_win]
+    uint32_t n_ant, S_win;
+};
+hipError_t launch_ring_gather(const ring_args& a, uint32_t n, hipStream_t st);
+
 // ---- synchronisation (sync.hip): sync_chunk_t::search() per window, reports in search order
 struct sync_res {  // layout of dnrp_sync_result (include/dnrp.h)
     uint32_t found, det_ant;

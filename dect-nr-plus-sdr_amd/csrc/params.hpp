@@ -19,7 +19,10 @@ namespace dnrp::prm {
 constexpr bool STF_COVER_SEQUENCE_ACTIVE = true;
 
 // ------------------------------------------------------------------ sync_param.hpp
+constexpr uint32_t SYNC_MAX_BUFFERABLE = 10;             // RX_SYNC_PARAM_MAX_NOF_BUFFERABLE_SYNC_BEFORE_ACQUIRING_BATON
 constexpr uint32_t SYNC_ANTENNA_LIMIT = 8;               // RX_SYNC_PARAM_AUTOCORRELATOR_ANTENNA_LIMIT
+constexpr double SYNC_TIME_UNIQUE_LIMIT_PATTERNS = 1.0;  // RX_SYNC_PARAM_SYNC_TIME_UNIQUE_LIMIT_IN_STF_PATTERNS_DP
+constexpr double SYNC_OVERLAP_STFS = 4.0;                // ..._DETECTION_OVERLAP_LENGTH_IN_STFS_DP
 constexpr uint32_t SYNC_STEP_DIVIDER = 4;                // ..._DETECTION_STEP_DIVIDER
 constexpr double SYNC_RMS_MIN_REF_RATE = 30.72e6;        // ..._DETECTION_RMS_THRESHOLD_MIN_REFERENCE_SAMPLE_RATE_DP
 constexpr float SYNC_RMS_MIN = 0.005f;                   // ..._DETECTION_RMS_THRESHOLD_MIN_SP
@@ -81,6 +84,9 @@ constexpr float RS_ATT_DB[3][4] = {{14.0f, 20.0f, 20.0f, 20.0f}, {14.0f, 20.0f, 
 constexpr float RS_RIPPLE_DONT_CARE = 100.0f;            // resampler_param_t::PASSBAND_RIPPLE_DONT_CARE
 enum rs_user : uint32_t { RS_TX = 0, RS_SYNC = 1, RS_RX_SYNCED = 2 };
 __host__ __device__ constexpr uint32_t rs_os_index(uint32_t os) { return os == 1 ? 0 : os == 2 ? 1 : os == 4 ? 2 : 3; }
+
+// ------------------------------------------------------------------ common/adt/miscellaneous.hpp:71
+constexpr int64_t UNDEFINED_EARLY_64 = INT64_MIN / 8;    // common::adt::UNDEFINED_EARLY_64
 
 // ------------------------------------------------------------------ constants.hpp
 constexpr uint32_t N_B_DFT_MIN_U_B = 64;                 // constants::N_b_DFT_min_u_b

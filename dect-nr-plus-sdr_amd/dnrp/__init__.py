@@ -142,10 +142,17 @@ class PdcReq(C.Structure):
     _fields_ = [("psdef", PsDef), ("pcc_index", C.c_uint32), ("network_id", C.c_uint32), ("plcf_type", C.c_uint32)]
 
 
+class SyncStreamState(C.Structure):
+    """dnrp_sync_stream_state: baton_t's uniqueness state across dnrp_rx_sync_stream calls."""
+    _fields_ = [("sync_time_last", C.c_int64), ("sync_time_unique_limit", C.c_int64), ("packets", C.c_uint64),
+                ("not_unique", C.c_uint64)]
+
+
 EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_get_packet_sizes",
            "dnrp_compute_packet_sizes", "dnrp_tx_batch", "dnrp_rx_sync_batch",
            "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_kernel_time_total",
-           "dnrp_strerror", "dnrp_get_radio_device_class", "dnrp_query_param", "dnrp_param_name"]
+           "dnrp_strerror", "dnrp_get_radio_device_class", "dnrp_query_param", "dnrp_param_name",
+           "dnrp_ring_gather", "dnrp_sync_stream_init", "dnrp_sync_stream_window", "dnrp_rx_sync_stream"]
 
 _lib = None
 
@@ -171,6 +178,12 @@ def lib():
         L.dnrp_rx_pdc_batch.argtypes = [P, C.c_uint32, C.POINTER(PdcReq), P, C.c_uint32, P, C.c_uint32,
                                         C.POINTER(PdcReport), P]
         L.dnrp_sync.argtypes = [P, P]
+        L.dnrp_ring_gather.argtypes = [P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P, C.c_uint32, P, P]
+        L.dnrp_sync_stream_init.argtypes = [P, C.POINTER(SyncCfg), C.POINTER(SyncStreamState)]
+        L.dnrp_sync_stream_window.argtypes = [P, C.POINTER(SyncCfg)]
+        L.dnrp_sync_stream_window.restype = C.c_uint32
+        L.dnrp_rx_sync_stream.argtypes = [P, C.POINTER(SyncCfg), P, C.c_uint64, C.c_uint64, C.c_int64, C.c_uint32,
+                                          C.POINTER(SyncStreamState), P, C.POINTER(C.c_uint32), P, P]
         L.dnrp_last_kernel_ms.argtypes = [P, C.c_char_p, C.POINTER(C.c_float)]
         L.dnrp_kernel_time_total.argtypes = [P, C.c_char_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.c_int]
         L.dnrp_strerror.argtypes = [C.c_int]
@@ -350,6 +363,48 @@ class Phy:
 
     def sync(self, stream=None):
         _chk(lib().dnrp_sync(self._ctx, _stream_ptr(stream)), "dnrp_sync")
+
+    def _check_ring(self, ring, n_ant):
+        import torch
+        _check_tensor(ring, "ring", torch.float32, 3, int(self.cfg.device))
+        if ring.shape[0] < n_ant or ring.shape[2] != 2:
+            raise ValueError(f"ring shape {tuple(ring.shape)}, expected [>= {n_ant}, ring_len, 2]")
+
+    def ring_gather(self, ring, starts, S_win, out, n_ant=None, stream=None):
+        """buffer_rx_t ring (float32 [N_ant, ring_len, 2], sample t at t % ring_len) -> windows
+        out float32 [n, n_ant, S_win, 2] starting at the global times `starts` (rx_pacer wrap copy)."""
+        import torch
+        n_ant = n_ant or ring.shape[0]
+        self._check_ring(ring, n_ant)
+        st = np.ascontiguousarray(np.asarray(starts, dtype=np.int64))
+        n = len(st)
+        _check_tensor(out, "out", torch.float32, 4, int(self.cfg.device))
+        if out.shape[0] < n or out.shape[1] != n_ant or out.shape[2] != S_win or out.shape[3] != 2:
+            raise ValueError(f"out shape {tuple(out.shape)}, expected [>={n}, {n_ant}, {S_win}, 2]")
+        _chk(lib().dnrp_ring_gather(self._ctx, C.c_void_p(ring.data_ptr()), ring.shape[1], ring.shape[1], n_ant, n,
+                                    C.c_void_p(st.ctypes.data), S_win, C.c_void_p(out.data_ptr()), _stream_ptr(stream)),
+             "dnrp_ring_gather")
+
+    def sync_stream_init(self, sc):
+        state = SyncStreamState()
+        _chk(lib().dnrp_sync_stream_init(self._ctx, C.byref(sc), C.byref(state)), "dnrp_sync_stream_init")
+        return state
+
+    def sync_stream_window(self, sc):
+        return int(lib().dnrp_sync_stream_window(self._ctx, C.byref(sc)))
+
+    def rx_sync_stream(self, sc, ring, t0, n_chunks, state, stream=None):
+        """Continuous-stream sync of n_chunks chunks from global time t0 over the ring; returns the
+        unique reports (SYNC_RESULT_DTYPE, global times) and the chunk each was found in."""
+        self._check_ring(ring, sc.N_ant_limited)
+        out = np.zeros(max(1, n_chunks * sc.max_reports), SYNC_RESULT_DTYPE)
+        chunk_of = np.zeros(max(1, n_chunks * sc.max_reports), np.uint32)
+        n_out = C.c_uint32()
+        _chk(lib().dnrp_rx_sync_stream(self._ctx, C.byref(sc), C.c_void_p(ring.data_ptr()), ring.shape[1],
+                                       ring.shape[1], int(t0), n_chunks, C.byref(state), C.c_void_p(out.ctypes.data),
+                                       C.byref(n_out), C.c_void_p(chunk_of.ctypes.data), _stream_ptr(stream)),
+             "dnrp_rx_sync_stream")
+        return out[: n_out.value], chunk_of[: n_out.value]
 
     def kernel_time_total(self, name, reset=True):
         ms, cnt = C.c_float(), C.c_uint32()

@@ -237,6 +237,47 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
 
 int dnrp_sync(dnrp_ctx* ctx, void* stream);
 
+/*
+ * Ring-buffer window gather <- rx_pacer_t's wrap copy (rx_pacer.cpp:106-143) over the per-antenna
+ * ring of radio::buffer_rx_t (radio/buffer_rx.hpp:46-141; sample of global time t at index
+ * t % ring_len). Copies window w = global samples [start[w], start[w] + S_win) of antennas
+ * 0..N_ant-1 into out [n][N_ant][S_win] cf32 (device), ready for dnrp_rx_sync_batch or the RX.
+ *   ring   device cf32, antenna a at ring + 2*a*ant_stride floats (ant_stride >= ring_len)
+ *   start  host [n], >= 0; S_win <= ring_len (one wrap at most); n * N_ant <= 65535
+ */
+int dnrp_ring_gather(dnrp_ctx* ctx, const float* ring, uint64_t ring_len, uint64_t ant_stride, uint32_t N_ant,
+                     uint32_t n, const int64_t* start, uint32_t S_win, float* out, void* stream);
+
+/* Continuous-stream synchronisation state = baton_t's uniqueness state (baton.cpp:37-52,157-169):
+ * the latest unique fine peak time and the minimum distance to it (worker_pool.cpp:299-321) */
+typedef struct {
+    int64_t sync_time_last;          /* global hw time of the latest unique packet */
+    int64_t sync_time_unique_limit;  /* one STF pattern at b * os_min (..._UNIQUE_LIMIT_IN_STF_PATTERNS_DP) */
+    uint64_t packets, not_unique;    /* worker_sync_t stats: job_packet, job_packet_not_unique */
+} dnrp_sync_stream_state;
+
+int dnrp_sync_stream_init(const dnrp_ctx* ctx, const dnrp_sync_cfg* sc, dnrp_sync_stream_state* state);
+
+/* hw samples one chunk's search reads from the ring: chunk_len plus the detection overlap into the
+ * next chunk, the coarse-peak and cross-correlation spans and the resampler filter (sync_chunk.cpp:
+ * 32-123); 0 on a bad argument. Must be <= the ring length. */
+uint32_t dnrp_sync_stream_window(const dnrp_ctx* ctx, const dnrp_sync_cfg* sc);
+
+/*
+ * Continuous-stream synchronisation <- the sync worker pool (worker_sync_t::work,
+ * worker_sync.cpp:57-221) over n_chunks consecutive chunks of sc->chunk_len hw samples starting at
+ * global time t0: every chunk's window is gathered from the ring, searched with
+ * sync_chunk_t::search() (up to sc->max_reports packets per chunk), its reports converted to global
+ * time (coarse_peak_time / fine_peak_time, sync_chunk.cpp:213-245) and passed through the baton's
+ * double-detection filter in chunk order (baton.cpp:157-169: unique iff fine_peak_time - last >
+ * limit). out (host, n_chunks * max_reports) receives the unique reports in time order, n_out their
+ * count, chunk_of (host, optional) the chunk each was found in. Blocking: returns after the stream's
+ * work has completed. Call again with t0 advanced by n_chunks * chunk_len to continue the stream.
+ */
+int dnrp_rx_sync_stream(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, const float* ring, uint64_t ring_len,
+                        uint64_t ant_stride, int64_t t0, uint32_t n_chunks, dnrp_sync_stream_state* state,
+                        dnrp_sync_result* out, uint32_t* n_out, uint32_t* chunk_of, void* stream);
+
 /* sp3::radio_device_class_t (sections_part3/radio_device_class.hpp): the capabilities of a device
  * class string such as "8.16.8.A"; a worker pool sizes itself from them (dnrp_cfg.u_max = u_min,
  * b_max = b_min, N_TX_max = N_TX_min, as worker_pool_config_t does). Host only. DNRP_ECONFIG for a
