@@ -181,6 +181,9 @@ struct dnrp_ctx {
     // ring-buffer gather / continuous-stream synchronisation (stream.cpp)
     dbuf ring_start, ring_win;
     pinned st_ring, st_stream;
+    // simulated channel (channel.cpp): per-call link realisations
+    dbuf chan_tab;
+    pinned st_chan;
     // timing: HIP events recorded on the caller's stream around every launch (DNRP_TIMING=1)
     bool timing = false;
     struct ev_pool {

@@ -192,6 +192,30 @@ struct ring_args {
 };
 hipError_t launch_ring_gather(const ring_args& a, uint32_t n, hipStream_t st);
 
+// ---- simulated wireless channel (channel.hip): simulation/wireless channel_{awgn,flat,doubly}
+enum : uint32_t { CH_AWGN = 0, CH_FLAT = 1, CH_DOUBLY = 2 };
+struct channel_tap {
+    int32_t delay;  // samples (link_t::set_pdp)
+    float amp;      // sqrt(p_i) / sqrt(N_sin), as link.cpp:280-283 scales
+};
+struct channel_sin {
+    int64_t period;     // samples per Doppler cycle, signed (INT64_MAX inside the dead band)
+    double phase_rev;   // initial phase / 2 pi
+};
+struct channel_args {
+    uint32_t kind, N_TX, N_RX, S_tx, S_rx, n_taps, n_sin;
+    const float2* tx;        // [n][N_TX][S_tx]
+    float2* rx;              // [n][N_RX][S_rx]
+    const int64_t* offset;   // [n] TX sample 0 lands at RX sample offset
+    const int64_t* t0;       // [n] global time of RX sample 0 (Doppler phases)
+    const float2* coef;      // flat: [n][N_RX][N_TX]
+    const channel_tap* taps; // doubly: [n][N_RX][N_TX][n_taps]
+    const channel_sin* sins; // doubly: [n][N_RX][N_TX][n_taps][n_sin]
+    float large_scale, sigma;
+    uint64_t seed;
+};
+hipError_t launch_channel(const channel_args& a, uint32_t n, hipStream_t st);
+
 // ---- synchronisation (sync.hip): sync_chunk_t::search() per window, reports in search order
 struct sync_res {  // layout of dnrp_sync_result (include/dnrp.h)
     uint32_t found, det_ant;

@@ -148,11 +148,24 @@ class SyncStreamState(C.Structure):
                 ("not_unique", C.c_uint64)]
 
 
+CH_AWGN, CH_FLAT, CH_DOUBLY = 0, 1, 2
+CH_NOISELESS_DB = 1000.0
+CH_N_SIN = 40  # WIRELESS_CHANNEL_DOUBLY_NOF_SINUSOIDS (link.hpp:126)
+
+
+class ChannelCfg(C.Structure):
+    """dnrp_channel_cfg: simulated wireless channel (simulation/wireless channel_{awgn,flat,doubly})."""
+    _fields_ = [("kind", C.c_uint32), ("pdp_idx", C.c_uint32), ("tau_rms_ns", C.c_float), ("fD_Hz", C.c_float),
+                ("samp_rate", C.c_uint32), ("large_scale", C.c_float), ("snr_db", C.c_float),
+                ("net_bw_norm", C.c_float), ("seed", C.c_uint64)]
+
+
 EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_get_packet_sizes",
            "dnrp_compute_packet_sizes", "dnrp_tx_batch", "dnrp_rx_sync_batch",
            "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_kernel_time_total",
            "dnrp_strerror", "dnrp_get_radio_device_class", "dnrp_query_param", "dnrp_param_name",
-           "dnrp_ring_gather", "dnrp_sync_stream_init", "dnrp_sync_stream_window", "dnrp_rx_sync_stream"]
+           "dnrp_ring_gather", "dnrp_sync_stream_init", "dnrp_sync_stream_window", "dnrp_rx_sync_stream",
+           "dnrp_channel_batch", "dnrp_channel_realization"]
 
 _lib = None
 
@@ -179,6 +192,10 @@ def lib():
                                         C.POINTER(PdcReport), P]
         L.dnrp_sync.argtypes = [P, P]
         L.dnrp_ring_gather.argtypes = [P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P, C.c_uint32, P, P]
+        L.dnrp_channel_batch.argtypes = [P, C.POINTER(ChannelCfg), C.c_uint32, C.c_uint32, P, C.c_uint32, C.c_uint32, P, P,
+                                         P, C.c_uint32, P]
+        L.dnrp_channel_realization.argtypes = [C.POINTER(ChannelCfg), C.c_uint32, C.c_uint32, C.c_uint32,
+                                               C.POINTER(C.c_uint32), P, P, P, P, P]
         L.dnrp_sync_stream_init.argtypes = [P, C.POINTER(SyncCfg), C.POINTER(SyncStreamState)]
         L.dnrp_sync_stream_window.argtypes = [P, C.POINTER(SyncCfg)]
         L.dnrp_sync_stream_window.restype = C.c_uint32
@@ -213,6 +230,27 @@ def compute_packet_sizes(ps, u_max=None, b_max=None, os_min=1, L=10, M=9):
     if rc != 0:
         raise DnrpError(rc, "dnrp_compute_packet_sizes")
     return out.as_dict()
+
+
+def channel_realization(cfg, window, n_tx, n_rx):
+    """Host-only: window `window`'s link realisation of a ChannelCfg (dnrp_channel_realization):
+    dict with delay / amp [n_rx, n_tx, taps], period / phase_rev [n_rx, n_tx, taps, 40], coef [n_rx, n_tx]."""
+    nt = C.c_uint32()
+    _chk(lib().dnrp_channel_realization(C.byref(cfg), window, n_tx, n_rx, C.byref(nt), None, None, None, None, None),
+         "dnrp_channel_realization")
+    t = max(1, nt.value)
+    delay = np.zeros((n_rx, n_tx, t), np.int32)
+    amp = np.zeros((n_rx, n_tx, t), np.float32)
+    period = np.zeros((n_rx, n_tx, t, CH_N_SIN), np.int64)
+    phase = np.zeros((n_rx, n_tx, t, CH_N_SIN), np.float64)
+    coef = np.zeros((n_rx, n_tx, 2), np.float32)
+    _chk(lib().dnrp_channel_realization(C.byref(cfg), window, n_tx, n_rx, C.byref(nt), C.c_void_p(delay.ctypes.data),
+                                        C.c_void_p(amp.ctypes.data), C.c_void_p(period.ctypes.data),
+                                        C.c_void_p(phase.ctypes.data), C.c_void_p(coef.ctypes.data)),
+         "dnrp_channel_realization")
+    k = nt.value
+    return {"delay": delay[..., :k], "amp": amp[..., :k], "period": period[:, :, :k], "phase_rev": phase[:, :, :k],
+            "coef": coef[..., 0] + 1j * coef[..., 1]}
 
 
 def _check_tensor(t, what, dtype, ndim, device):
@@ -384,6 +422,22 @@ class Phy:
         _chk(lib().dnrp_ring_gather(self._ctx, C.c_void_p(ring.data_ptr()), ring.shape[1], ring.shape[1], n_ant, n,
                                     C.c_void_p(st.ctypes.data), S_win, C.c_void_p(out.data_ptr()), _stream_ptr(stream)),
              "dnrp_ring_gather")
+
+    def channel_batch(self, cfg, tx, offsets, t0s, rx, stream=None):
+        """Simulated channel: tx float32 [n, N_TX, S_tx, 2] -> rx float32 [n, N_RX, S_rx, 2] (device);
+        offsets / t0s: per window, TX sample 0 at RX sample offset, global time of RX sample 0."""
+        import torch
+        dev = int(self.cfg.device)
+        _check_tensor(tx, "tx", torch.float32, 4, dev)
+        _check_tensor(rx, "rx", torch.float32, 4, dev)
+        off = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+        t0 = np.ascontiguousarray(np.asarray(t0s, dtype=np.int64))
+        n = len(off)
+        if len(t0) != n or tx.shape[0] < n or rx.shape[0] < n or tx.shape[3] != 2 or rx.shape[3] != 2:
+            raise ValueError("channel_batch: window counts / shapes disagree")
+        _chk(lib().dnrp_channel_batch(self._ctx, C.byref(cfg), n, tx.shape[1], C.c_void_p(tx.data_ptr()), tx.shape[2],
+                                      rx.shape[1], C.c_void_p(off.ctypes.data), C.c_void_p(t0.ctypes.data),
+                                      C.c_void_p(rx.data_ptr()), rx.shape[2], _stream_ptr(stream)), "dnrp_channel_batch")
 
     def sync_stream_init(self, sc):
         state = SyncStreamState()

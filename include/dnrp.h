@@ -278,6 +278,46 @@ int dnrp_rx_sync_stream(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, const float* rin
                         uint64_t ant_stride, int64_t t0, uint32_t n_chunks, dnrp_sync_stream_state* state,
                         dnrp_sync_result* out, uint32_t* n_out, uint32_t* chunk_of, void* stream);
 
+/*
+ * Simulated wireless channel <- the virtual space links of the reference's simulator
+ * (lib/src/simulation/wireless/channel_awgn.cpp, channel_flat.cpp, channel_doubly.cpp + link.cpp;
+ * noise: lib/src/simulation/hardware/noise.cpp). Applies N_TX x N_RX links to n TX windows:
+ *   awgn    every TX antenna superimposed onto every RX antenna (large-scale factor only)
+ *   flat    one Rayleigh coefficient per link and window
+ *   doubly  tapped delay line per link: a 3GPP power delay profile (link.hpp:88-108, pdp_idx 0..2 =
+ *           EPA / EVA / ETU) scaled to tau_rms_ns, 40 Doppler sinusoids per tap (Jakes, fD_Hz)
+ * then complex AWGN with n0 = -10 log10(net_bw_norm) - snr_db dB (per unit signal power in the net
+ * bandwidth; snr_db >= DNRP_CH_NOISELESS_DB: none). Link realisations are drawn per window from the
+ * seed (window index within the call); dnrp_channel_realization returns them (host only).
+ *   tx      device [n][N_TX][S_tx] cf32; rx device [n][N_RX][S_rx] cf32 (every sample written)
+ *   offset  host [n]: TX sample 0 lands at RX sample offset[w] (zero input outside [0, S_tx))
+ *   t0      host [n]: global hw time of RX sample 0 (phases of the Doppler sinusoids)
+ */
+#define DNRP_CH_AWGN 0
+#define DNRP_CH_FLAT 1
+#define DNRP_CH_DOUBLY 2
+#define DNRP_CH_NOISELESS_DB 1000.0f
+typedef struct {
+    uint32_t kind;          /* DNRP_CH_* */
+    uint32_t pdp_idx;       /* doubly: power delay profile 0..2 */
+    float tau_rms_ns;       /* doubly: delay spread, <= 2000 */
+    float fD_Hz;            /* doubly: maximum Doppler, <= 2000 */
+    uint32_t samp_rate;     /* hw sample rate in S/s (tap delays, Doppler periods) */
+    float large_scale;      /* amplitude factor of every link (path loss / RX sensitivity) */
+    float snr_db;           /* noise level, see above */
+    float net_bw_norm;      /* N_b_OCC / N_b_DFT_os scaled to the hw rate (noise.cpp net_bandwidth_norm) */
+    uint64_t seed;
+} dnrp_channel_cfg;
+
+int dnrp_channel_batch(dnrp_ctx* ctx, const dnrp_channel_cfg* cfg, uint32_t n, uint32_t N_TX, const float* tx,
+                       uint32_t S_tx, uint32_t N_RX, const int64_t* offset, const int64_t* t0, float* rx, uint32_t S_rx,
+                       void* stream);
+/* Host only: window w's realisation. n_taps receives the taps per link (doubly); arrays (optional)
+ * are [N_RX][N_TX][n_taps] delay (samples) / amp, [N_RX][N_TX][n_taps][40] period / phase_rev
+ * (initial phase in revolutions), [N_RX][N_TX][2] coef (flat). */
+int dnrp_channel_realization(const dnrp_channel_cfg* cfg, uint32_t window, uint32_t N_TX, uint32_t N_RX, uint32_t* n_taps,
+                             int32_t* delay, float* amp, int64_t* period, double* phase_rev, float* coef);
+
 /* sp3::radio_device_class_t (sections_part3/radio_device_class.hpp): the capabilities of a device
  * class string such as "8.16.8.A"; a worker pool sizes itself from them (dnrp_cfg.u_max = u_min,
  * b_max = b_min, N_TX_max = N_TX_min, as worker_pool_config_t does). Host only. DNRP_ECONFIG for a
