@@ -165,7 +165,8 @@ EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_g
            "dnrp_rx_pcc_batch", "dnrp_rx_pdc_batch", "dnrp_sync", "dnrp_last_kernel_ms", "dnrp_kernel_time_total",
            "dnrp_strerror", "dnrp_get_radio_device_class", "dnrp_query_param", "dnrp_param_name",
            "dnrp_ring_gather", "dnrp_sync_stream_init", "dnrp_sync_stream_window", "dnrp_rx_sync_stream",
-           "dnrp_channel_batch", "dnrp_channel_realization"]
+           "dnrp_channel_batch", "dnrp_channel_realization", "dnrp_tx_transmit_length", "dnrp_tx_packet_json",
+           "dnrp_rx_packet_json"]
 
 _lib = None
 
@@ -196,6 +197,11 @@ def lib():
                                          P, C.c_uint32, P]
         L.dnrp_channel_realization.argtypes = [C.POINTER(ChannelCfg), C.c_uint32, C.c_uint32, C.c_uint32,
                                                C.POINTER(C.c_uint32), P, P, P, P, P]
+        L.dnrp_tx_transmit_length.argtypes = [C.POINTER(Cfg), C.POINTER(PsDef), C.c_uint32, C.POINTER(C.c_uint32)]
+        L.dnrp_tx_packet_json.argtypes = [C.POINTER(Cfg), C.POINTER(PsDef), C.POINTER(TxDesc), C.c_uint32, C.c_uint64,
+                                          C.c_int64, P, P, P, C.c_uint32, C.c_char_p]
+        L.dnrp_rx_packet_json.argtypes = [C.POINTER(Cfg), C.c_uint32, P, C.c_uint32, C.POINTER(PccReport),
+                                          C.POINTER(PdcReport), C.c_char_p]
         L.dnrp_sync_stream_init.argtypes = [P, C.POINTER(SyncCfg), C.POINTER(SyncStreamState)]
         L.dnrp_sync_stream_window.argtypes = [P, C.POINTER(SyncCfg)]
         L.dnrp_sync_stream_window.restype = C.c_uint32
@@ -251,6 +257,40 @@ def channel_realization(cfg, window, n_tx, n_rx):
     k = nt.value
     return {"delay": delay[..., :k], "amp": amp[..., :k], "period": period[:, :, :k], "phase_rev": phase[:, :, :k],
             "coef": coef[..., 0] + 1j * coef[..., 1]}
+
+
+def _host_cfg(u_max, b_max, n_ant, os_min=1, L=10, M=9):
+    return Cfg(u_max, b_max, n_ant, os_min, L, M, 1, 2, 1, 0)
+
+
+def tx_transmit_length(ps, GI_percentage, u_max, b_max, os_min=1, L=10, M=9):
+    """Host-only: N_samples_transmit_os_rs (tx.cpp:555-566) of a packet configuration."""
+    out = C.c_uint32()
+    _chk(lib().dnrp_tx_transmit_length(C.byref(_host_cfg(u_max, b_max, 1, os_min, L, M)), C.byref(ps), GI_percentage,
+                                       C.byref(out)), "dnrp_tx_transmit_length")
+    return int(out.value)
+
+
+def tx_packet_json(path, ps, desc, pcc_d, pdc_d, iq, u_max, b_max, n_tx, os_min=1, L=10, M=9, rv=0, tx_order_id=0,
+                   tx_time_64=0):
+    """Host-only: tx_t::write_all_data_to_json of one packet. pcc_d / pdc_d uint8 (packed d-bits),
+    iq complex64 [N_TX, S] (a host copy of the dnrp_tx_batch output row)."""
+    pcc = np.ascontiguousarray(pcc_d, np.uint8)
+    pdc = np.ascontiguousarray(pdc_d, np.uint8)
+    x = np.ascontiguousarray(iq, np.complex64)
+    _chk(lib().dnrp_tx_packet_json(C.byref(_host_cfg(u_max, b_max, n_tx, os_min, L, M)), C.byref(ps), C.byref(desc), rv,
+                                   tx_order_id, tx_time_64, C.c_void_p(pcc.ctypes.data), C.c_void_p(pdc.ctypes.data),
+                                   C.c_void_p(x.ctypes.data), x.shape[1], str(path).encode()), "dnrp_tx_packet_json")
+
+
+def rx_packet_json(path, sync_result, u_max, b_max, n_ant, mcs_index, pcc_report=None, pdc_report=None, os_min=1, L=10,
+                   M=9, worker_id=0):
+    """Host-only: the RADIO/PHY part of worker_tx_rx_t::collect_and_write_json for one packet."""
+    r = np.ascontiguousarray(np.asarray(sync_result, dtype=SYNC_RESULT_DTYPE).reshape(1))
+    _chk(lib().dnrp_rx_packet_json(C.byref(_host_cfg(u_max, b_max, n_ant, os_min, L, M)), worker_id,
+                                   C.c_void_p(r.ctypes.data), mcs_index, C.byref(pcc_report) if pcc_report else None,
+                                   C.byref(pdc_report) if pdc_report else None, str(path).encode()),
+         "dnrp_rx_packet_json")
 
 
 def _check_tensor(t, what, dtype, ndim, device):

@@ -318,6 +318,25 @@ int dnrp_channel_batch(dnrp_ctx* ctx, const dnrp_channel_cfg* cfg, uint32_t n, u
 int dnrp_channel_realization(const dnrp_channel_cfg* cfg, uint32_t window, uint32_t N_TX, uint32_t N_RX, uint32_t* n_taps,
                              int32_t* delay, float* amp, int64_t* period, double* phase_rev, float* coef);
 
+/* Host only. N_samples_transmit_os_rs: the samples a radio buffer holds once the packet is complete
+ * (packet without GI + GI_percentage % of the GI, tx.cpp:555-566) = the final value of the
+ * reference's progressive buffer_tx_t::set_tx_length_samples_cnt (tx.cpp:241,277,292). dnrp_tx_batch
+ * completes every buffer before its stream work completes; samples past this length are zero. */
+int dnrp_tx_transmit_length(const dnrp_cfg* cfg, const dnrp_psdef* psdef, uint32_t GI_percentage, uint32_t* len);
+
+/* Host only: JSON export in the reference's formats.
+ *   dnrp_tx_packet_json <- tx_t::write_all_data_to_json (tx.cpp:316-427): packet definition, TX
+ *     meta, d-bits of PCC and PDC (PLCF / TB fields empty: they sit above the FEC), the antenna
+ *     streams (host copy of dnrp_tx_batch's iq_out row, [N_TX][S] cf32) up to the transmit length,
+ *     resampler parameters.
+ *   dnrp_rx_packet_json <- worker_tx_rx_t::collect_and_write_json's RADIO/PHY part
+ *     (worker_tx_rx.cpp:354-396; rx_synced's channel estimates are not exported). */
+int dnrp_tx_packet_json(const dnrp_cfg* cfg, const dnrp_psdef* psdef, const dnrp_tx_desc* desc, uint32_t rv,
+                        uint64_t tx_order_id, int64_t tx_time_64, const uint8_t* pcc_d, const uint8_t* pdc_d,
+                        const float* iq, uint32_t S, const char* path);
+int dnrp_rx_packet_json(const dnrp_cfg* cfg, uint32_t worker_id, const dnrp_sync_result* sr, uint32_t mcs_index,
+                        const dnrp_pcc_report* pcc, const dnrp_pdc_report* pdc, const char* path);
+
 /* sp3::radio_device_class_t (sections_part3/radio_device_class.hpp): the capabilities of a device
  * class string such as "8.16.8.A"; a worker pool sizes itself from them (dnrp_cfg.u_max = u_min,
  * b_max = b_min, N_TX_max = N_TX_min, as worker_pool_config_t does). Host only. DNRP_ECONFIG for a
