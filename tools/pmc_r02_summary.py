@@ -20,8 +20,9 @@ for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), rec
         cnt[k].add((f, r["Dispatch_Id"]))
 lines = []
 for k, c in sorted(agg.items()):
-    n_disp = max(1, len({d for _, d in cnt[k]}) // max(1, len({f for f, _ in cnt[k]})))
-    w = c.get("SQ_WAVES", 0) / 2 or 1  # SQ_WAVES is collected in both SQ passes
+    per_file = collections.Counter(f for f, _ in cnt[k])  # dispatches of this kernel in each pass
+    n_disp = max(1, max(per_file.values()))
+    w = c.get("SQ_WAVES", 0) / 2 or 1  # SQ_WAVES is collected in both SQ passes (all dispatches)
     per_wave = " ".join(f"{n}={v / w:.0f}" for n, v in sorted(c.items())
                         if n.startswith("SQ_") and n != "SQ_WAVES")
     fetch = 2 * c.get("FETCH_SIZE", 0) * 1024 / 1e9 / n_disp

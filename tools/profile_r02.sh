@@ -17,6 +17,11 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_
   timeout -k 10 240 rocprofv3 --pmc $set --output-format csv -d $out/p$i -o run -- python3 bench.py $args > $out/p$i.log 2>&1
 done
 python3 tools/pmc_r02_summary.py $out > $out/summary.txt
-rm -f $out/trace/run_kernel_trace.csv
+# FETCH_SIZE / WRITE_SIZE per launch -> traffic.json (tools/traffic_summary.py layout)
+mkdir -p $out/pmc_fetch $out/pmc_write
+mv $(find $out/p3 -name "*counter_collection.csv" | head -1) $out/pmc_fetch/run_counter_collection.csv
+mv $(find $out/p4 -name "*counter_collection.csv" | head -1) $out/pmc_write/run_counter_collection.csv
+python3 tools/traffic_summary.py $out $out > $out/traffic.txt
+rm -f $out/trace/run_kernel_trace.csv $out/pmc_fetch/*.csv $out/pmc_write/*.csv
 rm -rf $out/p1 $out/p2 $out/p3 $out/p4
 cat $out/summary.txt
