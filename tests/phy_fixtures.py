@@ -42,6 +42,20 @@ PARITY_CASES = {
 }
 
 
+# TX-only parity configurations: transmission modes the reference RX cannot demodulate (spatial
+# multiplexing, N_SS > 1: rx_synced.cpp:1331-1333) or that the RX here declines (N_eff_TX = 8,
+# DESIGN.md §7) -- their TX (tx.cpp:1004-1116 N_SS streams, transmit_diversity_precoding.cpp modulo
+# 12 pairs, beamforming_and_antenna_port_mapping.cpp 8-antenna W) still has a parity gate.
+TX_ONLY_CASES = {
+    "tm2_sm2": ((2, 2, 1, 2, 2, 4), (2, 2, 2, 1, 10, 9), 1, (), 0),
+    "tm6_sm4": ((1, 4, 1, 2, 6, 3), (1, 4, 4, 1, 10, 9), 1, (), 0),
+    "tm9_sm4_cb": ((1, 2, 1, 2, 9, 2), (1, 2, 4, 1, 10, 9), 1, (), 1),
+    "tm10_txdiv8": ((1, 2, 1, 2, 10, 4), (1, 2, 8, 1, 10, 9), 1, (), 0),
+    "tm10_u8b16": ((8, 16, 1, 1, 10, 8), (8, 16, 8, 1, 10, 9), 1, (), 0),
+    "tm11_sm8": ((1, 4, 1, 1, 11, 2), (1, 4, 8, 1, 10, 9), 1, (), 0),
+}
+
+
 def random_bits(rng, n_bits):
     return rng.integers(0, 2, n_bits, dtype=np.uint8)
 

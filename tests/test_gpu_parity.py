@@ -26,11 +26,12 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 CASES = F.PARITY_CASES
+TX_CASES = {**F.PARITY_CASES, **F.TX_ONLY_CASES}
 
 
 def _ctx(name, max_batch=8):
     import dnrp
-    ps, cf, lr, _, _ = CASES[name]
+    ps, cf, lr, _, _ = TX_CASES[name]
     u_max, b_max, ntx, os_min, L, M = cf
     phy = dnrp.Phy(u_max, b_max, ntx, os_min, L, M, chestim_mode_lr=bool(lr), max_batch=max_batch)
     for nid in range(100, 106):
@@ -68,12 +69,12 @@ def _check_tx(iq_gpu, ref, sz, S, n_tx_ref, tag):
     assert n_tx_ref == keep + (S - keep) * 5 // 100
 
 
-@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("name", sorted(TX_CASES))
 def test_tx_parity(name):
     import dnrp
     rng = np.random.default_rng(0xDEC7)
     phy, ps, ops, ocf = _ctx(name)
-    cb = CASES[name][4]
+    cb = TX_CASES[name][4]
     sz = phy.packet_sizes(ps)
     S = sz["N_samples_packet_os_rs"]
     n = 3
