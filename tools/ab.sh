@@ -6,7 +6,6 @@ for v in "$@"; do
   python3 - "$v" <<'PY'
 import json, sys
 d = json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1])
-n = d['steps'] * d['config']['slots_per_gpu_per_step'] // d['config']['chunk']
-print(sys.argv[1], d['value'], {k: round(v / n, 2) for k, v in d['kernels_ms_total'].items()}, 'ber', round(d['check']['pdc_hard_ber'], 6))
+print(sys.argv[1], d['value'], {k: round(v, 2) for k, v in d['kernel_ms_per_chunk'].items()}, 'ber', round(d['check']['pdc_hard_ber'], 6))
 PY
 done

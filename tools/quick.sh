@@ -8,6 +8,5 @@ timeout -k 10 200 python bench.py --steps 3 --no-cpu-baseline "$@" > gpurun_out/
 python3 - <<'PY'
 import json
 d = json.loads(open('gpurun_out/bench.log').read().strip().splitlines()[-1])
-n = d['steps'] * d['config']['slots_per_gpu_per_step'] // d['config']['chunk']
-print(d['value'], {k: round(v / n, 2) for k, v in d['kernels_ms_total'].items()}, d['check'])
+print(d['value'], {k: round(v, 2) for k, v in d['kernel_ms_per_chunk'].items()}, d['check'])
 PY
