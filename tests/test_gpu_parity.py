@@ -246,6 +246,21 @@ def test_rx_pdc_request_errors():
     assert e.value.code == -6
 
 
+def test_rx_tm10_unsupported():
+    """N_eff_TX = 8 (device class 8.16.8.A): the reference receiver aborts on its l-mode LUT at the
+    TS 4-7 DRS symbol; the boundary returns DNRP_EUNSUPPORTED instead of output."""
+    import dnrp
+    phy = dnrp.Phy(8, 16, 8, 1, 10, 9, max_batch=2)
+    ps = dnrp.psdef(8, 16, 1, 1, 10, 8)
+    S = phy.packet_sizes(ps)["N_samples_packet_os_rs"]
+    dev = torch.device("cuda:0")
+    iq = torch.zeros((1, 8, S, 2), dtype=torch.float32, device=dev)
+    pcc_llr = torch.zeros((1, 196), dtype=torch.int16, device=dev)
+    with pytest.raises(dnrp.DnrpError) as e:
+        phy.rx_pcc_batch([dnrp.SyncReport(0, 0.0, 0.0, 8, 16, 8)], iq, pcc_llr)
+    assert e.value.code == -3
+
+
 def test_rx_negative_fine_peak():
     """A sync report whose packet starts before the window (fine_peak_time < 0): the samples before
     the window read as zero history, never memory before the window row."""
