@@ -233,6 +233,14 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
     return r;
 }
 
+// OFDM symbol of every PCC cell (rx_cells_kernel reads the symbol per cell in both phases)
+std::vector<uint16_t> pcc_cell_symbols(const geo::maps_t& m) {
+    std::vector<uint16_t> sym(m.pcc_k.size());
+    for (size_t s = 0; s + 1 < m.pcc_sym_off.size(); ++s)
+        for (uint32_t j = m.pcc_sym_off[s]; j < m.pcc_sym_off[s + 1]; ++j) sym[j] = static_cast<uint16_t>(m.pcc_l[s]);
+    return sym;
+}
+
 rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, int* err) {
     const auto key = std::make_tuple(u, b, N_eff_TX);
     auto it = ctx->rx1t.find(key);
@@ -270,6 +278,7 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
     const auto plan = geo::build_rx_plan(t->maps, pcc_ops, N_eff_TX);
     bool ok = t->stf.upload(stfv) && t->tw.upload(twiddles(t->Nd)) && t->taps.upload(t->rs.h) && t->taps_pp.upload(taps_polyphase(t->rs, &t->npp)) &&
               t->drs_k.upload(t->maps.drs_k) && t->drs_v.upload(t->maps.drs_v) && t->pcc_k.upload(t->maps.pcc_k) &&
+              t->pcc_sym.upload(pcc_cell_symbols(t->maps)) &&
               t->bplan.upload(plan);
     const uint32_t Nsv = N_eff_TX <= 2 ? 5 : 10;
     for (uint32_t mode = 0; mode < 2 && ok; ++mode)
@@ -277,13 +286,16 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
             const auto L = geo::build_lut(mode ? Nsv : 0, b, c.b_max, c.u_max, p);
             ok = t->lut_pw[mode][p].upload(L.pilot_weight) && t->lut_w[mode][p].upload(L.weights);
             t->lut_n[mode][p] = L.n;
+            t->lut_nw[mode][p] = static_cast<uint32_t>(L.weights.size());
+            t->wcap[mode] = std::max(t->wcap[mode], t->lut_nw[mode][p]);
             ok = ok && L.n < (1u << 15);  // eq_work packs the tap count into 15 bits
             t->lut_T[mode] = L.T;
         }
     std::vector<dev::rx_lut> luts(6);
     for (uint32_t mode = 0; mode < 2; ++mode)
         for (uint32_t p = 0; p < 3; ++p)
-            luts[mode * 3 + p] = {t->lut_pw[mode][p].as<uint32_t>(), t->lut_w[mode][p].as<float>(), t->lut_n[mode][p], 0};
+            luts[mode * 3 + p] = {t->lut_pw[mode][p].as<uint32_t>(), t->lut_w[mode][p].as<float>(), t->lut_n[mode][p],
+                                  t->lut_nw[mode][p]};
     if (!ok || !t->luts.upload(luts)) {
         *err = DNRP_ENOMEM;
         return nullptr;
@@ -411,10 +423,10 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, con
 
 // back-end launches of one phase: SNR chain, then cells (rx_back.hip)
 int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t n, const uint32_t* sel, bool pdc,
-                uint32_t N_bps, const uint32_t* kk, const uint16_t* pdc_sym, int16_t* llr, uint32_t llr_stride,
+                uint32_t N_bps, const uint32_t* kk, const uint16_t* cell_sym, int16_t* llr, uint32_t llr_stride,
                 hipStream_t st) {
     const char* name = pdc ? "rx_pdc" : "rx_pcc";
-    if (plan.n_dops > dev::RX_MAX_DOPS) return DNRP_EUNSUPPORTED;
+    if (plan.n_dops > dev::RX_MAX_DOPS || !plan.cells_ok) return DNRP_EUNSUPPORTED;
     if (!ctx->lut_d.ensure(size_t(ctx->cfg.max_batch) * dev::RX_MAX_DOPS)) return DNRP_ENOMEM;
     dev::rx_snr_args s{};
     s.N_RX = ctx->cfg.N_TX_max;
@@ -442,6 +454,8 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     c.n_dops = plan.n_dops;
     c.n_epochs = plan.n_epochs;
     c.N_bps = N_bps;
+    c.wcap[0] = t->wcap[0];
+    c.wcap[1] = t->wcap[1];
     fill_pairs(t->N_eff_TX, c.pair, c.mod);
     c.is_pdc = pdc;
     c.epochs = plan.epochs.as<dev::rx_epoch>();
@@ -451,7 +465,7 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     c.drs_k = s.drs_k;
     c.drs_v = s.drs_v;
     c.kk = kk;
-    c.pdc_sym = pdc_sym;
+    c.cell_sym = cell_sym;
     c.luts = t->luts.as<dev::rx_lut>();
     c.Y = s.Y;
     c.lut_d = s.lut_d;
@@ -779,7 +793,7 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         ctx->tic("rx_fft_pcc", st);
         if (dev::launch_rx_fft(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
         ctx->toc("rx_fft_pcc", st);
-        if ((err = launch_back(ctx, t, t->bplan, ng, gsel, false, 2, t->pcc_k.as<uint32_t>(), nullptr, pcc_llr, 196,
+        if ((err = launch_back(ctx, t, t->bplan, ng, gsel, false, 2, t->pcc_k.as<uint32_t>(), t->pcc_sym.as<uint16_t>(), pcc_llr, 196,
                                st)) != DNRP_OK)
             return err;
     }

@@ -101,12 +101,17 @@ struct tx_tables {
 // device copy of a geo::rx_plan_t
 struct rx_plan_dev {
     uint32_t n_dops = 0, n_epochs = 0;
+    bool cells_ok = true;  // every epoch fits rx_cells_kernel: <= CELL_MAX_SEGS segments, one DRS count
     dbuf dl, dmeta, segs, epochs;
     bool upload(const geo::rx_plan_t& p) {
         static_assert(sizeof(geo::rx_seg_t) == sizeof(dev::rx_seg), "rx_seg layout");
         static_assert(sizeof(geo::rx_epoch_t) == sizeof(dev::rx_epoch), "rx_epoch layout");
         n_dops = static_cast<uint32_t>(p.dl.size());
         n_epochs = static_cast<uint32_t>(p.epochs.size());
+        for (const auto& e : p.epochs) {
+            cells_ok = cells_ok && e.seg1 - e.seg0 <= dev::CELL_MAX_SEGS;
+            for (uint32_t i = e.seg0; i < e.seg1; ++i) cells_ok = cells_ok && p.segs[i].drs_cnt == p.segs[e.seg0].drs_cnt;
+        }
         return dl.upload(p.dl) && dmeta.upload(p.dmeta) && segs.upload(p.segs) && epochs.upload(p.epochs);
     }
 };
@@ -117,11 +122,12 @@ struct rx1_tables {  // per (u, b, N_eff_TX): STF/PCC phase
     geo::resampler_t rs;
     geo::maps_t maps;
     uint32_t pcc_max = 0;
-    dbuf stf, tw, taps, taps_pp, drs_k, drs_v, pcc_k;
+    dbuf stf, tw, taps, taps_pp, drs_k, drs_v, pcc_k, pcc_sym;
     uint32_t npp = 0;  // floats in taps_pp
     rx_plan_dev bplan;  // PCC phase back end
     dbuf lut_pw[2][3], lut_w[2][3], luts;
-    uint32_t lut_n[2][3] = {}, lut_T[2] = {};
+    uint32_t lut_n[2][3] = {}, lut_nw[2][3] = {}, lut_T[2] = {};
+    uint32_t wcap[2] = {};  // largest weight table of mode l / lr (rx_cells_kernel LDS slots)
 };
 
 struct rx2_tables {  // per (psdef): PDC phase

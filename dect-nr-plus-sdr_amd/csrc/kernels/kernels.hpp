@@ -140,11 +140,12 @@ hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st);
 struct rx_lut {             // one Wiener LUT: [T][4][Nf] pilot | weight << 16, weights [n_vec][n]
     const uint32_t* pw;
     const float* w;
-    uint32_t n, pad;
+    uint32_t n, nw;         // taps per weight vector, floats in w (n_vec n)
 };
 
 struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epoch)
     uint32_t N_occ, N_RX, NT, Nf_pad, n_sym_total, n_drs, n_dops, n_epochs, N_bps, mod, is_pdc;
+    uint32_t wcap[2];          // floats of the LDS weight-table slot of mode l / lr (largest such table)
     uint32_t pair[12];
     const rx_epoch* epochs;
     const rx_seg* segs;
@@ -153,7 +154,7 @@ struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epo
     const uint32_t* drs_k;
     const float* drs_v;
     const uint32_t* kk;        // pcc_k (PCC phase) or pdc_k (PDC phase)
-    const uint16_t* pdc_sym;   // per PDC cell: OFDM symbol
+    const uint16_t* cell_sym;  // per PCC (PCC phase) / PDC cell: OFDM symbol
     const rx_lut* luts;        // [mode l / lr][profile] (device table: no dynamic kernel-argument indexing)
     const float2* Y;
     const uint8_t* lut_d;
@@ -164,6 +165,32 @@ struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epo
     const uint32_t* sel;            // launch packet -> slot / output row
 };
 hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st);
+
+// rx_cells_kernel's per-workgroup LDS staging (rx_back.hip, rx_eq.hpp).
+// The epoch's pilot buffer zfi: one row per (rx, ts) of 2 nd interlaced pilots plus ZFI_PAD zeros.
+// The pad puts the rows of different streams on different LDS banks (a wave's lanes alternate between
+// the streams of consecutive SFBC pairs) and lets a union window run past a row's last pilot.
+constexpr uint32_t ZFI_PAD = 8;
+constexpr uint32_t CELL_MAX_SEGS = 64;  // segments per epoch (host-checked, rx_plan_dev)
+__host__ __device__ constexpr uint32_t zfi_stride(uint32_t n_drs) { return 2 * n_drs + ZFI_PAD; }
+
+// An epoch segment with the packet's Wiener LUT resolved: the LUT row block of the segment's
+// processing-stage symbol and its weight table's slot in LDS
+struct cell_seg {
+    uint32_t u0, j0, l;
+    uint32_t info;       // mode | swap << 1 | off << 4 | nI << 12
+    const uint32_t* pw;  // LT.pw + rel * 4 * Nf
+    uint32_t wbase, pad;
+};
+
+// LDS bytes of one rx_cells workgroup: pilot buffer, the weight-table slots of mode l and lr,
+// segments, SFBC pairs
+__host__ __device__ constexpr size_t cell_lds_bytes(uint32_t N_RX, uint32_t NT, uint32_t n_drs, uint32_t wcap_l,
+                                                    uint32_t wcap_lr) {
+    return size_t(N_RX) * NT * zfi_stride(n_drs) * 8 + size_t(wcap_l + wcap_lr) * 4 + CELL_MAX_SEGS * sizeof(cell_seg) +
+           16 * 4;
+}
+
 
 struct rx_mimo_args {  // estimator_mimo_t::process_drs at the packet end, one wavefront per packet
     uint32_t N_RX, N_TS, Nf_pad, n_sym_total;

@@ -124,48 +124,71 @@ constexpr uint32_t CELL_THREADS = 512;
 
 template <int NRX, int NT>
 __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A) {
-    extern __shared__ __attribute__((aligned(16))) float2 zfi[];  // [NRX][NT][2 nd]
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const uint32_t zst = zfi_stride(A.n_drs);
+    float2* zfi = smem;                                                       // [NRX][NT][zst]
+    float* wtab = reinterpret_cast<float*>(zfi + NRX * NT * zst);            // slots: mode l, mode lr
+    cell_seg* sg = reinterpret_cast<cell_seg*>(wtab + A.wcap[0] + A.wcap[1]);  // CELL_MAX_SEGS
+    uint32_t* pairs = reinterpret_cast<uint32_t*>(sg + CELL_MAX_SEGS);       // 12
     const uint32_t pl = blockIdx.x / A.n_epochs, ep = blockIdx.x % A.n_epochs;
     const uint32_t pkt = rx_slot_of(A.sel, pl), row = rx_row_of(A.sel, pl);
-    const rx_epoch E = A.epochs[ep];
-    const uint32_t nd2 = 2 * A.n_drs;
+    const rx_epoch* E = A.epochs + ep;
+    const uint32_t units = E->units, seg0 = E->seg0, nseg = E->seg1 - E->seg0;
     const float2* Yp = A.Y + size_t(pkt) * NRX * A.n_sym_total * A.Nf_pad;
-    build_pilots<NRX, NT>(A, A.epochs + ep, Yp, zfi, threadIdx.x, CELL_THREADS);
+    const uint32_t tid = threadIdx.x;
+    // the epoch's segments share one DRS count (host-checked), so one LUT profile: weight table
+    // slot m holds the profile's table of mode m (l / lr)
+    const uint8_t* lutp = A.lut_d + size_t(pkt) * RX_MAX_DOPS;
+    const uint32_t dc = nseg ? A.segs[seg0].drs_cnt : 0u;
+    const uint32_t prof = dc ? lutp[dc - 1] : 0u;
+    if (units) {
+#pragma unroll
+        for (uint32_t m = 0; m < 2; ++m) {
+            const rx_lut LT = A.luts[m * 3 + prof];
+            for (uint32_t i = tid; i < LT.nw; i += CELL_THREADS) wtab[m * A.wcap[0] + i] = LT.w[i];
+        }
+        if (tid < nseg) {
+            const rx_seg S = A.segs[seg0 + tid];
+            const rx_lut LT = A.luts[S.mode * 3 + prof];
+            cell_seg c;
+            c.u0 = S.u0;
+            c.j0 = S.j0;
+            c.l = S.l;
+            c.info = (S.mode & 1u) | (S.swap & 3u) << 1 | (S.off & 0xFFu) << 4 | LT.n << 12;
+            c.pw = LT.pw + size_t(S.rel) * 4 * (A.N_occ + 1);
+            c.wbase = (S.mode & 1u) * A.wcap[0];
+            c.pad = 0;
+            sg[tid] = c;
+        }
+        if (tid < 12) pairs[tid] = A.pair[tid];
+    }
+    build_pilots<NRX, NT>(A, E, Yp, zfi, tid, CELL_THREADS);
     __syncthreads();
+    if (tid >= units) return;
     const uint8_t* __restrict__ seq = A.is_pdc ? A.pdc_seq[row] : A.pcc_seq;
     int16_t* __restrict__ llr = A.llr + size_t(row) * A.llr_stride;
-    const uint8_t* lutp = A.lut_d + size_t(pkt) * RX_MAX_DOPS;
-    if (E.units == 0) return;
-    // software pipeline over the thread's units: the index loads (segment, kk, LUT pilot | weight
-    // indices) of unit u + CELL_THREADS are in flight while unit u is equalised
-    uint32_t si = E.seg0;
-    uint32_t seg_end = si + 1 < E.seg1 ? A.segs[si + 1].u0 : E.units;
-    auto gather = [&](uint32_t u, eq_work<NT>& w) {
-        while (u >= seg_end) {
-            ++si;
-            seg_end = si + 1 < E.seg1 ? A.segs[si + 1].u0 : E.units;
-        }
-        const rx_seg S = A.segs[si];
-        const uint32_t lut = S.drs_cnt ? lutp[S.drs_cnt - 1] : 0u;
-        const uint32_t jj = S.j0 + (NT == 1 ? 1u : 2u) * (u - S.u0);
-        const uint32_t l = A.is_pdc ? static_cast<uint32_t>(A.pdc_sym[jj]) : S.l;
-        eq_gather<NT>(A, S, lut, jj, l * A.Nf_pad, w);
-    };
-    uint32_t u = threadIdx.x;
-    if (u >= E.units) return;
-    eq_work<NT> cur;
-    gather(u, cur);
-    for (; u < E.units; u += CELL_THREADS) {
-        eq_work<NT> nxt;
-        const bool more = u + CELL_THREADS < E.units;
-        if (more) gather(u + CELL_THREADS, nxt);
-        eq_finish<NRX, NT>(A, cur, Yp, zfi, nd2, seq, llr);
-        if (more) cur = nxt;
+    constexpr uint32_t per_unit = NT == 1 ? 1u : 2u;
+    // stage A two units ahead, stage B one unit ahead of eq_compute (rx_eq.hpp)
+    uint32_t si = 0;
+    unit_a na;
+    unit_b<NRX, NT> cur;
+    uint32_t u = tid;
+    unit_stage_a(A, sg, nseg, si, u, per_unit, na);
+    unit_stage_b<NRX, NT>(A, sg, pairs, Yp, seq, na, cur);
+    if (u + CELL_THREADS < units) unit_stage_a(A, sg, nseg, si, u + CELL_THREADS, per_unit, na);
+    for (; u < units; u += CELL_THREADS) {
+        unit_b<NRX, NT> nb;
+        const bool m1 = u + CELL_THREADS < units, m2 = u + 2 * CELL_THREADS < units;
+        if (m1) unit_stage_b<NRX, NT>(A, sg, pairs, Yp, seq, na, nb);
+        if (m2) unit_stage_a(A, sg, nseg, si, u + 2 * CELL_THREADS, per_unit, na);
+        eq_compute<NRX, NT>(A, sg, zfi, wtab, zst, cur, llr);
+        if (m1) cur = nb;
     }
 }
 
 hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st) {
-    const size_t lds = size_t(a.N_RX) * a.NT * 2 * a.n_drs * sizeof(float2);
+    const size_t lds = cell_lds_bytes(a.N_RX, a.NT, a.n_drs, a.wcap[0], a.wcap[1]);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
     const dim3 g(n * a.n_epochs), b(CELL_THREADS);
 #define DNRP_CELLS(R, T)                                                                 \
     if (a.N_RX == R && a.NT == T) {                                                      \

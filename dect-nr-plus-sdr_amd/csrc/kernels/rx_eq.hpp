@@ -57,19 +57,82 @@ __device__ __forceinline__ void demap(float2 y, uint32_t N_bps, float* L) {
     }
 }
 
-// demap + descramble + int16 of cell j (LLRs j*N_bps .. j*N_bps+N_bps-1)
-__device__ __forceinline__ void emit_cell(float2 x, uint32_t j, uint32_t N_bps, const uint8_t* __restrict__ seq,
+// Unit pipeline (one unit: cell jj for MRC, NT == 1, or the SFBC pair jj, jj+1): stage A resolves the
+// segment (LDS) and loads the subcarrier indices and symbol; stage B loads the LUT pilot | weight
+// words, the received cells of every RX antenna and the unit's scrambling bits; eq_compute works from
+// registers and LDS only. The kernel keeps stage A two units ahead and stage B one unit ahead.
+struct unit_a {
+    uint32_t si, jj, k0, k1, l;
+};
+template <int NRX, int NT>
+struct unit_b {
+    static constexpr int NC = NT == 1 ? 1 : 4;  // interpolated channels per unit
+    uint32_t si, jj, tab;                       // tab: tA | tB << 4
+    uint32_t pw[NC];
+    uint32_t sb[3];                             // scrambling bytes from bit (jj N_bps) & ~7 (raw loads)
+    float2 r0[NRX], r1[NT == 1 ? 1 : NRX];
+};
+
+__device__ __forceinline__ void unit_stage_a(const rx_cells_args& A, const cell_seg* sg, uint32_t nseg, uint32_t& si,
+                                             uint32_t u, uint32_t per_unit, unit_a& a) {
+    while (si + 1 < nseg && u >= sg[si + 1].u0) ++si;
+    a.si = si;
+    a.jj = sg[si].j0 + per_unit * (u - sg[si].u0);
+    a.k0 = A.kk[a.jj];
+    a.k1 = per_unit == 2 ? A.kk[a.jj + 1] : a.k0;
+    a.l = A.cell_sym[a.jj];
+}
+
+template <int NRX, int NT>
+__device__ __forceinline__ void unit_stage_b(const rx_cells_args& A, const cell_seg* sg, const uint32_t* pairs,
+                                             const float2* __restrict__ Yp, const uint8_t* __restrict__ seq,
+                                             const unit_a& a, unit_b<NRX, NT>& b) {
+    const uint32_t Nf = A.N_occ + 1;
+    const cell_seg& S = sg[a.si];
+    const uint32_t swap = (S.info >> 1) & 3u;
+    b.si = a.si;
+    b.jj = a.jj;
+    if constexpr (NT == 1) {
+        b.tab = 0;
+        b.pw[0] = S.pw[swap * Nf + a.k0];
+    } else {
+        const uint32_t pr = pairs[(a.jj >> 1) % A.mod];
+        const uint32_t tA = pr & 0xFu, tB = pr >> 4;
+        b.tab = tA | tB << 4;
+        b.pw[0] = S.pw[((tA & 3u) ^ swap) * Nf + a.k0];
+        b.pw[1] = S.pw[((tA & 3u) ^ swap) * Nf + a.k1];
+        b.pw[2] = S.pw[((tB & 3u) ^ swap) * Nf + a.k0];
+        b.pw[3] = S.pw[((tB & 3u) ^ swap) * Nf + a.k1];
+    }
+    const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
+    const uint32_t yoff = a.l * A.Nf_pad;
+#pragma unroll
+    for (int r = 0; r < NRX; ++r) {
+        b.r0[r] = Yp[r * ast + yoff + a.k0];
+        if constexpr (NT > 1) b.r1[r] = Yp[r * ast + yoff + a.k1];
+    }
+    // the unit's scrambling bits [jj N_bps, (jj + cells) N_bps) lie in at most 3 bytes
+    // (loads clamped to the last byte and kept raw: nothing here waits on the loads in flight)
+    const uint32_t b0 = (a.jj * A.N_bps) >> 3, bl = ((a.jj + (NT == 1 ? 1u : 2u)) * A.N_bps - 1) >> 3;
+    b.sb[0] = seq[b0];
+    b.sb[1] = seq[min(b0 + 1, bl)];
+    b.sb[2] = seq[min(b0 + 2, bl)];
+}
+
+// demap + descramble + int16 of cell j (LLRs j*N_bps .. j*N_bps+N_bps-1); bits: the scrambling bytes
+// from bit (j0 N_bps) & ~7 of the unit's first cell j0
+__device__ __forceinline__ void emit_cell(float2 x, uint32_t j, uint32_t j0, uint32_t N_bps, uint32_t bits,
                                           int16_t* __restrict__ llr) {
     float L[8];
     demap(x, N_bps, L);
-    const uint32_t base = j * N_bps;
-    if (N_bps == 8) {  // one scrambling byte, one 16-B store
-        const uint32_t sb = seq[j];
+    const uint32_t base = j * N_bps, r0 = base - ((j0 * N_bps) & ~7u);  // bit offset in `bits`
+    auto sbit = [&](uint32_t i) { const uint32_t r = r0 + i; return (bits >> (8 * (r >> 3) + 7 - (r & 7u))) & 1u; };
+    if (N_bps == 8) {  // one 16-B store
         uint32_t w[4];
 #pragma unroll
         for (int b = 0; b < 8; b += 2) {
-            const float v0 = ((sb >> (7 - b)) & 1u) ? -L[b] : L[b];
-            const float v1 = ((sb >> (6 - b)) & 1u) ? -L[b + 1] : L[b + 1];
+            const float v0 = sbit(b) ? -L[b] : L[b];
+            const float v1 = sbit(b + 1) ? -L[b + 1] : L[b + 1];
             w[b / 2] = static_cast<uint16_t>(q16(v0)) | (static_cast<uint32_t>(static_cast<uint16_t>(q16(v1))) << 16);
         }
         int16_t* dst = llr + base;
@@ -85,190 +148,156 @@ __device__ __forceinline__ void emit_cell(float2 x, uint32_t j, uint32_t N_bps, 
         return;
     }
 #pragma unroll
-    for (uint32_t b = 0; b < 8; ++b) {
-        if (b < N_bps) {
-            const uint32_t i = base + b;
-            const uint32_t sbit = (seq[i >> 3] >> (7u - (i & 7u))) & 1u;
-            llr[i] = q16(sbit ? -L[b] : L[b]);
-        }
-    }
+    for (uint32_t b = 0; b < 8; ++b)
+        if (b < N_bps) llr[base + b] = q16(sbit(b) ? -L[b] : L[b]);
 }
 
-#ifndef CELL_WCHUNK_DEF
-#define CELL_WCHUNK_DEF 4
-#endif
-constexpr uint32_t CELL_WCHUNK = CELL_WCHUNK_DEF;  // interpolation taps per weight-load batch
-
-// One work unit: cell jj (MRC, NT == 1) or the SFBC pair jj, jj+1 (NT > 1) under segment S's
-// interpolation event, in two steps so a caller can take the dependent index loads of one unit off
-// the critical path of another: eq_gather resolves the unit's segment, subcarrier indices and LUT
-// pilot | weight indices (kk -> pw), eq_finish loads the received cells of every RX antenna together
-// with the interpolation weights, reads the epoch's pilot buffer zfi [NRX][NT][2 nd], interpolates,
-// combines, demaps and stores. lut: the Wiener LUT profile picked after the segment's last DRS.
-template <int NT>
-struct eq_work {
-    static constexpr int NC = NT == 1 ? 1 : 4;  // interpolated channels per unit
-    uint32_t jj, k0, k1, yoff;
-    uint32_t meta;  // mode | tA << 1 | tB << 5 | off << 9 | nI << 17
-    const float* wt;
-    uint32_t pw[NC];
-};
-
-__device__ __forceinline__ uint32_t eq_meta_mode(uint32_t m) { return m & 1u; }
-__device__ __forceinline__ uint32_t eq_meta_tA(uint32_t m) { return (m >> 1) & 0xFu; }
-__device__ __forceinline__ uint32_t eq_meta_tB(uint32_t m) { return (m >> 5) & 0xFu; }
-__device__ __forceinline__ uint32_t eq_meta_off(uint32_t m) { return (m >> 9) & 0xFFu; }
-__device__ __forceinline__ uint32_t eq_meta_nI(uint32_t m) { return m >> 17; }
-
-// yoff: offset of the unit's symbol row in the packet's Y block (antenna 0)
-template <int NT>
-__device__ __forceinline__ void eq_gather(const rx_cells_args& A, const rx_seg& S, uint32_t lut, uint32_t jj, uint32_t yoff,
-                                          eq_work<NT>& w) {
-    const uint32_t Nf = A.N_occ + 1;
-    const rx_lut LT = A.luts[S.mode * 3 + lut];
-    const uint32_t* __restrict__ pwt = LT.pw + size_t(S.rel) * 4 * Nf;
-    w.jj = jj;
-    w.yoff = yoff;
-    w.wt = LT.w;
-    uint32_t tA = 0, tB = 0;
-    if constexpr (NT == 1) {
-        w.k0 = w.k1 = A.kk[jj];
-        w.pw[0] = pwt[(0u ^ S.swap) * Nf + w.k0];
-    } else {
-        w.k0 = A.kk[jj];
-        w.k1 = A.kk[jj + 1];
-        const uint32_t pr = A.pair[(jj >> 1) % A.mod];
-        tA = pr & 0xFu;
-        tB = pr >> 4;
-        w.pw[0] = pwt[((tA & 3u) ^ S.swap) * Nf + w.k0];
-        w.pw[1] = pwt[((tA & 3u) ^ S.swap) * Nf + w.k1];
-        w.pw[2] = pwt[((tB & 3u) ^ S.swap) * Nf + w.k0];
-        w.pw[3] = pwt[((tB & 3u) ^ S.swap) * Nf + w.k1];
-    }
-    w.meta = (S.mode & 1u) | tA << 1 | tB << 5 | (S.off & 0xFFu) << 9 | LT.n << 17;
-}
-
-// Y: the packet's received cells [NRX][n_sym_total][Nf_pad]
+// Wiener interpolation (rx_synced.cpp:893-949), MRC (1204-1306) or SFBC combining (1335-1392),
+// demapping and the LLR store of one unit. zfi: the epoch's pilot rows [NRX][NT][zst]; wtab: the
+// weight-table slots.
 template <int NRX, int NT>
-__device__ __forceinline__ void eq_finish(const rx_cells_args& A, const eq_work<NT>& W, const float2* __restrict__ Y,
-                                          const float2* zfi, uint32_t nd2, const uint8_t* __restrict__ seq,
-                                          int16_t* __restrict__ llr) {
-    constexpr int NC = eq_work<NT>::NC;
-    const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
-    float2 r0[NRX], r1[NT == 1 ? 1 : NRX];
-#pragma unroll
-    for (int a = 0; a < NRX; ++a) {
-        r0[a] = Y[a * ast + W.yoff + W.k0];
-        if constexpr (NT > 1) r1[a] = Y[a * ast + W.yoff + W.k1];
-    }
-    const uint32_t mode = eq_meta_mode(W.meta), off = eq_meta_off(W.meta), nI = eq_meta_nI(W.meta);
+__device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_seg* sg, const float2* zfi,
+                                           const float* wtab, uint32_t zst, const unit_b<NRX, NT>& b,
+                                           int16_t* __restrict__ llr) {
+    constexpr int NC = unit_b<NRX, NT>::NC;
+    const uint32_t b0 = (b.jj * A.N_bps) >> 3, bl = ((b.jj + (NT == 1 ? 1u : 2u)) * A.N_bps - 1) >> 3;
+    const uint32_t bits = b.sb[0] | (b0 + 1 <= bl ? b.sb[1] << 8 : 0u) | (b0 + 2 <= bl ? b.sb[2] << 16 : 0u);
+    const uint32_t info = sg[b.si].info, wbase = sg[b.si].wbase;
+    const uint32_t mode = info & 1u, off = (info >> 4) & 0xFFu, nI = info >> 12;
     const uint32_t step = mode ? 1u : 2u;
-    // interpolation weights and pilot start of channel c (stream tA / tB at k0 / k1)
-    const float* w[NC];
-    uint32_t pos[NC];
+    uint32_t pos[NC], wo[NC];  // pilot start (LDS float2 index) and weight offset (LDS float index)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        const uint32_t t = c < 2 ? eq_meta_tA(W.meta) : eq_meta_tB(W.meta);
-        w[c] = W.wt + size_t(W.pw[c] >> 16) * nI;
-        uint32_t p = W.pw[c] & 0xFFFFu;
+        const uint32_t t = c < 2 ? (b.tab & 0xFu) : (b.tab >> 4);
+        uint32_t p = b.pw[c] & 0xFFFFu;
         if (!mode) p = 2 * p + ((off >> t) & 1u);  // non-interlaced: latest DRS symbol only
-        pos[c] = p + t * nd2;
-    }
-    float2 h[NRX][NC];
-#pragma unroll
-    for (int a = 0; a < NRX; ++a)
-#pragma unroll
-        for (int c = 0; c < NC; ++c) h[a][c] = make_float2(0.f, 0.f);
-    // weights in chunks of CELL_WCHUNK taps: all of a chunk's (global / L1) weight loads are in
-    // flight together instead of one dependent load per tap
-    for (uint32_t i0 = 0; i0 < nI; i0 += CELL_WCHUNK) {
-        float wc[NC][CELL_WCHUNK];
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-#pragma unroll
-            for (uint32_t ii = 0; ii < CELL_WCHUNK; ++ii) wc[c][ii] = i0 + ii < nI ? w[c][i0 + ii] : 0.f;
-#pragma unroll
-        for (uint32_t ii = 0; ii < CELL_WCHUNK; ++ii) {
-            if (i0 + ii >= nI) break;
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const uint32_t p = pos[c] + (i0 + ii) * step;
-#pragma unroll
-                for (int a = 0; a < NRX; ++a) {
-                    const float2 z = zfi[a * NT * nd2 + p];
-                    h[a][c].x = fmaf(z.x, wc[c][ii], h[a][c].x);
-                    h[a][c].y = fmaf(z.y, wc[c][ii], h[a][c].y);
-                }
-            }
-        }
+        pos[c] = p + t * zst;
+        wo[c] = wbase + (b.pw[c] >> 16) * nI;
     }
     if constexpr (NT == 1) {
+        float2 h[NRX];
+#pragma unroll
+        for (int a = 0; a < NRX; ++a) h[a] = make_float2(0.f, 0.f);
+        for (uint32_t i = 0; i < nI; ++i) {
+            const float wv = wtab[wo[0] + i];
+            const uint32_t p = pos[0] + i * step;
+#pragma unroll
+            for (int a = 0; a < NRX; ++a) {
+                const float2 z = zfi[a * NT * zst + p];
+                h[a].x = fmaf(z.x, wv, h[a].x);
+                h[a].y = fmaf(z.y, wv, h[a].y);
+            }
+        }
         float2 num = make_float2(0.f, 0.f);
         float den = 0.f;
 #pragma unroll
         for (int a = 0; a < NRX; ++a) {  // MRC (rx_synced.cpp:1204-1306)
-            num = cadd(num, cmulc(r0[a], h[a][0]));
-            den += cnorm(h[a][0]);
+            num = cadd(num, cmulc(b.r0[a], h[a]));
+            den += cnorm(h[a]);
         }
-        emit_cell(cscale(num, 1.0f / den), W.jj, A.N_bps, seq, llr);
+        emit_cell(cscale(num, 1.0f / den), b.jj, b.jj, A.N_bps, bits, llr);
     } else {
+        // SFBC: a stream's pair channel is the mean of its interpolations at k0 and k1
+        // (rx_synced.cpp:1365-1371). Both read the stream's pilot row with windows sh pilots apart
+        // (0 or 1 almost everywhere): one pass over the union window of nI + sh taps with the mean
+        // weights gives the mean with about half the pilot reads and FMAs of two passes.
+        uint32_t base[2], sh[2], wl[2], wh[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const bool up = pos[2 * s + 1] >= pos[2 * s];
+            base[s] = up ? pos[2 * s] : pos[2 * s + 1];
+            sh[s] = (up ? pos[2 * s + 1] - pos[2 * s] : pos[2 * s] - pos[2 * s + 1]) / step;
+            wl[s] = up ? wo[2 * s] : wo[2 * s + 1];
+            wh[s] = up ? wo[2 * s + 1] : wo[2 * s];
+        }
+        const uint32_t ntap = nI + max(sh[0], sh[1]);
+        float2 g[NRX][2];
+#pragma unroll
+        for (int a = 0; a < NRX; ++a) g[a][0] = g[a][1] = make_float2(0.f, 0.f);
+        for (uint32_t i = 0; i < ntap; ++i) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const float lo = i < nI ? wtab[wl[s] + i] : 0.f;
+                const float hi = i >= sh[s] && i - sh[s] < nI ? wtab[wh[s] + i - sh[s]] : 0.f;
+                const float wv = 0.5f * (lo + hi);
+                // past this stream's union window: weight 0, the read stays in the row + ZFI_PAD
+                const uint32_t p = base[s] + min(i, nI + sh[s]) * step;
+#pragma unroll
+                for (int a = 0; a < NRX; ++a) {
+                    const float2 z = zfi[a * NT * zst + p];
+                    g[a][s].x = fmaf(z.x, wv, g[a][s].x);
+                    g[a][s].y = fmaf(z.y, wv, g[a][s].y);
+                }
+            }
+        }
         float2 n0 = make_float2(0.f, 0.f), n1 = make_float2(0.f, 0.f);
         float den = 0.f;
 #pragma unroll
-        for (int a = 0; a < NRX; ++a) {  // SFBC pair (rx_synced.cpp:1335-1392)
-            const float2 h0 = cscale(cadd(h[a][0], h[a][1]), 0.5f);
-            const float2 h1 = cscale(cadd(h[a][2], h[a][3]), 0.5f);
-            n0 = cadd(n0, cadd(cmul(cconj(h0), r0[a]), cmul(h1, cconj(r1[a]))));
-            n1 = cadd(n1, cadd(cmul(make_float2(-h1.x, -h1.y), cconj(r0[a])), cmul(cconj(h0), r1[a])));
+        for (int a = 0; a < NRX; ++a) {  // SFBC pair combining (rx_synced.cpp:1373-1391)
+            const float2 h0 = g[a][0], h1 = g[a][1];
+            n0 = cadd(n0, cadd(cmul(cconj(h0), b.r0[a]), cmul(h1, cconj(b.r1[a]))));
+            n1 = cadd(n1, cadd(cmul(make_float2(-h1.x, -h1.y), cconj(b.r0[a])), cmul(cconj(h0), b.r1[a])));
             den += cnorm(h0) + cnorm(h1);
         }
-        emit_cell(cscale(n0, 1.0f / den), W.jj, A.N_bps, seq, llr);
-        emit_cell(cscale(n1, 1.0f / den), W.jj + 1, A.N_bps, seq, llr);
+        emit_cell(cscale(n0, 1.0f / den), b.jj, b.jj, A.N_bps, bits, llr);
+        emit_cell(cscale(n1, 1.0f / den), b.jj + 1, b.jj, A.N_bps, bits, llr);
     }
 }
 
 // The epoch's pilot buffer: zero-forced DRS cells of every (rx, ts) at their interlace slots
 // (channel_antenna.hpp:38-63), read from the DRS symbols in Y. Whole workgroup, no barrier. The
 // source DRS op of every (ts, interlace slot), its parity and symbol are workgroup-uniform (scalar
-// loads); a thread then has the DRS cells of one pilot index i for every (rx, ts, slot) in flight
-// together: two dependent loads (drs_k -> Y) instead of a four-load chain per element.
+// loads); a thread loads the subcarrier indices of one pilot index for every (ts, slot) at once, then
+// the cells of every (rx, ts, slot): two memory round trips. Slots without a source read a valid
+// cell and store zero.
 template <int NRX, int NT>
 __device__ __forceinline__ void build_pilots(const rx_cells_args& A, const rx_epoch* E, const float2* Yp, float2* zfi,
                                              uint32_t tid, uint32_t nthreads) {
-    const uint32_t nd = A.n_drs, nd2 = 2 * nd;
+    const uint32_t nd = A.n_drs, zst = zfi_stride(nd);
     const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
-    uint32_t kb[NT][2], yo[NT][2];  // drs_k row base (~0: no source) and Y row offset
+    for (uint32_t e = tid; e < NRX * NT * ZFI_PAD; e += nthreads)
+        zfi[(e / ZFI_PAD) * zst + 2 * nd + e % ZFI_PAD] = make_float2(0.f, 0.f);
+    // sources of all (ts, slot) first, then their DRS ops (two scalar round trips); a slot without a
+    // source reads op 0 and is stored as zero
+    uint32_t src[NT][2], kb[NT][2], yo[NT][2];
+    bool ok[NT][2];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int o = 0; o < 2; ++o) src[t][o] = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(E->src[t][o]));
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int o = 0; o < 2; ++o) {
-            const uint32_t src = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(E->src[t][o]));
-            kb[t][o] = 0xFFFFFFFFu;
-            yo[t][o] = 0;
-            if (src != 0xFFFFu) {
-                const uint32_t par = (A.dmeta[src] >> 16) & 0xFFu;
-                kb[t][o] = (par * 4 + (t & 3u)) * nd;
-                yo[t][o] = A.dl[src] * A.Nf_pad;
-            }
+            ok[t][o] = src[t][o] != 0xFFFFu;
+            const uint32_t op = ok[t][o] ? src[t][o] : 0u;
+            const uint32_t par = A.n_dops ? (A.dmeta[op] >> 16) & 0xFFu : 0u, l = A.n_dops ? A.dl[op] : 0u;
+            kb[t][o] = ok[t][o] ? par * 4 + (t & 3u) : (t & 3u);
+            yo[t][o] = ok[t][o] ? l * A.Nf_pad : 0u;
         }
     for (uint32_t i = tid; i < nd; i += nthreads) {
+        uint32_t k[NT][2];
+        float dv[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            const float dv = A.drs_v[t * nd + i];
+            dv[t] = A.drs_v[t * nd + i];
 #pragma unroll
-            for (int o = 0; o < 2; ++o) {
-                float2 v[NRX];
-#pragma unroll
-                for (int a = 0; a < NRX; ++a) v[a] = make_float2(0.f, 0.f);
-                if (kb[t][o] != 0xFFFFFFFFu) {
-                    const uint32_t k = A.drs_k[kb[t][o] + i];
-#pragma unroll
-                    for (int a = 0; a < NRX; ++a) v[a] = cscale(Yp[a * ast + yo[t][o] + k], dv);
-                }
-#pragma unroll
-                for (int a = 0; a < NRX; ++a) zfi[(a * NT + t) * nd2 + 2 * i + o] = v[a];
-            }
+            for (int o = 0; o < 2; ++o) k[t][o] = A.drs_k[kb[t][o] * nd + i];
         }
+        float2 v[NT][2][NRX];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int o = 0; o < 2; ++o)
+#pragma unroll
+                for (int a = 0; a < NRX; ++a) v[t][o][a] = Yp[a * ast + yo[t][o] + k[t][o]];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int o = 0; o < 2; ++o)
+#pragma unroll
+                for (int a = 0; a < NRX; ++a)
+                    zfi[(a * NT + t) * zst + 2 * i + o] = ok[t][o] ? cscale(v[t][o][a], dv[t]) : make_float2(0.f, 0.f);
     }
 }
 
