@@ -393,7 +393,9 @@ struct det_eval {
 __device__ bool detect_eval(const sync_args& A, const float* __restrict__ P, const float2* __restrict__ Cs, uint32_t s,
                             det_eval& out) {
     const uint32_t np = 4 * A.n_pattern, nc = 4 * A.n_uw;
+    // unrolled so each batch of loads is in flight together; the sums keep the reference's order
     double pw = 0.0;
+#pragma unroll 8
     for (uint32_t i = 0; i < np; ++i) pw += P[s - (np - 1) + i];
     const double rms = sqrt(pw / static_cast<double>(A.stf_len));
     static_assert(prm::SYNC_RMS_FRONT_STEPS == 2 && prm::SYNC_RMS_BACK_STEPS == 2, "front/back register pairs");
@@ -402,6 +404,7 @@ __device__ bool detect_eval(const sync_args& A, const float* __restrict__ P, con
     const double front = static_cast<double>(P[s - (np - 1)]) + P[s];
     if (sqrt(back) * prm::SYNC_RMS_FRONT_TO_BACK_RATIO >= sqrt(front)) return false;
     double cr = 0.0, ci = 0.0;
+#pragma unroll 4
     for (uint32_t g = 0; g < A.n_uw; ++g) {
         double gr = 0.0, gi = 0.0;
         for (uint32_t j = 0; j < 4; ++j) {
