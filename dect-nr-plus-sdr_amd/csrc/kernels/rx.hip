@@ -72,22 +72,28 @@ __device__ __forceinline__ void extract_bins(const rx_front_args& A, const float
 }
 
 // ===================================================================== STF
+// float2 slots of rx_stf_kernel's input staging, which also holds the FFT's two Nd buffers
+__host__ __device__ inline uint32_t rx_stf_in(uint32_t n_stf, uint32_t Nd, uint32_t M, uint32_t L, uint32_t hl) {
+    const uint32_t n_in = (n_stf * M) / L + hl + 4;
+    return n_in > 2 * Nd ? n_in : 2 * Nd;
+}
+
 template <int HL>
 __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     __shared__ double red[16];
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x);
-    const uint32_t Nd = A.plan.N, N = A.N_occ, Nf = N + 1;
-    const uint32_t n_stf = A.STF_CP + Nd;
-    const uint32_t n_in_max = (n_stf * A.M) / A.L + A.hl + 4;
-    float2* sbuf = smem;                 // n_stf
-    float2* inbuf = sbuf + n_stf;        // n_in_max
-    float2* fa = inbuf + n_in_max;       // Nd
-    float2* fb = fa + Nd;                // Nd
-    float2* twl = fb + Nd;               // Nd
-    float2* Ys = twl + Nd;               // [N_RX][Nf]
-    float* taps = reinterpret_cast<float*>(Ys + A.N_RX * Nf);
-    for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) twl[i] = A.tw[i];
+    const uint32_t Nd = A.plan.N, N = A.N_occ;
+    const uint32_t n_stf = A.STF_CP + Nd, n = A.b * 14;  // n: STF cells per antenna
+    // LDS (rx_stf_lds): the FFT's two buffers alias the resampler's input staging (free once the
+    // STF is resampled), twiddles come through the L1, and only the STF cells of every antenna's
+    // spectrum are kept: three workgroups per CU instead of one
+    float2* sbuf = smem;                                    // n_stf
+    float2* inbuf = sbuf + n_stf;                           // rx_stf_in(...)
+    float2* fa = inbuf;                                     // Nd
+    float2* fb = inbuf + Nd;                                // Nd
+    float2* Ys = inbuf + rx_stf_in(n_stf, Nd, A.M, A.L, A.hl);  // [N_RX][n]: STF cells
+    float* taps = reinterpret_cast<float*>(Ys + A.N_RX * n);
     stage_copy<4>(taps, A.taps, (A.hl + 1) * A.L, threadIdx.x, blockDim.x);
     const rx_pkt_in in = A.pin[pkt];
     const uint32_t P = n_stf / A.n_pattern;
@@ -113,8 +119,8 @@ __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
         cs_im += block_sum(pi, red);
         for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) fa[i] = sbuf[A.STF_CP + i];
         __syncthreads();
-        const float2* F = fft_any<-1>(fa, fb, twl, A.plan);
-        for (uint32_t k = threadIdx.x; k < Nf; k += blockDim.x) extract_bins(A, F, &Ys[a * Nf + k], k);
+        const float2* F = fft_any<-1>(fa, fb, A.tw, A.plan);
+        for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) extract_bins(A, F, &Ys[a * n + w], w < n / 2 ? 4 * w : 4 * w + 4);
         __syncthreads();
     }
     for (uint32_t a = A.N_RX; a < 8; ++a) S.rms[a] = 0.f;
@@ -129,11 +135,10 @@ __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
     }
     S.cfo_fine = in.cfo_rad + delta;
     // STF zero-forcing and fractional STO (rx_synced.cpp:663-709, estimator_sto.cpp:124-146)
-    const uint32_t n = A.b * 14;
     auto rstf = [&](uint32_t w) { return w < n / 2 ? 4 * w : 4 * w + 4; };
     auto zf = [&](uint32_t a, uint32_t w, double inc) {
         const uint32_t r = rstf(w);
-        float2 y = Ys[a * Nf + r];
+        float2 y = Ys[a * n + w];
         if (inc != 0.0) y = cmul(y, phasor(-inc * static_cast<double>(N / 2) + inc * static_cast<double>(r)));
         const float2 s = A.stf[r];
         return make_float2((y.x * s.x + y.y * s.y) / cnorm(s), (y.y * s.x - y.x * s.y) / cnorm(s));
@@ -282,8 +287,8 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
 
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
     const uint32_t Nd = a.plan.N, n_stf = a.STF_CP + Nd;
-    const size_t lds = (n_stf + (n_stf * a.M) / a.L + a.hl + 4 + 3 * size_t(Nd) + size_t(a.N_RX) * (a.N_occ + 1)) *
-                           sizeof(float2) + (a.hl + 1) * a.L * sizeof(float);
+    const size_t lds = (n_stf + rx_stf_in(n_stf, Nd, a.M, a.L, a.hl) + size_t(a.N_RX) * a.b * 14) * sizeof(float2) +
+                       (a.hl + 1) * a.L * sizeof(float);
     DNRP_HL_DISPATCH(rx_stf_kernel, dim3(n), dim3(256), lds, st, a);
     return hipGetLastError();
 }

@@ -21,6 +21,7 @@ namespace dnrp::dev {
 
 // ===================================================================== SNR chain
 constexpr uint32_t SNR_THREADS = 256, MAX_DOPS = RX_MAX_DOPS;
+constexpr int SNR_ROUNDS = 4;  // DRS cells per (symbol, stream) <= 256 (b <= 16: 224)
 
 template <int NRX>
 __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
@@ -41,22 +42,36 @@ __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
         for (uint32_t t = tf; t <= tl; ++t) {
             const uint32_t* __restrict__ kb = A.drs_k + (par * 4 + (t & 3u)) * nd;
             const float* __restrict__ vv = A.drs_v + t * nd;
-            for (uint32_t i0 = 0; i0 < nd; i0 += 64) {
-                const uint32_t i = i0 + lane;
+            // all SNR_ROUNDS rounds' index loads, then all their cells, in flight together
+            uint32_t k[SNR_ROUNDS], k1[SNR_ROUNDS];
+            float w[SNR_ROUNDS], w1[SNR_ROUNDS];
+#pragma unroll
+            for (int r = 0; r < SNR_ROUNDS; ++r) {
+                const uint32_t i = 64 * r + lane;
                 const bool in = i < nd, nx = lane == 63 && i + 1 < nd;
-                const uint32_t k = in ? kb[i] : 0u, k1 = nx ? kb[i + 1] : 0u;
-                const float w = in ? vv[i] : 0.f, w1 = nx ? vv[i + 1] : 0.f;
-                float2 y[NRX], y1[NRX];
+                k[r] = in ? kb[i] : 0u;
+                k1[r] = nx ? kb[i + 1] : 0u;
+                w[r] = in ? vv[i] : 0.f;
+                w1[r] = nx ? vv[i + 1] : 0.f;
+            }
+            float2 y[SNR_ROUNDS][NRX], y1[SNR_ROUNDS][NRX];
+#pragma unroll
+            for (int r = 0; r < SNR_ROUNDS; ++r)
 #pragma unroll
                 for (int a = 0; a < NRX; ++a) {
-                    y[a] = in ? rows[a * ast + k] : make_float2(0.f, 0.f);
-                    y1[a] = nx ? rows[a * ast + k1] : make_float2(0.f, 0.f);
+                    y[r][a] = rows[a * ast + k[r]];
+                    y1[r][a] = rows[a * ast + k1[r]];
                 }
 #pragma unroll
+            for (int r = 0; r < SNR_ROUNDS; ++r) {
+                const uint32_t i = 64 * r + lane;
+                if (64 * r >= nd) break;
+                const bool in = i < nd;
+#pragma unroll
                 for (int a = 0; a < NRX; ++a) {
-                    const float2 v = cscale(y[a], w);
+                    const float2 v = cscale(y[r][a], w[r]);
                     float2 vn = make_float2(__shfl_down(v.x, 1), __shfl_down(v.y, 1));
-                    if (lane == 63) vn = cscale(y1[a], w1);
+                    if (lane == 63) vn = cscale(y1[r][a], w1[r]);
                     if (in) s1 += cnorm(v);
                     if (i + 1 < nd) s2 += cnorm(csub(v, vn));
                 }
@@ -108,7 +123,7 @@ __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
 }
 
 hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st) {
-    if (a.n_dops > MAX_DOPS) return hipErrorInvalidValue;
+    if (a.n_dops > MAX_DOPS || a.n_drs > 64 * SNR_ROUNDS) return hipErrorInvalidValue;
     switch (a.N_RX) {
         case 1: hipLaunchKernelGGL(rx_snr_kernel<1>, dim3(n), dim3(SNR_THREADS), 0, st, a); break;
         case 2: hipLaunchKernelGGL(rx_snr_kernel<2>, dim3(n), dim3(SNR_THREADS), 0, st, a); break;

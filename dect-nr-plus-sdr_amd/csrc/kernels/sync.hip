@@ -390,8 +390,9 @@ struct det_eval {
 // the push: power over the last 4*n_pattern step values, correlation over the last 4*(n_pattern-1)
 // with the cover pairwise products per group of 4; front = newest + oldest register, back = the
 // two after the oldest: movsum.hpp get_sum_front/get_sum_back with ptr at the oldest element)
-__device__ bool detect_eval(const sync_args& A, const float* __restrict__ P, const float2* __restrict__ Cs, uint32_t s,
-                            det_eval& out) {
+// P[i], Cs[i]: step values of step index i (global, or LDS copies addressed through offset pointers)
+__device__ __forceinline__ bool detect_eval(const sync_args& A, const float* __restrict__ P, const float2* __restrict__ Cs,
+                                            uint32_t s, det_eval& out) {
     const uint32_t np = 4 * A.n_pattern, nc = 4 * A.n_uw;
     // unrolled so each batch of loads is in flight together; the sums keep the reference's order
     double pw = 0.0;
@@ -650,17 +651,33 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
     const float* Pw = A.P + static_cast<size_t>(w) * A.n_ant * A.n_steps;
     const float2* Cw = A.Cs + static_cast<size_t>(w) * A.n_ant * A.n_steps;
     sync_res* out = A.res + static_cast<size_t>(w) * A.max_reports;
+    // detection staging (aliases the resampler stage, dead during detection): per antenna det_p
+    // powers and det_c correlations
+    const uint32_t np = 4 * A.n_pattern, nc = 4 * A.n_uw;
+    const uint32_t det_p = (SYNC_THREADS + np + 3) / 4 * 4, det_c = SYNC_THREADS + nc;
+    float2* dc = stage;
+    float* dp = reinterpret_cast<float*>(dc + A.n_ant * det_c);
     uint32_t nrep = 0, s_cur = 4, ignore = A.stf_len + A.pattern;
     while (nrep < A.max_reports) {
         // ---------------- detection: first step at or after s_cur meeting the conditions
         if (threadIdx.x == 0) s_min = 0x7FFFFFFF;
         __syncthreads();
         for (uint32_t base = s_cur; base < A.n_steps; base += blockDim.x) {
+            // the batch's step values of every antenna in LDS (one coalesced round trip); steps a
+            // detection can evaluate have s - (np - 1) >= 0 (ignore >= stf_len + pattern)
+            const uint32_t nb = min(blockDim.x, A.n_steps - base);
+            const uint32_t lo_p = base >= np - 1 ? base - (np - 1) : 0u, lo_c = base >= nc - 1 ? base - (nc - 1) : 0u;
+            const uint32_t len_p = base + nb - lo_p, len_c = base + nb - lo_c;
+            for (uint32_t a = 0; a < A.n_ant; ++a) {
+                for (uint32_t i = threadIdx.x; i < len_p; i += blockDim.x) dp[a * det_p + i] = Pw[a * A.n_steps + lo_p + i];
+                for (uint32_t i = threadIdx.x; i < len_c; i += blockDim.x) dc[a * det_c + i] = Cw[a * A.n_steps + lo_c + i];
+            }
+            __syncthreads();
             const uint32_t s = base + threadIdx.x;
             if (s < A.n_steps && (s + 1) * A.step >= ignore) {
                 for (uint32_t a = 0; a < A.n_ant; ++a) {
                     det_eval e;
-                    if (detect_eval(A, Pw + a * A.n_steps, Cw + a * A.n_steps, s, e)) {
+                    if (detect_eval(A, dp + a * det_p - lo_p, dc + a * det_c - lo_c, s, e)) {
                         atomicMin(&s_min, static_cast<int>(s));
                         break;
                     }
@@ -871,7 +888,9 @@ size_t sync_detect_lds(const sync_args& a) {
     const size_t lb = (region + 1) / 2 * 2 * sizeof(float2);
     const size_t stage = sync_stage_cap(a.L, a.M, a.hl, region) * sizeof(float2);
     const size_t alias = ((region + 15) / 16 + 2) * (sizeof(double2) + sizeof(double)) + a.D * sizeof(double);
-    return SYNC_SHARED_F2 * sizeof(float2) + taps + lb + (stage > alias ? stage : alias);
+    const size_t det = a.n_ant * ((SYNC_THREADS + 4 * a.n_uw) * sizeof(float2) +
+                                  (SYNC_THREADS + 4 * a.n_pattern + 3) / 4 * 4 * sizeof(float));
+    return SYNC_SHARED_F2 * sizeof(float2) + taps + lb + std::max(stage, std::max(alias, det));
 }
 
 #define SYNC_DISPATCH(KERNEL, GRID, LDS)                                                   \
