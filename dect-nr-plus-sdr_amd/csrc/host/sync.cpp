@@ -10,6 +10,9 @@
 #include <memory>
 #include <vector>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "ctx_internal.hpp"
 
 using namespace dnrp;
@@ -194,6 +197,7 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     a.tw_fft = t->tw_fft.as<float2>();
     a.u = sc->u;
     a.b = sc->b;
+    a.det_stage = dev::sync_detect_stage(a);
     if (dev::sync_detect_lds(a) > 160 * 1024 || (4 + 3 * (size_t(1) << a.log2_fft)) * sizeof(float2) > 160 * 1024)
         return DNRP_EUNSUPPORTED;
     const size_t nsa = size_t(n) * a.n_ant * a.n_steps;
@@ -208,9 +212,39 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     ctx->tic("sync_steps", st);
     if (dev::launch_sync_steps(a, n, st) != hipSuccess) return DNRP_EDEVICE;
     ctx->toc("sync_steps", st);
+#ifdef DNRP_SYNC_PROFILE
+    // phase clocks of sync_detect per window (tools/sync_profile.py): averages to stderr
+    static dbuf prof;
+    const bool do_prof = std::getenv("DNRP_SYNC_PROFILE") && prof.ensure(size_t(n) * 16 * 8);
+    a.prof = do_prof ? prof.as<unsigned long long>() : nullptr;
+    if (do_prof) HIPCHK(hipMemsetAsync(prof.p, 0, size_t(n) * 16 * 8, st));
+#endif
     ctx->tic("sync_detect", st);
     if (dev::launch_sync_detect(a, n, st) != hipSuccess) return DNRP_EDEVICE;
     ctx->toc("sync_detect", st);
+#ifdef DNRP_SYNC_PROFILE
+    if (do_prof) {
+        std::vector<unsigned long long> h(size_t(n) * 16);
+        HIPCHK(hipMemcpyAsync(h.data(), prof.p, h.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        double acc[16] = {};
+        uint32_t cnt = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const unsigned long long* r = &h[size_t(i) * 16];
+            if (!r[0] || !r[11]) continue;
+            ++cnt;
+            unsigned long long prev = r[0];
+            for (int k = 1; k < 12; ++k)
+                if (r[k]) {
+                    acc[k] += double(r[k] - prev);
+                    prev = r[k];
+                }
+        }
+        std::fprintf(stderr, "sync_detect phases (wall_clock64 ticks, mean over %u windows):", cnt);
+        for (int k = 1; k < 12; ++k) std::fprintf(stderr, " p%d=%.0f", k, cnt ? acc[k] / cnt : 0.0);
+        std::fprintf(stderr, "\n");
+    }
+#endif
     ctx->tic("sync_fine", st);
     if (dev::launch_sync_fine(a, n, st) != hipSuccess) return DNRP_EDEVICE;
     ctx->toc("sync_fine", st);

@@ -555,6 +555,34 @@ __device__ __forceinline__ void wave_fft1024_rt(float2 (&v)[16], float2* xb, con
 }
 
 // block-wide sum of a double, result valid in all threads (blockDim.x multiple of 64, <= 1024)
+// three block sums with one set of barriers (each value summed exactly as block_sum sums it);
+// red holds >= 3 * waves doubles
+__device__ __forceinline__ void block_sum3(double& a, double& b, double& c, double* red) {
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o);
+        b += __shfl_xor(b, o);
+        c += __shfl_xor(c, o);
+    }
+    const uint32_t w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        red[w] = a;
+        red[nw + w] = b;
+        red[2 * nw + w] = c;
+    }
+    __syncthreads();
+    double sa = 0.0, sb = 0.0, sc = 0.0;
+    for (uint32_t i = 0; i < nw; ++i) {
+        sa += red[i];
+        sb += red[nw + i];
+        sc += red[2 * nw + i];
+    }
+    __syncthreads();
+    a = sa;
+    b = sb;
+    c = sc;
+}
+
 __device__ __forceinline__ double block_sum(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     const uint32_t w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;

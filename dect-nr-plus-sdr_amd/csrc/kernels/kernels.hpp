@@ -270,6 +270,8 @@ struct sync_args {
     float* P;                                  // [n][n_ant][n_steps] step powers
     float2* Cs;                                // [n][n_ant][n_steps] step correlations
     uint32_t max_reports;
+    uint32_t det_stage;                        // sync_detect: float2 slots of the resampler stage (sync_detect_lds)
+    unsigned long long* prof;                  // DNRP_SYNC_PROFILE builds: per-window phase clocks [n][16]
     sync_res* res;                             // [n][max_reports]
     uint32_t* n_found;                         // [n]
     // fine search (crosscorrelator.cpp): hw rate, FFT correlation against the STF templates
@@ -281,6 +283,7 @@ struct sync_args {
 hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st);
 hipError_t launch_sync_detect(const sync_args& a, uint32_t n, hipStream_t st);
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st);
+uint32_t sync_detect_stage(const sync_args& a);
 size_t sync_detect_lds(const sync_args& a);
 
 }  // namespace dnrp::dev

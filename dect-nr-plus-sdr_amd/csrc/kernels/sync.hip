@@ -39,7 +39,7 @@ __device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) { return a >= 
 // Whole block participates; ends with a barrier.
 template <int LR, int MR, int HLR>
 __device__ void sync_resample(const sync_args& A, const float2* __restrict__ x, int64_t y0, uint32_t cnt,
-                              float2* stage, float2* dst, const float* taps) {
+                              float2* stage, float2* dst, const float* taps, uint32_t stage_cap = 0xFFFFFFFFu) {
     const int64_t S = A.S_win;
     if constexpr (LR == 1) {
             stage_span<8>(dst, x, y0, cnt, S, threadIdx.x, blockDim.x);
@@ -67,21 +67,26 @@ __device__ void sync_resample(const sync_args& A, const float2* __restrict__ x, 
         using PB = pp_block<LR, MR, HLR>;
         const int64_t ms = A.m_star;
         const int64_t q0 = floordiv(y0 - ms, LR), q1 = floordiv(y0 + cnt - ms + LR - 1, LR);
-        const int64_t in0 = static_cast<int64_t>(A.p_star) + MR * q0 - HLR;
-        const uint32_t n_in = static_cast<uint32_t>(MR * (q1 - 1 - q0) + PB::W);
-        stage_span<8>(stage, x, in0, n_in, S, threadIdx.x, blockDim.x);
-        __syncthreads();
-        for (int64_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
-            float2 yv[LR];
-            PB::run(stage + MR * (q - q0), taps, yv);
-            const int64_t mb = ms + LR * q;
+        // pieces of nbp blocks whose input span fits the stage (stage_cap float2)
+        const int64_t nbp = stage_cap >= static_cast<uint32_t>(PB::W) + MR ? (stage_cap - PB::W) / MR + 1 : 1;
+        for (int64_t qa = q0; qa < q1; qa += nbp) {
+            const int64_t qe = min(qa + nbp, q1);
+            const int64_t in0 = static_cast<int64_t>(A.p_star) + MR * qa - HLR;
+            const uint32_t n_in = static_cast<uint32_t>(MR * (qe - 1 - qa) + PB::W);
+            stage_span<8>(stage, x, in0, n_in, S, threadIdx.x, blockDim.x);
+            __syncthreads();
+            for (int64_t q = qa + threadIdx.x; q < qe; q += blockDim.x) {
+                float2 yv[LR];
+                PB::run(stage + MR * (q - qa), taps, yv);
+                const int64_t mb = ms + LR * q;
 #pragma unroll
-            for (int k = 0; k < LR; ++k) {
-                const int64_t idx = mb + k - y0;
-                if (idx >= 0 && idx < static_cast<int64_t>(cnt)) dst[idx] = (mb + k >= 0) ? yv[k] : make_float2(0.f, 0.f);
+                for (int k = 0; k < LR; ++k) {
+                    const int64_t idx = mb + k - y0;
+                    if (idx >= 0 && idx < static_cast<int64_t>(cnt)) dst[idx] = (mb + k >= 0) ? yv[k] : make_float2(0.f, 0.f);
+                }
             }
+            __syncthreads();
         }
-        __syncthreads();
     }
 }
 
@@ -457,7 +462,7 @@ __device__ void wave_scan_d2(double2* v, uint32_t n, uint32_t lane) {
 struct peak_lds {
     double2* ckc;  // correlation prefix at every 16th product
     double* ckp;   // power prefix at every 16th sample
-    double* met;   // metric per position of the peak search
+    float* met;    // metric per position of the peak search (float, as the reference's movsum stages)
 };
 
 // autocorrelator_peak.cpp:145-264 for one antenna: per-sample metric over [r0, r0 + D), smoothed
@@ -560,7 +565,7 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
                 pw += static_cast<double>(cnorm(lbuf[yoff + i])) - static_cast<double>(cnorm(lbuf[yoff + i - A.stf_len]));
             }
             const double q = static_cast<double>(A.prefactor) * sqrt(cr * cr + ci * ci) / pw;
-            L.met[i] = q * q;
+            L.met[i] = static_cast<float>(q * q);
         }
     }
     __syncthreads();
@@ -614,6 +619,20 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
     __syncthreads();
 }
 
+#ifdef DNRP_SYNC_PROFILE
+#define SYNC_STAMP(i) \
+    if (threadIdx.x == 0 && A.prof) A.prof[size_t(w) * 16 + (i)] = wall_clock64()
+#else
+#define SYNC_STAMP(i)
+#endif
+
+// three waves per SIMD (<= 168 VGPRs, a few spills in the post-processing): with three workgroups'
+// LDS per CU this beats the 2-wave default in the pipelined bench (A/B on MI355X: 181.4k vs 184.9k
+// slot-pairs/s)
+#ifndef SYNC_DETECT_ATTR
+#define SYNC_DETECT_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#endif
+
 struct sync_shared {  // block scalars, at the start of the dynamic LDS (no static __shared__)
     double red[24];
     int s_min;
@@ -625,7 +644,7 @@ struct sync_shared {  // block scalars, at the start of the dynamic LDS (no stat
 constexpr uint32_t SYNC_SHARED_F2 = (sizeof(sync_shared) + 15) / 16 * 2;  // float2 slots, 16-B multiple
 
 template <int LR, int MR, int HLR>
-__global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) {
+__global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     sync_shared& sh = *reinterpret_cast<sync_shared*>(smem);
     double* red = sh.red;
@@ -644,7 +663,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
     peak_lds pl;  // aliases the staging area (dead once the resampler has run)
     pl.ckc = reinterpret_cast<double2*>(stage);
     pl.ckp = reinterpret_cast<double*>(pl.ckc + (region + 15) / 16 + 2);
-    pl.met = pl.ckp + (region + 15) / 16 + 2;
+    pl.met = reinterpret_cast<float*>(pl.ckp + (region + 15) / 16 + 2);
     if (LR > 1)
         stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, blockDim.x);
     __syncthreads();
@@ -658,6 +677,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
     float2* dc = stage;
     float* dp = reinterpret_cast<float*>(dc + A.n_ant * det_c);
     uint32_t nrep = 0, s_cur = 4, ignore = A.stf_len + A.pattern;
+    SYNC_STAMP(0);
     while (nrep < A.max_reports) {
         // ---------------- detection: first step at or after s_cur meeting the conditions
         if (threadIdx.x == 0) s_min = 0x7FFFFFFF;
@@ -703,6 +723,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
             }
         }
         __syncthreads();
+        SYNC_STAMP(1);
         s_cur = static_cast<uint32_t>(sd) + 1;
         const uint32_t det_time = s_cur * A.step, r0 = det_time - prm::SYNC_JUMP_BACK_PATTERNS * A.pattern;
         const float det_metric = s_metric;
@@ -710,8 +731,10 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
         const int64_t yb = static_cast<int64_t>(r0) - A.stf_len - SYNC_PAD_PEAK;
         for (uint32_t a = 0; a < A.n_ant; ++a) {
             const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
-            sync_resample<LR, MR, HLR>(A, x, yb, region, stage, lbuf, taps);
+            sync_resample<LR, MR, HLR>(A, x, yb, region, stage, lbuf, taps, A.det_stage);
+            SYNC_STAMP(2 + 2 * min(a, 3u));
             peak_search(A, lbuf, region, pl, r0, red, s_pk_metric[a], s_pk_idx[a]);
+            SYNC_STAMP(3 + 2 * min(a, 3u));
         }
         // post_processing_validity (autocorrelator_peak.cpp:311-364), float as in the reference
         float cm[8];
@@ -740,7 +763,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
             rms[a] = 0.f;
             if (!(cm[a] > 0.f)) continue;
             const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
-            sync_resample<LR, MR, HLR>(A, x, cpl, A.stf_len, stage, lbuf, taps);
+            sync_resample<LR, MR, HLR>(A, x, cpl, A.stf_len, stage, lbuf, taps, A.det_stage);
             double cr = 0.0, ci = 0.0, pw = 0.0;
             const uint32_t Lw = A.pattern * A.n_uw;
             for (uint32_t i = threadIdx.x; i < A.stf_len; i += blockDim.x) {
@@ -752,14 +775,13 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
                     ci += u * static_cast<double>(c.y);
                 }
             }
-            pw = block_sum(pw, red);
-            cr = block_sum(cr, red);
-            ci = block_sum(ci, red);
+            block_sum3(pw, cr, ci, red);
             const float m = s_pk_metric[a];
             msum2 += m;
             rms[a] = sqrtf(static_cast<float>(pw) / static_cast<float>(A.stf_len));
             cfo_w += m * atan2f(static_cast<float>(ci), static_cast<float>(cr)) / static_cast<float>(A.pattern);
         }
+        SYNC_STAMP(10);
         if (threadIdx.x == 0) {
             sync_res r{};
             r.found = 1;
@@ -787,6 +809,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_detect_kernel(sync_args A) 
         ++nrep;
         __syncthreads();
     }
+    SYNC_STAMP(11);
     if (threadIdx.x == 0) {
         A.n_found[w] = nrep;
         for (uint32_t k = nrep; k < A.max_reports; ++k) out[k].found = 0;
@@ -882,14 +905,27 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_fine_kernel(sync_args A) {
 }
 
 // ===================================================================== launchers
+// float2 slots of sync_detect's stage area: the peak-search arrays and the detection staging alias
+// it, and the resampler runs in pieces whose input span fits it (at least 64 blocks per piece)
+uint32_t sync_detect_stage(const sync_args& a) {
+    const uint32_t region = a.stf_len + a.D + SYNC_PAD_PEAK;
+    const size_t alias = ((region + 15) / 16 + 2) * (sizeof(double2) + sizeof(double)) + a.D * sizeof(float);
+    const size_t det = a.n_ant * ((SYNC_THREADS + 4 * a.n_uw) * sizeof(float2) +
+                                  (SYNC_THREADS + 4 * a.n_pattern + 3) / 4 * 4 * sizeof(float));
+    const size_t full = sync_stage_cap(a.L, a.M, a.hl, region);
+    const size_t piece = a.L > 1 ? a.hl + 1 + ((a.L - 1) * a.M) / a.L + 64 * a.M : 0;
+    const size_t need = std::max((std::max(alias, det) + sizeof(float2) - 1) / sizeof(float2), piece);
+    return static_cast<uint32_t>((std::min(full, need) + 1) / 2 * 2);
+}
+
 size_t sync_detect_lds(const sync_args& a) {
     const uint32_t region = a.stf_len + a.D + SYNC_PAD_PEAK;
     const size_t taps = (a.npp + 3) / 4 * 2 * sizeof(float2);
     const size_t lb = (region + 1) / 2 * 2 * sizeof(float2);
-    const size_t stage = sync_stage_cap(a.L, a.M, a.hl, region) * sizeof(float2);
-    const size_t alias = ((region + 15) / 16 + 2) * (sizeof(double2) + sizeof(double)) + a.D * sizeof(double);
+    const size_t alias = ((region + 15) / 16 + 2) * (sizeof(double2) + sizeof(double)) + a.D * sizeof(float);
     const size_t det = a.n_ant * ((SYNC_THREADS + 4 * a.n_uw) * sizeof(float2) +
                                   (SYNC_THREADS + 4 * a.n_pattern + 3) / 4 * 4 * sizeof(float));
+    const size_t stage = size_t(sync_detect_stage(a)) * sizeof(float2);
     return SYNC_SHARED_F2 * sizeof(float2) + taps + lb + std::max(stage, std::max(alias, det));
 }
 

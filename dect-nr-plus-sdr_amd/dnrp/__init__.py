@@ -21,7 +21,8 @@ import numpy as np
 import torch  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libdnrp.so")
+# DNRP_LIB: an alternative build of the library (tools/build_variant.sh, A/B experiments)
+LIB_PATH = os.environ.get("DNRP_LIB") or os.path.join(os.path.dirname(_HERE), "libdnrp.so")
 
 
 class DnrpError(RuntimeError):
