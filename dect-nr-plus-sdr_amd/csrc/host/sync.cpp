@@ -198,12 +198,14 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     a.u = sc->u;
     a.b = sc->b;
     a.det_stage = dev::sync_detect_stage(a);
-    if (dev::sync_detect_lds(a) > 160 * 1024 || (4 + 3 * (size_t(1) << a.log2_fft)) * sizeof(float2) > 160 * 1024)
+    if (dev::sync_detect_lds(a) > 160 * 1024 || (4 + 2 * (size_t(1) << a.log2_fft)) * sizeof(float2) > 160 * 1024)
         return DNRP_EUNSUPPORTED;
     const size_t nsa = size_t(n) * a.n_ant * a.n_steps;
     if (!ctx->sy_P.ensure(nsa * sizeof(float)) || !ctx->sy_C.ensure(nsa * sizeof(float2)) ||
-        !ctx->sy_res.ensure(size_t(n) * a.max_reports * sizeof(dev::sync_res)) || !ctx->sy_cnt.ensure(size_t(n) * 4))
+        !ctx->sy_res.ensure(size_t(n) * a.max_reports * sizeof(dev::sync_res)) || !ctx->sy_cnt.ensure(size_t(n) * 4) ||
+        !ctx->sy_spec.ensure(size_t(n) * a.max_reports * (size_t(1) << a.log2_fft) * sizeof(float2)))
         return DNRP_ENOMEM;
+    a.spec = ctx->sy_spec.as<float2>();
     a.P = ctx->sy_P.as<float>();
     a.Cs = ctx->sy_C.as<float2>();
     a.res = ctx->sy_res.as<dev::sync_res>();

@@ -278,6 +278,7 @@ struct sync_args {
     uint32_t Ltx, Mtx, xc_l, xc_len, tmpl_len, n_templates, log2_fft;
     const float2* tmpl_f;                      // [n_templates][n_fft] conj(DFT(template)) / n_fft
     const float2* tw_fft;                      // forward twiddles of n_fft
+    float2* spec;                              // sync_fine scratch: forward spectrum per report [n * max_reports][n_fft]
     uint32_t u, b;
 };
 hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st);

@@ -827,7 +827,9 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_fine_kernel(sync_args A) {
     const uint32_t nf = 1u << A.log2_fft;
     float2* xb = smem + 4;
     float2* yb = xb + nf;
-    float2* Sb = yb + nf;
+    // the forward spectrum is read once per template: kept in a global scratch row (L2-resident
+    // while the workgroup runs) instead of a third LDS buffer, for two workgroups per CU
+    float2* Sb = A.spec + static_cast<size_t>(blockIdx.x) * nf;
     // strongest antenna: first maximum of coarse_peak_array (ant.cpp:104-108)
     uint32_t best = 0;
     for (uint32_t a = 1; a < A.n_ant; ++a)
@@ -846,7 +848,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_fine_kernel(sync_args A) {
     __syncthreads();
     const float2* S = fft_pow2<-1>(xb, yb, A.tw_fft, A.log2_fft);
     for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) Sb[i] = S[i];
-    __syncthreads();
+    __syncthreads();  // S's buffer is overwritten below; each thread re-reads only its own Sb[i]
     float xm[4];
     uint32_t xi[4];
     for (uint32_t k = 0; k < A.n_templates; ++k) {
@@ -986,7 +988,7 @@ hipError_t launch_sync_detect(const sync_args& a, uint32_t n, hipStream_t st) {
 }
 
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st) {
-    const size_t lds = (4 + 3 * (size_t(1) << a.log2_fft)) * sizeof(float2);
+    const size_t lds = (4 + 2 * (size_t(1) << a.log2_fft)) * sizeof(float2);
     hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(SYNC_THREADS), lds, st, a);
     return hipGetLastError();
 }
