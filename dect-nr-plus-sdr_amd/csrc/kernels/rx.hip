@@ -8,6 +8,8 @@
 //                  + CP removal + FFT + bin extraction + amplitude scaling + STO derotation
 //                  (rx_synced.cpp:711-771) into the frequency-domain grid Y in HBM.
 // The back end (channel estimation, equalisation, demapping) is in rx_back.hip.
+#include <cstdlib>
+
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
@@ -306,12 +308,15 @@ __host__ __device__ inline uint32_t rxw_region(uint32_t L, uint32_t M, uint32_t 
     return (r + 15) / 16 * 16;
 }
 
-template <int LR, int MR, int HLR, bool CT>
+// WPG symbols (= wavefronts) per workgroup: the compile-time-tap path shares nothing between its
+// waves, so it can run one wave per workgroup and free each wave's LDS region when that wave retires
+template <int LR, int MR, int HLR, bool CT, int WPG = RXW_SYMS>
 __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu(4))) rx_fft_wave_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     using PB = pp_block<LR, MR, HLR>;
     constexpr uint32_t Nd = 1024;
-    const uint32_t nblk = (A.sym_count + RXW_SYMS - 1) / RXW_SYMS;
+    static_assert(CT || WPG == RXW_SYMS, "the table path shares its tables among RXW_SYMS waves");
+    const uint32_t nblk = (A.sym_count + WPG - 1) / WPG;
     const uint32_t blk = blockIdx.x % nblk;
     const uint32_t a = (blockIdx.x / nblk) % A.N_RX;
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / (nblk * A.N_RX));
@@ -326,7 +331,7 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
         stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, RX_THREADS);
     }
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t l = A.sym_first + blk * RXW_SYMS + w;
+    const uint32_t l = A.sym_first + blk * WPG + w;
     const bool active = l < A.sym_first + A.sym_count;
     const rx_pkt_in in = A.pin[pkt];
     const rx_pkt_state S = A.st[pkt];
@@ -400,8 +405,21 @@ hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
     if (Nd == 1024 && a.L == 9 && a.M == 10 && a.hl == 24 && a.sym_per_block == RXW_SYMS) {  // os_min 1
         const uint32_t W = pp_block<9, 10, 24>::W;
         if (a.stream) {  // host: run-time taps == compiled-in taps bit for bit
-            const size_t lds = RXW_SYMS * size_t(rxw_region(9, 10, W)) * sizeof(float2);
-            hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true>), g, b, lds, st, a);
+            // one wave per workgroup by default: each wave's LDS region is freed when it retires
+            // instead of with its slowest sibling (A/B on MI355X: 179.4k vs 176.4k slot-pairs/s);
+            // DNRP_RX_WPG = 2 / 4 for the grouped launches
+            static const int wpg = [] {
+                const char* e = std::getenv("DNRP_RX_WPG");
+                return e ? std::atoi(e) : 1;
+            }();
+            const size_t lds1 = size_t(rxw_region(9, 10, W)) * sizeof(float2);
+            auto grid = [&](uint32_t per) { return dim3(n * a.N_RX * ((a.sym_count + per - 1) / per)); };
+            if (wpg == 1)
+                hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 1>), grid(1), dim3(64), lds1, st, a);
+            else if (wpg == 2)
+                hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 2>), grid(2), dim3(128), 2 * lds1, st, a);
+            else
+                hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true>), g, b, RXW_SYMS * lds1, st, a);
         } else {
             const size_t lds = (Nd + (a.npp + 1) / 2 + RXW_SYMS * size_t(rxw_region(9, 10, W))) * sizeof(float2);
             hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, false>), g, b, lds, st, a);

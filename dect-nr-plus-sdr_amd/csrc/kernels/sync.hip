@@ -265,7 +265,7 @@ __host__ __device__ constexpr uint32_t ss_inbuf() {  // float2 per wave, 16-B mu
     return ((HLR + 1 + ((LR - 1) * MR) / LR - MR) + 64 * MR + 1) / 2 * 2;
 }
 
-template <int LR, int MR, int HLR, int SQ>
+template <int LR, int MR, int HLR, int SQ, int WPG = SS_WPG>
 __global__ void __launch_bounds__(64 * SS_WPG) sync_steps_stream_kernel(sync_args A, uint32_t seg_steps, uint32_t n_seg) {
     using PD = pp_direct<LR, MR, HLR>;
     constexpr int W = PD::W, CARRY = W - MR, NEW = 64 * MR;
@@ -274,7 +274,7 @@ __global__ void __launch_bounds__(64 * SS_WPG) sync_steps_stream_kernel(sync_arg
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;  // uniform
     float2* inb = smem + wv * (INB + SS_RING);
     float2* ring = inb + INB;
-    const uint32_t gw = blockIdx.x * SS_WPG + wv;
+    const uint32_t gw = blockIdx.x * WPG + wv;
     const uint32_t seg = gw % n_seg, a = (gw / n_seg) % A.n_ant, w = gw / (n_seg * A.n_ant);
     if (w >= A.n_win) return;  // no barriers below: a retired wave stalls nobody
     const uint32_t s_a = seg * seg_steps, s_b = min(s_a + seg_steps, A.n_steps);
@@ -958,7 +958,16 @@ hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
         const uint64_t waves = uint64_t(n) * a.n_ant * n_seg;
         const size_t lds = SS_WPG * size_t(ss_inbuf<9, 10, 24>() + SS_RING) * sizeof(float2);
         const dim3 g(static_cast<uint32_t>((waves + SS_WPG - 1) / SS_WPG)), b(64 * SS_WPG);
-        if (a.step == 64)
+        // one wave per workgroup by default: a retired segment frees its LDS at once (A/B on
+        // MI355X: sync_steps 4.32 -> 3.81 ms, 176.4k -> 186.0k slot-pairs/s); DNRP_SYNC_WPG=4 groups
+        static const int wpg = [] {
+            const char* e = std::getenv("DNRP_SYNC_WPG");
+            return e ? std::atoi(e) : 1;
+        }();
+        if (a.step == 64 && wpg == 1)
+            hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 16, 1>), dim3(static_cast<uint32_t>(waves)), dim3(64),
+                               lds / SS_WPG, st, a, seg_steps, n_seg);
+        else if (a.step == 64)
             hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 16>), g, b, lds, st, a, seg_steps, n_seg);
         else
             hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 0>), g, b, lds, st, a, seg_steps, n_seg);
