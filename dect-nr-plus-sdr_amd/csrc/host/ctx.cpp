@@ -182,6 +182,10 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         fill_pairs(t->tm.N_TS, pair, mod);
         for (auto& c : code) {
             const uint32_t ty = c & dev::CODE_MASK;
+            if (ty == dev::CODE_DRS) {  // DRS: the stream in the pair field too (one W-row read per bin)
+                c |= (c & 7u) << dev::CODE_PAIR_SHIFT;
+                continue;
+            }
             if (ty != dev::CODE_PCC && ty != dev::CODE_PDC) continue;
             const uint32_t j = c & ~dev::CODE_MASK;
             if (j > dev::CODE_J_MASK) {

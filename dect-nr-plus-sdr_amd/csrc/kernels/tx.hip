@@ -463,7 +463,7 @@ struct txs_wave {
     __device__ float2 bin_df(uint32_t c, const uint8_t* sb, uint32_t ab, const uint8_t* pcb) const {
         const uint32_t ty = c & CODE_MASK, j = c & CODE_J_MASK, pr = (c >> CODE_PAIR_SHIFT) & 0xFFu;
         float2 x0 = pdc_sym<Q8>(sb, ab, j);
-        float2 v;
+        float2 v, wa_drs = make_float2(0.f, 0.f);
         if (MODE == TXS_SISO) {  // SISO (N_SS = 1): PCC and PDC alike
             if (PCC && ty == CODE_PCC) x0 = pcc_sym(pcb, j);
             v = cmul(wrow[0], x0);
@@ -477,11 +477,14 @@ struct txs_wave {
             }
             x1 = (j & 1u) ? make_float2(x1.x, -x1.y) : make_float2(-x1.x, x1.y);
             v = cadd(cmul(wrow[pr & 0xFu], x0), cmul(wrow[pr >> 4], x1));
+            if (MODE == TXS_TXDIV) wa_drs = wrow[pr & 0xFu];
         } else {
             v = make_float2(0.f, 0.f);
             for (uint32_t ss = 0; ss < A->N_SS; ++ss) v = cadd(v, cmul(wrow[ss], pdc_sym<Q8>(sb, ab, j * A->N_SS + ss)));
         }
-        const float2 d = cscale(wrow[j & 7u], (j & 8u) ? -1.f : 1.f);
+        // DRS codes carry their stream in the pair field: in transmit diversity the pair's first W
+        // entry above is the DRS weight (no second read)
+        const float2 d = cscale(MODE == TXS_TXDIV ? wa_drs : wrow[j & 7u], (j & 8u) ? -1.f : 1.f);
         v = ty == CODE_DRS ? d : v;
         v = (ty == CODE_PDC || ty == CODE_DRS || (PCC && ty == CODE_PCC)) ? v : make_float2(0.f, 0.f);
         return cscale(v, P.scale_df);
