@@ -244,7 +244,17 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
         }
         std::fprintf(stderr, "sync_detect phases (wall_clock64 ticks, mean over %u windows):", cnt);
         for (int k = 1; k < 12; ++k) std::fprintf(stderr, " p%d=%.0f", k, cnt ? acc[k] / cnt : 0.0);
-        std::fprintf(stderr, "\n");
+        double q[4] = {};
+        for (uint32_t i = 0; i < n; ++i) {
+            const unsigned long long* r = &h[size_t(i) * 16];
+            if (!r[8] || !r[12] || !r[13] || !r[14]) continue;
+            q[0] += double(r[12] - r[8]);
+            q[1] += double(r[13] - r[12]);
+            q[2] += double(r[14] - r[13]);
+            q[3] += double(r[9] - r[14]);
+        }
+        std::fprintf(stderr, " | last peak search: sums %.0f scans %.0f metric %.0f smooth+argmax %.0f\n",
+                     cnt ? q[0] / cnt : 0.0, cnt ? q[1] / cnt : 0.0, cnt ? q[2] / cnt : 0.0, cnt ? q[3] / cnt : 0.0);
     }
 #endif
     ctx->tic("sync_fine", st);

@@ -459,6 +459,13 @@ __device__ void wave_scan_d2(double2* v, uint32_t n, uint32_t lane) {
     if (lane == 63) v[n] = make_double2(ix, iy);
 }
 
+#ifdef DNRP_SYNC_PROFILE
+#define SYNC_STAMP(i) \
+    if (threadIdx.x == 0 && A.prof) A.prof[size_t(w) * 16 + (i)] = wall_clock64()
+#else
+#define SYNC_STAMP(i)
+#endif
+
 struct peak_lds {
     double2* ckc;  // correlation prefix at every 16th product
     double* ckp;   // power prefix at every 16th sample
@@ -497,6 +504,10 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
         }
     }
     __syncthreads();
+#ifdef DNRP_SYNC_PROFILE
+    const uint32_t w = blockIdx.x;
+#endif
+    SYNC_STAMP(12);
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     if (wv == 0) wave_scan_d2(L.ckc, nsc, lane);
     if (wv == 1) {  // power prefix: scan as double2 with zero imaginary parts via a temporary view
@@ -518,6 +529,7 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
         if (lane == 63) L.ckp[nsp] = inc;
     }
     __syncthreads();
+    SYNC_STAMP(13);
     // prefix helpers: PC(z) = sum of prod with product index < z; PP(z) = sum of power index < z
     auto PC = [&](uint32_t z, double& rx, double& ry) {
         const uint32_t g = z >> 4;
@@ -564,11 +576,13 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
                 }
                 pw += static_cast<double>(cnorm(lbuf[yoff + i])) - static_cast<double>(cnorm(lbuf[yoff + i - A.stf_len]));
             }
-            const double q = static_cast<double>(A.prefactor) * sqrt(cr * cr + ci * ci) / pw;
-            L.met[i] = static_cast<float>(q * q);
+            // (prefactor |c| / pw)^2 without the square root (equal to double rounding, stored as float)
+            const double pf = static_cast<double>(A.prefactor);
+            L.met[i] = static_cast<float>(pf * pf * (cr * cr + ci * ci) / (pw * pw));
         }
     }
     __syncthreads();
+    SYNC_STAMP(14);
     // smoother (length 2 bos + 1, zero history) and last-maximum argmax
     const uint32_t ns = (prm::SYNC_PEAK_SMOOTH_LEFT + prm::SYNC_PEAK_SMOOTH_RIGHT) * A.bos + 1;
     double best = -1.0;
@@ -619,12 +633,6 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
     __syncthreads();
 }
 
-#ifdef DNRP_SYNC_PROFILE
-#define SYNC_STAMP(i) \
-    if (threadIdx.x == 0 && A.prof) A.prof[size_t(w) * 16 + (i)] = wall_clock64()
-#else
-#define SYNC_STAMP(i)
-#endif
 
 // three waves per SIMD (<= 168 VGPRs, a few spills in the post-processing): with three workgroups'
 // LDS per CU this beats the 2-wave default in the pipelined bench (A/B on MI355X: 181.4k vs 184.9k
