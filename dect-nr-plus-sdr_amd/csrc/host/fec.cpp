@@ -1,0 +1,609 @@
+// fec.cpp — DECT NR+ channel coding on the host (see fec.hpp), behind the C-ABI in dnrp.h:
+//   dnrp_fec_cbsegm    <- sp3::fix::srsran_cbsegm_FIX        (sections_part3/fix/cbsegm.cpp:65-123)
+//   dnrp_pcc_encode    <- pcc_enc_encode up to scrambling     (phy/fec/pcc_enc.cpp:145-208)
+//   dnrp_pcc_decode    <- pcc_enc_decode after descrambling   (phy/fec/pcc_enc.cpp:215-364)
+//   dnrp_pdc_encode    <- pdc_encode_codeblocks w/o scrambling(phy/fec/pdc_enc.cpp:127-229)
+//   dnrp_pdc_decode    <- pdc_decode_codeblocks w/o descramb. (phy/fec/pdc_enc.cpp:291-492)
+//   dnrp_harq_rx_*     <- harq::buffer_rx_t softbuffer (cb softbits, cb CRC flags, cb data)
+// Scrambling is not repeated here: dnrp_tx_batch scrambles the d-bits and dnrp_rx_pcc/pdc_batch
+// descramble the LLRs (the library's boundary, pcc_enc.cpp:212,297 / pdc_enc.cpp:220,339-344).
+#include "fec.hpp"
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <memory>
+#include <mutex>
+
+#include "dnrp.h"
+
+namespace dnrp::fec {
+
+// TS 36.212 Table 5.1.3-3: (f1, f2) of the QPP interleaver for each code-block size K. The K column
+// itself follows from the table's steps (8 up to 512, 16 up to 1024, 32 up to 2048, 64 up to 6144)
+// and is pinned against the reference's tc_cb_sizes (cbsegm.cpp:34-46, tests/golden/ref_fec.json);
+// every (f1, f2) row is checked to be a permutation (tests/test_fec_host.py).
+static const uint16_t kQpp[kNofCbSizes][2] = {
+    {3, 10},    {7, 12},    {19, 42},   {7, 16},    {7, 18},    {11, 20},   {5, 22},    {11, 24},
+    {7, 26},    {41, 84},   {103, 90},  {15, 32},   {9, 34},    {17, 108},  {9, 38},    {21, 120},
+    {101, 84},  {21, 44},   {57, 46},   {23, 48},   {13, 50},   {27, 52},   {11, 36},   {27, 56},
+    {85, 58},   {29, 60},   {33, 62},   {15, 32},   {17, 198},  {33, 68},   {103, 210}, {19, 36},
+    {19, 74},   {37, 76},   {19, 78},   {21, 120},  {21, 82},   {115, 84},  {193, 86},  {21, 44},
+    {133, 90},  {81, 46},   {45, 94},   {23, 48},   {243, 98},  {151, 40},  {155, 102}, {25, 52},
+    {51, 106},  {47, 72},   {91, 110},  {29, 168},  {29, 114},  {247, 58},  {29, 118},  {89, 180},
+    {91, 122},  {157, 62},  {55, 84},   {31, 64},   {17, 66},   {35, 68},   {227, 420}, {65, 96},
+    {19, 74},   {37, 76},   {41, 234},  {39, 80},   {185, 82},  {43, 252},  {21, 86},   {155, 44},
+    {79, 120},  {139, 92},  {23, 94},   {217, 48},  {25, 98},   {17, 80},   {127, 102}, {25, 52},
+    {239, 106}, {17, 48},   {137, 110}, {215, 112}, {29, 114},  {15, 58},   {147, 118}, {29, 60},
+    {59, 122},  {65, 124},  {55, 84},   {31, 64},   {17, 66},   {171, 204}, {67, 140},  {35, 72},
+    {19, 74},   {39, 76},   {19, 78},   {199, 240}, {21, 82},   {211, 252}, {21, 86},   {43, 88},
+    {149, 60},  {45, 92},   {49, 846},  {71, 48},   {13, 28},   {17, 80},   {25, 102},  {183, 104},
+    {55, 954},  {127, 96},  {27, 110},  {29, 112},  {29, 114},  {57, 116},  {45, 354},  {31, 120},
+    {59, 610},  {185, 124}, {113, 420}, {31, 64},   {17, 66},   {171, 136}, {209, 420}, {253, 216},
+    {367, 444}, {265, 456}, {181, 468}, {39, 80},   {27, 164},  {127, 504}, {143, 172}, {43, 88},
+    {29, 300},  {45, 92},   {157, 188}, {47, 96},   {13, 28},   {111, 240}, {443, 204}, {51, 104},
+    {51, 212},  {451, 192}, {257, 220}, {57, 336},  {313, 228}, {271, 232}, {179, 236}, {331, 120},
+    {363, 244}, {375, 248}, {127, 168}, {31, 64},   {33, 130},  {43, 264},  {33, 134},  {477, 408},
+    {35, 138},  {233, 280}, {357, 142}, {337, 480}, {37, 146},  {71, 444},  {71, 120},  {37, 152},
+    {39, 462},  {127, 234}, {39, 158},  {39, 80},   {31, 96},   {113, 902}, {41, 166},  {251, 336},
+    {43, 170},  {21, 86},   {43, 174},  {45, 176},  {45, 178},  {161, 120}, {89, 182},  {323, 184},
+    {47, 186},  {23, 94},   {47, 190},  {263, 480}};
+
+uint32_t cb_size(uint32_t idx) {
+    if (idx < 60) return 40 + 8 * idx;
+    if (idx < 92) return 528 + 16 * (idx - 60);
+    if (idx < 124) return 1056 + 32 * (idx - 92);
+    if (idx < kNofCbSizes) return 2112 + 64 * (idx - 124);
+    return 0;
+}
+
+int cb_index(uint32_t long_cb) {
+    for (uint32_t j = 0; j < kNofCbSizes; ++j)
+        if (cb_size(j) >= long_cb) return (int)j;
+    return -1;
+}
+
+void qpp_params(uint32_t idx, uint32_t* f1, uint32_t* f2) {
+    *f1 = idx < kNofCbSizes ? kQpp[idx][0] : 0;
+    *f2 = idx < kNofCbSizes ? kQpp[idx][1] : 0;
+}
+
+// Per code-block size: QPP permutation and the rate-matching circular-buffer map. Built once.
+struct SizeTables {
+    std::vector<uint32_t> pi;    // QPP interleaver
+    std::vector<int32_t> wmap;   // circular buffer position -> stream * (K + 4) + index, -1 = dummy bit
+    uint32_t R = 0, Kpi = 0;
+};
+static std::array<SizeTables, kNofCbSizes> g_tab;
+static std::array<std::once_flag, kNofCbSizes> g_once;
+
+// TS 36.212 §5.1.4.1.1 inter-column permutation of the 32-column sub-block interleaver
+static const uint8_t kPerm[32] = {0, 16, 8,  24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
+                                  1, 17, 9,  25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
+
+static const SizeTables& tables(uint32_t idx) {
+    std::call_once(g_once[idx], [idx] {
+        SizeTables& t = g_tab[idx];
+        const uint32_t K = cb_size(idx);
+        t.pi.resize(K);
+        const uint64_t f1 = kQpp[idx][0], f2 = kQpp[idx][1];
+        for (uint64_t i = 0; i < K; ++i) t.pi[i] = (uint32_t)((f1 * i + f2 * i * i) % K);
+        const uint32_t D = K + 4;
+        t.R = (D + 31) / 32;
+        t.Kpi = 32 * t.R;
+        const uint32_t ND = t.Kpi - D;
+        t.wmap.assign(3 * t.Kpi, -1);
+        for (uint32_t k = 0; k < t.Kpi; ++k) {
+            const uint32_t y01 = kPerm[k / t.R] + 32 * (k % t.R);             // streams 0 and 1
+            const uint32_t y2 = (kPerm[k / t.R] + 32 * (k % t.R) + 1) % t.Kpi;  // stream 2
+            if (y01 >= ND) {
+                t.wmap[k] = (int32_t)(y01 - ND);
+                t.wmap[t.Kpi + 2 * k] = (int32_t)(D + y01 - ND);
+            }
+            if (y2 >= ND) t.wmap[t.Kpi + 2 * k + 1] = (int32_t)(2 * D + y2 - ND);
+        }
+    });
+    return g_tab[idx];
+}
+
+const std::vector<uint32_t>& qpp(uint32_t idx) { return tables(idx).pi; }
+
+int cbsegm(uint32_t tbs, uint32_t Z, Segm* s) {
+    std::memset(s, 0, sizeof(*s));
+    s->Z = Z;
+    if (tbs == 0) return 0;
+    const uint32_t B = tbs + 24;
+    s->tbs = tbs;
+    uint32_t Bp;
+    if (B <= Z) {
+        s->C = 1;
+        Bp = B;
+    } else {
+        if (Z <= 24) return -1;
+        s->C = (B + (Z - 24) - 1) / (Z - 24);
+        Bp = B + 24 * s->C;
+    }
+    const int i1 = cb_index((Bp - 1) / s->C + 1);
+    if (i1 < 0) return -1;
+    s->K1 = cb_size((uint32_t)i1);
+    s->K1_idx = (uint32_t)i1;
+    if (s->C == 1) {
+        s->C1 = 1;
+    } else {
+        if (i1 == 0) return -1;
+        s->K2 = cb_size((uint32_t)i1 - 1);
+        s->K2_idx = (uint32_t)i1 - 1;
+        s->C2 = (s->C * s->K1 - Bp) / (s->K1 - s->K2);
+        s->C1 = s->C - s->C2;
+    }
+    s->F = s->C1 * s->K1 + s->C2 * s->K2 - Bp;
+    return 0;
+}
+
+uint32_t crc_bits(const uint8_t* data, uint32_t nbits, uint32_t poly, uint32_t len) {
+    const uint32_t mask = (len == 32) ? 0xFFFFFFFFu : ((1u << len) - 1);
+    uint32_t reg = 0;
+    uint32_t i = 0;
+    if (len >= 8) {
+        // byte-wise (MSB first) over the whole bytes
+        static thread_local uint32_t tab[256], tab_poly = 0, tab_len = 0;
+        if (tab_poly != poly || tab_len != len) {
+            for (uint32_t b = 0; b < 256; ++b) {
+                uint32_t r = b << (len - 8);
+                for (int k = 0; k < 8; ++k) r = (r & (1u << (len - 1))) ? ((r << 1) ^ poly) & mask : (r << 1) & mask;
+                tab[b] = r;
+            }
+            tab_poly = poly;
+            tab_len = len;
+        }
+        for (; i + 8 <= nbits; i += 8) reg = ((reg << 8) & mask) ^ tab[((reg >> (len - 8)) ^ data[i / 8]) & 0xFF];
+    }
+    for (; i < nbits; ++i) {
+        const uint32_t bit = (data[i / 8] >> (7 - i % 8)) & 1;
+        const uint32_t top = (reg >> (len - 1)) & 1;
+        reg = (reg << 1) & mask;
+        if (top ^ bit) reg ^= poly;
+    }
+    return reg;
+}
+
+// ---- turbo encoder (TS 36.212 §5.1.3.2): g0 = 1 + D^2 + D^3 feedback, g1 = 1 + D + D^3 ----------
+static void rsc(const uint8_t* in, const uint32_t* pi, uint32_t K, uint8_t* z, uint8_t tx[3], uint8_t tz[3]) {
+    uint32_t s1 = 0, s2 = 0, s3 = 0;
+    for (uint32_t k = 0; k < K; ++k) {
+        const uint32_t c = pi ? in[pi[k]] : in[k];
+        const uint32_t a = c ^ s2 ^ s3;
+        z[k] = (uint8_t)(a ^ s1 ^ s3);
+        s3 = s2;
+        s2 = s1;
+        s1 = a;
+    }
+    for (int t = 0; t < 3; ++t) {  // trellis termination: input = feedback, register fills with 0
+        tx[t] = (uint8_t)(s2 ^ s3);
+        tz[t] = (uint8_t)(s1 ^ s3);
+        s3 = s2;
+        s2 = s1;
+        s1 = 0;
+    }
+}
+
+void turbo_encode(const uint8_t* c, uint32_t idx, uint8_t* d0, uint8_t* d1, uint8_t* d2) {
+    const uint32_t K = cb_size(idx);
+    const auto& pi = tables(idx).pi;
+    uint8_t x1[3], z1[3], x2[3], z2[3];
+    std::memcpy(d0, c, K);
+    rsc(c, nullptr, K, d1, x1, z1);
+    rsc(c, pi.data(), K, d2, x2, z2);
+    d0[K] = x1[0], d0[K + 1] = z1[1], d0[K + 2] = x2[0], d0[K + 3] = z2[1];
+    d1[K] = z1[0], d1[K + 1] = x1[2], d1[K + 2] = z2[0], d1[K + 3] = x2[2];
+    d2[K] = x1[1], d2[K + 1] = z1[2], d2[K + 2] = x2[1], d2[K + 3] = z2[2];
+}
+
+// ---- rate matching (TS 36.212 §5.1.4.1) -----------------------------------------------------------
+uint32_t rm_kw(uint32_t idx) { return 3 * tables(idx).Kpi; }
+
+static uint32_t rm_k0(const SizeTables& t, uint32_t rv) {
+    const uint32_t Ncb = 3 * t.Kpi;  // no soft-buffer limitation (srsran_rm_turbo_tx_lut)
+    return t.R * (2 * ((Ncb + 8 * t.R - 1) / (8 * t.R)) * rv + 2);
+}
+
+void rm_tx(const uint8_t* d0, const uint8_t* d1, const uint8_t* d2, uint32_t idx, uint32_t E, uint32_t rv,
+           uint8_t* e) {
+    const SizeTables& t = tables(idx);
+    const uint32_t D = cb_size(idx) + 4, Ncb = 3 * t.Kpi;
+    uint32_t pos = rm_k0(t, rv) % Ncb;
+    for (uint32_t k = 0; k < E;) {
+        const int32_t m = t.wmap[pos];
+        if (m >= 0) {
+            const uint32_t s = (uint32_t)m / D, i = (uint32_t)m % D;
+            e[k++] = s == 0 ? d0[i] : (s == 1 ? d1[i] : d2[i]);
+        }
+        if (++pos == Ncb) pos = 0;
+    }
+}
+
+void rm_rx(const int16_t* e, uint32_t idx, uint32_t E, uint32_t rv, int16_t* w) {
+    const SizeTables& t = tables(idx);
+    const uint32_t Ncb = 3 * t.Kpi;
+    uint32_t pos = rm_k0(t, rv) % Ncb;
+    for (uint32_t k = 0; k < E;) {
+        if (t.wmap[pos] >= 0) {
+            const int32_t v = (int32_t)w[pos] + e[k++];
+            w[pos] = (int16_t)std::min(32767, std::max(-32768, v));
+        }
+        if (++pos == Ncb) pos = 0;
+    }
+}
+
+void rm_deinterleave(const int16_t* w, uint32_t idx, int32_t* d0, int32_t* d1, int32_t* d2) {
+    const SizeTables& t = tables(idx);
+    const uint32_t D = cb_size(idx) + 4;
+    for (uint32_t pos = 0; pos < 3 * t.Kpi; ++pos) {
+        const int32_t m = t.wmap[pos];
+        if (m < 0) continue;
+        const uint32_t s = (uint32_t)m / D, i = (uint32_t)m % D;
+        (s == 0 ? d0 : (s == 1 ? d1 : d2))[i] = w[pos];
+    }
+}
+
+// ---- max-log-MAP decoder --------------------------------------------------------------------------
+// State s = 4 s1 + 2 s2 + s3 (s1 = newest register bit). LLRs: positive = bit 1. Branch metric of
+// input u / parity p: u (L_sys + L_apriori) + p L_par (the max-log metric up to a per-step constant).
+// Integer arithmetic throughout, so the device decoder reproduces it bit for bit.
+static constexpr int32_t kNeg = -(1 << 28);
+static inline void trans(uint32_t s, uint32_t u, uint32_t* next, uint32_t* p) {
+    const uint32_t s1 = (s >> 2) & 1, s2 = (s >> 1) & 1, s3 = s & 1;
+    const uint32_t a = u ^ s2 ^ s3;
+    *p = a ^ s1 ^ s3;
+    *next = (a << 2) | (s1 << 1) | s2;
+}
+
+// One constituent decoder over K steps + 3 tail steps. A[k] = systematic + a priori, B[k] = parity,
+// tx/tz = tail systematic / parity. Writes the full LLR into llr and the extrinsic into le.
+static void map_decode(uint32_t K, const int32_t* A, const int32_t* B, const int32_t* tx, const int32_t* tz,
+                       int32_t* alpha, int32_t* llr, int32_t* le) {
+    int32_t* al = alpha;
+    for (int s = 0; s < 8; ++s) al[s] = s == 0 ? 0 : kNeg;
+    for (uint32_t k = 0; k < K; ++k) {
+        const int32_t* a0 = al + 8 * k;
+        int32_t* a1 = al + 8 * (k + 1);
+        for (int s = 0; s < 8; ++s) a1[s] = kNeg;
+        for (uint32_t s = 0; s < 8; ++s)
+            for (uint32_t u = 0; u < 2; ++u) {
+                uint32_t nx, p;
+                trans(s, u, &nx, &p);
+                const int32_t v = a0[s] + (u ? A[k] : 0) + (p ? B[k] : 0);
+                a1[nx] = std::max(a1[nx], v);
+            }
+        int32_t mx = a1[0];
+        for (int s = 1; s < 8; ++s) mx = std::max(mx, a1[s]);
+        for (int s = 0; s < 8; ++s) a1[s] = std::max(a1[s] - mx, kNeg);
+    }
+    // backward through the termination (input forced to the feedback value, register fills with 0)
+    int32_t be[8], bn[8];
+    for (int s = 0; s < 8; ++s) be[s] = s == 0 ? 0 : kNeg;
+    for (int t = 2; t >= 0; --t) {
+        for (uint32_t s = 0; s < 8; ++s) {
+            const uint32_t u = ((s >> 1) ^ s) & 1;  // s2 ^ s3
+            uint32_t nx, p;
+            trans(s, u, &nx, &p);
+            bn[s] = be[nx] + (u ? tx[t] : 0) + (p ? tz[t] : 0);
+        }
+        int32_t mx = bn[0];
+        for (int s = 1; s < 8; ++s) mx = std::max(mx, bn[s]);
+        for (int s = 0; s < 8; ++s) be[s] = std::max(bn[s] - mx, kNeg);
+    }
+    for (int64_t k = (int64_t)K - 1; k >= 0; --k) {
+        const int32_t* a0 = al + 8 * k;
+        int32_t m1 = INT32_MIN, m0 = INT32_MIN;
+        for (uint32_t s = 0; s < 8; ++s) {
+            int32_t b = INT32_MIN;
+            for (uint32_t u = 0; u < 2; ++u) {
+                uint32_t nx, p;
+                trans(s, u, &nx, &p);
+                const int32_t g = (u ? A[k] : 0) + (p ? B[k] : 0);
+                const int32_t v = a0[s] + g + be[nx];
+                if (u) m1 = std::max(m1, v); else m0 = std::max(m0, v);
+                b = std::max(b, g + be[nx]);
+            }
+            bn[s] = b;
+        }
+        llr[k] = m1 - m0;
+        const int32_t e = llr[k] - A[k];
+        le[k] = std::min(1 << 20, std::max(-(1 << 20), (e * 3) >> 2));  // extrinsic scaled by 3/4
+        int32_t mx = bn[0];
+        for (int s = 1; s < 8; ++s) mx = std::max(mx, bn[s]);
+        for (int s = 0; s < 8; ++s) be[s] = std::max(bn[s] - mx, kNeg);
+    }
+}
+
+void Tdec::load(const int16_t* w, uint32_t idx_) {
+    idx = idx_;
+    K = cb_size(idx);
+    std::vector<int32_t> d0(K + 4), d1(K + 4), d2(K + 4);
+    rm_deinterleave(w, idx, d0.data(), d1.data(), d2.data());
+    sys.assign(d0.begin(), d0.begin() + K);
+    p1.assign(d1.begin(), d1.begin() + K);
+    p2.assign(d2.begin(), d2.begin() + K);
+    // tails: encoder 1 (x, z) x3 then encoder 2 (x', z') x3 (TS 36.212 §5.1.3.2.2)
+    tail = {d0[K], d2[K], d1[K + 1], d1[K], d0[K + 1], d2[K + 1],
+            d0[K + 2], d2[K + 2], d1[K + 3], d1[K + 2], d0[K + 3], d2[K + 3]};
+    le1.assign(K, 0);
+    le2.assign(K, 0);
+    llr.assign(K, 0);
+    alpha.resize(8 * (K + 1));
+}
+
+void Tdec::iterate(uint8_t* bits) {
+    const auto& pi = tables(idx).pi;
+    std::vector<int32_t> A(K), Ai(K), tmp(K);
+    // decoder 1: a priori = deinterleaved extrinsic of decoder 2
+    for (uint32_t i = 0; i < K; ++i) tmp[pi[i]] = le2[i];
+    for (uint32_t k = 0; k < K; ++k) A[k] = sys[k] + tmp[k];
+    map_decode(K, A.data(), p1.data(), &tail[0], &tail[3], alpha.data(), llr.data(), le1.data());
+    // decoder 2 on the interleaved sequence
+    for (uint32_t i = 0; i < K; ++i) Ai[i] = sys[pi[i]] + le1[pi[i]];
+    map_decode(K, Ai.data(), p2.data(), &tail[6], &tail[9], alpha.data(), llr.data(), le2.data());
+    for (uint32_t i = 0; i < K; ++i) bits[pi[i]] = llr[i] > 0;
+}
+
+}  // namespace dnrp::fec
+
+// ==== C-ABI =========================================================================================
+using namespace dnrp::fec;
+
+static void pack_bits(const uint8_t* u, uint32_t n, uint8_t* out, uint32_t bit_off) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t b = bit_off + i;
+        if (u[i]) out[b / 8] |= (uint8_t)(0x80 >> (b % 8));
+        else out[b / 8] &= (uint8_t)~(0x80 >> (b % 8));
+    }
+}
+static void unpack_bits(const uint8_t* p, uint32_t bit_off, uint32_t n, uint8_t* u) {
+    for (uint32_t i = 0; i < n; ++i) u[i] = (p[(bit_off + i) / 8] >> (7 - (bit_off + i) % 8)) & 1;
+}
+
+struct dnrp_harq_rx {
+    uint32_t C_max, Kw_max, K_max;
+    std::vector<int16_t> w;      // [C_max][Kw_max] accumulated softbits (softbuffer->buffer_f)
+    std::vector<uint8_t> crc;    // [C_max] code-block CRC ok (softbuffer->cb_crc)
+    std::vector<uint8_t> data;   // [C_max][K_max/8] decoded code blocks kept for retransmissions
+};
+
+static int segm_of(const dnrp_fec_cfg* cfg, Segm* s) {
+    if (!cfg || cfg->N_bps == 0 || cfg->N_TB_bits == 0 || cfg->N_TB_bits % 8 || cfg->rv > 3) return DNRP_EINVAL;
+    if (cbsegm(cfg->N_TB_bits, cfg->Z, s) != 0) return DNRP_ECONFIG;
+    if (s->F != 0) return DNRP_ECONFIG;  // filler bits not supported (pdc_enc.cpp:144)
+    return DNRP_OK;
+}
+
+// E of code block r (pdc_enc.cpp:148-175)
+static uint32_t cb_E(const Segm& s, uint32_t r, uint32_t Qm, uint32_t G) {
+    const uint32_t Gp = G / Qm, gamma = Gp % s.C;
+    return r <= s.C - gamma - 1 ? Qm * (Gp / s.C) : Qm * ((Gp + s.C - 1) / s.C);
+}
+
+extern "C" {
+
+int dnrp_fec_cbsegm(uint32_t N_TB_bits, uint32_t Z, dnrp_cbsegm* out) {
+    if (!out) return DNRP_EINVAL;
+    Segm s;
+    if (cbsegm(N_TB_bits, Z, &s) != 0) return DNRP_ECONFIG;
+    *out = {s.tbs, s.Z, s.C, s.C1, s.C2, s.K1, s.K2, s.K1_idx, s.K2_idx, s.F};
+    return DNRP_OK;
+}
+
+int dnrp_fec_cb_size(uint32_t idx, uint32_t* K, uint32_t* f1, uint32_t* f2) {
+    if (idx >= kNofCbSizes || !K) return DNRP_EINVAL;
+    *K = cb_size(idx);
+    uint32_t a, b;
+    qpp_params(idx, &a, &b);
+    if (f1) *f1 = a;
+    if (f2) *f2 = b;
+    return DNRP_OK;
+}
+
+int dnrp_crc(const uint8_t* data, uint32_t nbits, uint32_t kind, uint32_t* crc) {
+    if (!data || !crc) return DNRP_EINVAL;
+    switch (kind) {
+        case DNRP_CRC16: *crc = crc_bits(data, nbits, kCrc16, 16); break;
+        case DNRP_CRC24A: *crc = crc_bits(data, nbits, kCrc24A, 24); break;
+        case DNRP_CRC24B: *crc = crc_bits(data, nbits, kCrc24B, 24); break;
+        default: return DNRP_EINVAL;
+    }
+    return DNRP_OK;
+}
+
+int dnrp_pcc_encode(const uint8_t* plcf, uint32_t plcf_type, uint32_t closed_loop, uint32_t beamforming,
+                    uint8_t* d) {
+    if (!plcf || !d || (plcf_type != 1 && plcf_type != 2)) return DNRP_EINVAL;
+    const uint32_t nb = plcf_type == 1 ? kPlcfType1Bits : kPlcfType2Bits;
+    uint8_t c_packed[12] = {0};
+    std::memcpy(c_packed, plcf, nb / 8);
+    const uint16_t mask = closed_loop ? (beamforming ? kMaskClBf : kMaskCl) : (beamforming ? kMaskBf : kMaskNone);
+    const uint32_t crc = crc_bits(c_packed, nb, kCrc16, 16) ^ mask;
+    c_packed[nb / 8] = (uint8_t)(crc >> 8);
+    c_packed[nb / 8 + 1] = (uint8_t)crc;
+    const uint32_t idx = (uint32_t)cb_index(nb + 16);  // K = 56 / 96: no filler bits
+    const uint32_t K = cb_size(idx);
+    std::vector<uint8_t> c(K), d0(K + 4), d1(K + 4), d2(K + 4), e(kPccBits);
+    unpack_bits(c_packed, 0, K, c.data());
+    turbo_encode(c.data(), idx, d0.data(), d1.data(), d2.data());
+    rm_tx(d0.data(), d1.data(), d2.data(), idx, kPccBits, 0, e.data());  // rv 0 (TS 103 636-3 §7.5.3)
+    std::memset(d, 0, 25);
+    pack_bits(e.data(), kPccBits, d, 0);
+    return DNRP_OK;
+}
+
+int dnrp_pcc_decode(const int16_t* llr, uint32_t plcf_type_test, uint8_t* plcf, uint32_t* closed_loop,
+                    uint32_t* beamforming, uint32_t* iterations) {
+    if (!llr || !plcf || (plcf_type_test != 1 && plcf_type_test != 2)) return DNRP_EINVAL;
+    const uint32_t nb = plcf_type_test == 1 ? kPlcfType1Bits : kPlcfType2Bits;
+    const uint32_t idx = (uint32_t)cb_index(nb + 16);
+    const uint32_t K = cb_size(idx);
+    std::vector<int16_t> w(rm_kw(idx), 0);
+    rm_rx(llr, idx, kPccBits, 0, w.data());
+    Tdec dec;
+    dec.load(w.data(), idx);
+    std::vector<uint8_t> bits(K);
+    uint8_t packed[12];
+    for (uint32_t it = 1; it <= kPccMaxIter; ++it) {
+        dec.iterate(bits.data());
+        std::memset(packed, 0, sizeof(packed));
+        pack_bits(bits.data(), K, packed, 0);
+        const uint32_t rx = ((uint32_t)packed[nb / 8] << 8) | packed[nb / 8 + 1];
+        const uint32_t re = crc_bits(packed, nb, kCrc16, 16);
+        const uint16_t masks[4] = {kMaskNone, kMaskCl, kMaskBf, kMaskClBf};  // pcc_enc.cpp:329-349
+        for (int m = 0; m < 4; ++m)
+            if ((rx ^ masks[m]) == re) {
+                std::memcpy(plcf, packed, nb / 8);
+                if (closed_loop) *closed_loop = (m & 1) != 0;
+                if (beamforming) *beamforming = (m & 2) != 0;
+                if (iterations) *iterations = it;
+                return 1;
+            }
+    }
+    if (iterations) *iterations = kPccMaxIter;
+    return 0;
+}
+
+int dnrp_pdc_encode(const dnrp_fec_cfg* cfg, const uint8_t* tb, uint8_t* d) {
+    Segm s;
+    int rc = segm_of(cfg, &s);
+    if (rc) return rc;
+    if (!tb || !d) return DNRP_EINVAL;
+    const uint32_t tbs = cfg->N_TB_bits, Qm = cfg->N_bps, G = cfg->G;
+    // b = a || CRC24A (TS 36.212 §5.1.1), segmented K- blocks first (pdc_enc.cpp:159-165)
+    std::vector<uint8_t> b(tbs + 24);
+    unpack_bits(tb, 0, tbs, b.data());
+    const uint32_t tcrc = crc_bits(tb, tbs, kCrc24A, 24);
+    for (int i = 0; i < 24; ++i) b[tbs + i] = (tcrc >> (23 - i)) & 1;
+    std::memset(d, 0, (G + 7) / 8);
+    std::vector<uint8_t> c, d0, d1, d2, e, cpk;
+    uint32_t rp = 0, wp = 0;
+    for (uint32_t r = 0; r < s.C; ++r) {
+        const uint32_t K = r < s.C2 ? s.K2 : s.K1, idx = r < s.C2 ? s.K2_idx : s.K1_idx;
+        const uint32_t rlen = s.C > 1 ? K - 24 : K;
+        c.assign(b.begin() + rp, b.begin() + rp + rlen);
+        if (s.C > 1) {  // code-block CRC24B
+            cpk.assign((rlen + 7) / 8, 0);
+            pack_bits(c.data(), rlen, cpk.data(), 0);
+            const uint32_t cc = crc_bits(cpk.data(), rlen, kCrc24B, 24);
+            for (int i = 0; i < 24; ++i) c.push_back((cc >> (23 - i)) & 1);
+        }
+        d0.resize(K + 4), d1.resize(K + 4), d2.resize(K + 4);
+        turbo_encode(c.data(), idx, d0.data(), d1.data(), d2.data());
+        const uint32_t E = cb_E(s, r, Qm, G);
+        e.resize(E);
+        rm_tx(d0.data(), d1.data(), d2.data(), idx, E, cfg->rv, e.data());
+        pack_bits(e.data(), E, d, wp);
+        rp += rlen;
+        wp += E;
+    }
+    return DNRP_OK;
+}
+
+int dnrp_harq_rx_create(uint32_t N_TB_bits_max, uint32_t Z, dnrp_harq_rx** out) {
+    if (!out) return DNRP_EINVAL;
+    Segm s;
+    if (cbsegm(N_TB_bits_max, Z, &s) != 0 || s.C == 0) return DNRP_ECONFIG;
+    // C of any smaller TB <= C of the largest; size the blocks for the largest code block of Z
+    const int imax = cb_index(std::min<uint32_t>(Z, 6144));
+    if (imax < 0) return DNRP_ECONFIG;
+    auto* h = new dnrp_harq_rx;
+    h->C_max = s.C;
+    h->Kw_max = rm_kw((uint32_t)imax);
+    h->K_max = cb_size((uint32_t)imax);
+    h->w.assign((size_t)h->C_max * h->Kw_max, 0);
+    h->crc.assign(h->C_max, 0);
+    h->data.assign((size_t)h->C_max * (h->K_max / 8), 0);
+    *out = h;
+    return DNRP_OK;
+}
+
+int dnrp_harq_rx_reset(dnrp_harq_rx* h) {
+    if (!h) return DNRP_EINVAL;
+    std::fill(h->w.begin(), h->w.end(), 0);
+    std::fill(h->crc.begin(), h->crc.end(), 0);
+    return DNRP_OK;
+}
+
+int dnrp_harq_rx_destroy(dnrp_harq_rx* h) {
+    delete h;
+    return DNRP_OK;
+}
+
+int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* llr, uint32_t n_llr, uint8_t* tb,
+                    uint32_t* iterations) {
+    Segm s;
+    int rc = segm_of(cfg, &s);
+    if (rc) return rc;
+    if (!llr || !tb || n_llr > cfg->G) return DNRP_EINVAL;
+    std::unique_ptr<dnrp_harq_rx, int (*)(dnrp_harq_rx*)> own(nullptr, dnrp_harq_rx_destroy);
+    if (!hb) {  // one-shot decode: a fresh softbuffer
+        dnrp_harq_rx* h = nullptr;
+        if ((rc = dnrp_harq_rx_create(cfg->N_TB_bits, cfg->Z, &h))) return rc;
+        own.reset(h);
+        hb = h;
+    }
+    if (s.C > hb->C_max || rm_kw(s.K1_idx) > hb->Kw_max) return DNRP_EINVAL;
+    const uint32_t tbs = cfg->N_TB_bits, Qm = cfg->N_bps, G = cfg->G;
+    std::vector<uint8_t> data((tbs + 48 + 7) / 8 + 8, 0), bits;
+    Tdec dec;
+    uint32_t it_total = 0, wp = 0, r = 0;
+    for (; r < s.C; ++r) {
+        const uint32_t K = r < s.C2 ? s.K2 : s.K1, idx = r < s.C2 ? s.K2_idx : s.K1_idx;
+        const uint32_t rlen = s.C == 1 ? K : K - 24;
+        // read positions as srsRAN's decode_tb_cb (pdc_enc.cpp:322-332): the block at index
+        // C - gamma is read with the shorter length although it was written with Qm more bits
+        const uint32_t Gp = G / Qm, gamma = Gp % s.C, n_e = Qm * (Gp / s.C);
+        uint32_t rpos = r * n_e, n_e2 = n_e;
+        if (r > s.C - gamma) {
+            n_e2 = n_e + Qm;
+            rpos = (s.C - gamma) * n_e + (r - (s.C - gamma)) * n_e2;
+        }
+        if (rpos + n_e2 > n_llr) break;  // not enough soft bits yet (pdc_enc.cpp:334-337)
+        int16_t* w = &hb->w[(size_t)r * hb->Kw_max];
+        uint8_t* keep = &hb->data[(size_t)r * (hb->K_max / 8)];
+        if (!hb->crc[r]) {
+            rm_rx(llr + rpos, idx, n_e2, cfg->rv, w);
+            dec.load(w, idx);
+            bits.resize(K);
+            std::vector<uint8_t> pk((K + 7) / 8);
+            for (uint32_t it = 1; it <= kPdcMaxIter; ++it) {
+                dec.iterate(bits.data());
+                ++it_total;
+                std::fill(pk.begin(), pk.end(), 0);
+                pack_bits(bits.data(), K, pk.data(), 0);
+                const bool ok = s.C > 1 ? crc_bits(pk.data(), K, kCrc24B, 24) == 0
+                                        : crc_bits(pk.data(), tbs + 24, kCrc24A, 24) == 0;
+                if (ok && it >= kPdcMinIter) {
+                    hb->crc[r] = 1;
+                    break;
+                }
+            }
+            pack_bits(bits.data(), K, data.data(), wp);
+            if (hb->crc[r]) std::memcpy(keep, pk.data(), rlen / 8);
+        } else {
+            std::vector<uint8_t> kb(rlen);
+            unpack_bits(keep, 0, rlen, kb.data());
+            pack_bits(kb.data(), rlen, data.data(), wp);
+        }
+        wp += rlen;
+    }
+    if (iterations) *iterations = it_total;
+    std::memcpy(tb, data.data(), tbs / 8);
+    if (r < s.C) return 0;
+    for (uint32_t i = 0; i < s.C; ++i)
+        if (!hb->crc[i]) return 0;
+    if (s.C == 1) return 1;
+    // all code blocks passed: check the transport-block CRC (pdc_enc.cpp:478-488)
+    const uint32_t tcrc = crc_bits(data.data(), tbs, kCrc24A, 24);
+    uint32_t rx = 0;
+    for (int i = 0; i < 24; ++i) rx = (rx << 1) | ((data[(tbs + i) / 8] >> (7 - (tbs + i) % 8)) & 1);
+    if (tcrc == rx) return 1;
+    std::fill(hb->crc.begin(), hb->crc.begin() + s.C, 0);  // false alarm: reset the CB CRC flags
+    return 0;
+}
+
+}  // extern "C"

@@ -167,7 +167,9 @@ EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_g
            "dnrp_strerror", "dnrp_get_radio_device_class", "dnrp_query_param", "dnrp_param_name",
            "dnrp_ring_gather", "dnrp_sync_stream_init", "dnrp_sync_stream_window", "dnrp_rx_sync_stream",
            "dnrp_channel_batch", "dnrp_channel_realization", "dnrp_tx_transmit_length", "dnrp_tx_packet_json",
-           "dnrp_rx_packet_json"]
+           "dnrp_rx_packet_json", "dnrp_crc", "dnrp_fec_cbsegm", "dnrp_fec_cb_size", "dnrp_pcc_encode",
+           "dnrp_pcc_decode", "dnrp_pdc_encode", "dnrp_pdc_decode", "dnrp_harq_rx_create", "dnrp_harq_rx_reset",
+           "dnrp_harq_rx_destroy"]
 
 _lib = None
 

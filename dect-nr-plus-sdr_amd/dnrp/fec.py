@@ -1,0 +1,143 @@
+"""Host channel coding of libdnrp.so (include/dnrp.h, csrc/host/fec.cpp) — the reference's fec_t
+(lib/src/phy/fec/fec.cpp:28-148) without the scrambling, which the GPU path applies:
+
+  pcc_encode  <- fec_t::encode_plcf      (pcc_enc.cpp:145-208)
+  pcc_decode  <- fec_t::decode_plcf_test (pcc_enc.cpp:215-364)
+  pdc_encode  <- fec_t::encode_tb        (pdc_enc.cpp:127-229)
+  pdc_decode  <- fec_t::decode_tb        (pdc_enc.cpp:291-492), HarqRx <- harq::buffer_rx_t
+  cbsegm      <- sp3::fix::srsran_cbsegm_FIX (sections_part3/fix/cbsegm.cpp:65-123)
+
+Bits are numpy uint8 arrays packed MSB first, LLRs numpy int16 (positive = bit 1).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import DnrpError, lib as _lib
+
+CRC16, CRC24A, CRC24B = 0, 1, 2
+P = C.c_void_p
+
+
+class CbSegm(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("tbs", "Z", "C", "C1", "C2", "K1", "K2", "K1_idx", "K2_idx", "F")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+class FecCfg(C.Structure):
+    """sp3::fec_cfg_t (sections_part3/derivative/fec_cfg.hpp)"""
+    _fields_ = [(n, C.c_uint32) for n in ("PLCF_type", "closed_loop", "beamforming", "N_TB_bits", "N_bps", "rv", "G",
+                                         "network_id", "Z")]
+
+
+_ready = False
+
+
+def lib():
+    global _ready
+    L = _lib()
+    if not _ready:
+        u32p = C.POINTER(C.c_uint32)
+        L.dnrp_crc.argtypes = [P, C.c_uint32, C.c_uint32, u32p]
+        L.dnrp_fec_cbsegm.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(CbSegm)]
+        L.dnrp_fec_cb_size.argtypes = [C.c_uint32, u32p, u32p, u32p]
+        L.dnrp_pcc_encode.argtypes = [P, C.c_uint32, C.c_uint32, C.c_uint32, P]
+        L.dnrp_pcc_decode.argtypes = [P, C.c_uint32, P, u32p, u32p, u32p]
+        L.dnrp_pdc_encode.argtypes = [C.POINTER(FecCfg), P, P]
+        L.dnrp_pdc_decode.argtypes = [P, C.POINTER(FecCfg), P, C.c_uint32, P, u32p]
+        L.dnrp_harq_rx_create.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(P)]
+        L.dnrp_harq_rx_reset.argtypes = [P]
+        L.dnrp_harq_rx_destroy.argtypes = [P]
+        _ready = True
+    return L
+
+
+def _chk(rc, what):
+    if rc < 0:
+        raise DnrpError(rc, what)
+    return rc
+
+
+def _ptr(a):
+    return a.ctypes.data_as(P)
+
+
+def crc(data, nbits, kind):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    assert data.size * 8 >= nbits
+    out = C.c_uint32()
+    _chk(lib().dnrp_crc(_ptr(data), nbits, kind, C.byref(out)), "dnrp_crc")
+    return out.value
+
+
+def cbsegm(N_TB_bits, Z):
+    out = CbSegm()
+    _chk(lib().dnrp_fec_cbsegm(N_TB_bits, Z, C.byref(out)), "dnrp_fec_cbsegm")
+    return out.as_dict()
+
+
+def cb_size(idx):
+    K, f1, f2 = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    _chk(lib().dnrp_fec_cb_size(idx, C.byref(K), C.byref(f1), C.byref(f2)), "dnrp_fec_cb_size")
+    return K.value, f1.value, f2.value
+
+
+def pcc_encode(plcf, plcf_type, closed_loop=False, beamforming=False):
+    plcf = np.ascontiguousarray(plcf, dtype=np.uint8)
+    assert plcf.size == (5 if plcf_type == 1 else 10)
+    d = np.zeros(25, np.uint8)
+    _chk(lib().dnrp_pcc_encode(_ptr(plcf), plcf_type, int(closed_loop), int(beamforming), _ptr(d)), "dnrp_pcc_encode")
+    return d
+
+
+def pcc_decode(llr, plcf_type_test):
+    """-> (ok, plcf bytes, closed_loop, beamforming, iterations)"""
+    llr = np.ascontiguousarray(llr, dtype=np.int16)
+    assert llr.size == 196
+    plcf = np.zeros(10, np.uint8)
+    cl, bf, it = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    ok = _chk(lib().dnrp_pcc_decode(_ptr(llr), plcf_type_test, _ptr(plcf), C.byref(cl), C.byref(bf), C.byref(it)),
+              "dnrp_pcc_decode")
+    return bool(ok), plcf[:5 if plcf_type_test == 1 else 10], bool(cl.value), bool(bf.value), it.value
+
+
+def fec_cfg(N_TB_bits, N_bps, G, Z=6144, rv=0, PLCF_type=1, network_id=0):
+    return FecCfg(PLCF_type, 0, 0, N_TB_bits, N_bps, rv, G, network_id, Z)
+
+
+def pdc_encode(cfg, tb):
+    tb = np.ascontiguousarray(tb, dtype=np.uint8)
+    assert tb.size == cfg.N_TB_bits // 8
+    d = np.zeros((cfg.G + 7) // 8, np.uint8)
+    _chk(lib().dnrp_pdc_encode(C.byref(cfg), _ptr(tb), _ptr(d)), "dnrp_pdc_encode")
+    return d
+
+
+class HarqRx:
+    """harq::buffer_rx_t: softbuffer kept across redundancy versions of one transport block"""
+
+    def __init__(self, N_TB_bits_max, Z=6144):
+        self.h = P()
+        _chk(lib().dnrp_harq_rx_create(N_TB_bits_max, Z, C.byref(self.h)), "dnrp_harq_rx_create")
+
+    def reset(self):
+        _chk(lib().dnrp_harq_rx_reset(self.h), "dnrp_harq_rx_reset")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().dnrp_harq_rx_destroy(self.h)
+            self.h = None
+
+
+def pdc_decode(cfg, llr, hb=None, n_llr=None):
+    """-> (crc ok, tb bytes, turbo iterations)"""
+    llr = np.ascontiguousarray(llr, dtype=np.int16)
+    n_llr = cfg.G if n_llr is None else n_llr
+    assert llr.size >= n_llr
+    tb = np.zeros(cfg.N_TB_bits // 8, np.uint8)
+    it = C.c_uint32()
+    ok = _chk(lib().dnrp_pdc_decode(hb.h if hb else None, C.byref(cfg), _ptr(llr), n_llr, _ptr(tb), C.byref(it)),
+              "dnrp_pdc_decode")
+    return bool(ok), tb, it.value

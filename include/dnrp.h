@@ -360,6 +360,61 @@ const char* dnrp_param_name(uint32_t index);
 int dnrp_last_kernel_ms(const dnrp_ctx* ctx, const char* name, float* ms);
 int dnrp_kernel_time_total(dnrp_ctx* ctx, const char* name, float* total_ms, uint32_t* count, int reset);
 
+/*
+ * Channel coding (host only) <- phy/fec/fec.cpp (fec_t), pcc_enc.cpp, pdc_enc.cpp and
+ * sections_part3/fix/cbsegm.cpp: CRC attachment, code-block segmentation, LTE turbo code (TS 36.212
+ * §5.1.3, QPP interleaver), turbo rate matching (§5.1.4.1) and a max-log-MAP turbo decoder with
+ * CRC early stopping. The split with the GPU path is the reference's scrambler: the encoders output
+ * the rate-matched d-bits dnrp_tx_batch takes (pcc_d / pdc_d: unscrambled, MSB first) and the
+ * decoders take the descrambled int16 LLRs dnrp_rx_pcc_batch / dnrp_rx_pdc_batch return.
+ */
+#define DNRP_CRC16 0   /* PLCF CRC, g = 0x1021 (pcc_enc.cpp:88-91) */
+#define DNRP_CRC24A 1  /* transport-block CRC, g = 0x864CFB (pdc_enc.cpp:60-63) */
+#define DNRP_CRC24B 2  /* code-block CRC, g = 0x800063 (pdc_enc.cpp:56-59) */
+
+/* srsran_cbsegm_t as filled by srsran_cbsegm_FIX (cbsegm.cpp:65-123): C2 blocks of K2 first */
+typedef struct {
+    uint32_t tbs, Z, C, C1, C2, K1, K2, K1_idx, K2_idx, F;
+} dnrp_cbsegm;
+
+/* sp3::fec_cfg_t (sections_part3/derivative/fec_cfg.hpp). PLCF_type and network_id select the
+ * scrambling sequence, which the GPU path applies: they are carried for the mirror only. */
+typedef struct {
+    uint32_t PLCF_type, closed_loop, beamforming, N_TB_bits, N_bps, rv, G, network_id, Z;
+} dnrp_fec_cfg;
+
+/* HARQ RX softbuffer (harq::buffer_rx_t): accumulated code-block softbits, code-block CRC flags
+ * and the code blocks already decoded, kept across redundancy versions of one transport block. */
+typedef struct dnrp_harq_rx dnrp_harq_rx;
+
+int dnrp_crc(const uint8_t* data, uint32_t nbits, uint32_t kind, uint32_t* crc);
+int dnrp_fec_cbsegm(uint32_t N_TB_bits, uint32_t Z, dnrp_cbsegm* out);
+/* row idx (0..187) of TS 36.212 Table 5.1.3-3: K and the QPP coefficients f1, f2 (optional) */
+int dnrp_fec_cb_size(uint32_t idx, uint32_t* K, uint32_t* f1, uint32_t* f2);
+
+/* fec_t::encode_plcf without the scrambling: plcf (5 or 10 bytes) -> d [25] bytes (196 bits).
+ * closed_loop / beamforming select the CRC mask (pcc_enc.cpp:170-183). */
+int dnrp_pcc_encode(const uint8_t* plcf, uint32_t plcf_type, uint32_t closed_loop, uint32_t beamforming, uint8_t* d);
+/* fec_t::decode_plcf_test after the descrambling: llr [196] -> 1 if a PLCF of plcf_type_test passed
+ * its CRC under one of the four masks (plcf [5 or 10], closed_loop, beamforming set), 0 if not.
+ * Up to 5 turbo iterations, stopping at the first CRC match (pcc_enc.cpp:309-351). */
+int dnrp_pcc_decode(const int16_t* llr, uint32_t plcf_type_test, uint8_t* plcf, uint32_t* closed_loop,
+                    uint32_t* beamforming, uint32_t* iterations);
+
+/* fec_t::encode_tb without the scrambling: tb [N_TB_bits/8] -> d [ceil(G/8)] (redundancy version
+ * cfg->rv). DNRP_ECONFIG for a segmentation with filler bits (pdc_enc.cpp:144). */
+int dnrp_pdc_encode(const dnrp_fec_cfg* cfg, const uint8_t* tb, uint8_t* d);
+/* fec_t::decode_tb after the descrambling: the first n_llr <= G LLRs of the packet (code blocks
+ * whose soft bits are not all present yet are left for a later call, pdc_enc.cpp:334-337) ->
+ * tb [N_TB_bits/8]. Returns 1 if the transport block passed its CRC(s), 0 if not. hb: the HARQ
+ * softbuffer to combine into (reset it for a new transport block), or NULL for a one-shot decode.
+ * Up to 10 iterations per code block, CRC early stop after at least 2. */
+int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* llr, uint32_t n_llr, uint8_t* tb,
+                    uint32_t* iterations);
+int dnrp_harq_rx_create(uint32_t N_TB_bits_max, uint32_t Z, dnrp_harq_rx** out);
+int dnrp_harq_rx_reset(dnrp_harq_rx* hb);
+int dnrp_harq_rx_destroy(dnrp_harq_rx* hb);
+
 const char* dnrp_strerror(int code);
 
 #ifdef __cplusplus
