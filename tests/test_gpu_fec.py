@@ -1,0 +1,90 @@
+"""End-to-end loopback with channel coding (SURVEY.md §8(f) row 1, C1's purpose): PLCF and transport
+blocks are FEC-encoded on the host (dnrp.fec <- fec_t::encode_plcf / encode_tb), transmitted by the
+GPU TX (dnrp_tx_batch), passed through a random MIMO channel with CFO and AWGN, demodulated by the
+GPU RX (dnrp_rx_pcc_batch / dnrp_rx_pdc_batch) and decoded on the host (fec_t::decode_plcf_test /
+decode_tb), as worker_tx_rx_t does per packet (worker_tx_rx.cpp:126-201). Checks: every PLCF and
+transport block passes its CRC with the transmitted contents at SNRs well above threshold, the
+closed-loop/beamforming CRC mask is recovered, and at an SNR far below threshold every CRC fails
+(no false passes) — for the GPU LLRs and for the oracle RX's LLRs of the same windows alike."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+import phy_fixtures as PF
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+# (psdef u, b, PacketLengthType, PacketLength, tm, mcs), (u_max, b_max, N_TX, os_min, L, M)
+LOOPS = {
+    "C2_siso_mcs1": ((1, 1, 1, 1, 0, 1), (1, 1, 1, 1, 10, 9)),
+    "1.1.1.A_mcs4": ((1, 1, 1, 2, 0, 4), (1, 1, 1, 1, 10, 9)),
+    "u2b4_tm5_mcs6": ((2, 4, 1, 1, 5, 6), (2, 4, 4, 1, 10, 9)),
+    "u2b4_mrc2_mcs3": ((2, 4, 1, 2, 0, 3), (2, 4, 2, 1, 10, 9)),
+}
+
+
+def _loop(name, snr_db, n=4, seed=1):
+    import dnrp
+    import dnrp.fec as FE
+    ps_t, cf = LOOPS[name]
+    u_max, b_max, ntx, os_min, L, M = cf
+    phy = dnrp.Phy(u_max, b_max, ntx, os_min, L, M, max_batch=n)
+    for nid in range(100, 106):
+        phy.add_network_id(nid)
+    ps = dnrp.psdef(*ps_t)
+    sz = phy.packet_sizes(ps)
+    S = sz["N_samples_packet_os_rs"]
+    rng = np.random.default_rng(seed)
+    plcf_types = [1 + i % 2 for i in range(n)]
+    plcfs = [rng.integers(0, 256, 5 * t, dtype=np.uint8) for t in plcf_types]
+    masks = [(i % 2, (i // 2) % 2) for i in range(n)]
+    tbs = [rng.integers(0, 256, sz["N_TB_bits"] // 8, dtype=np.uint8) for _ in range(n)]
+    fcfg = FE.fec_cfg(sz["N_TB_bits"], sz["N_bps"], sz["G"], Z=6144)
+    pcc = np.stack([FE.pcc_encode(plcfs[i], plcf_types[i], *masks[i]) for i in range(n)])
+    pdc = np.stack([FE.pdc_encode(fcfg, tbs[i]) for i in range(n)])
+    dev = torch.device("cuda:0")
+    descs = [dnrp.TxDesc(0, 100 + i, plcf_types[i], 5, 1.0, 0.0, 0.0, 0) for i in range(n)]
+    out = torch.empty((n, sz["N_TX"], S, 2), dtype=torch.float32, device=dev)
+    phy.tx_batch(ps, descs, torch.from_numpy(pcc).to(dev), torch.from_numpy(pdc).to(dev), out)
+    phy.sync()
+    iq_tx = out.cpu().numpy().view(np.complex64)[..., 0]
+    windows, reports = [], []
+    for i in range(n):
+        off = int(rng.integers(0, 32))
+        cfo = rng.uniform(-1.5, 1.5) * 2 * np.pi / sz["N_b_DFT_os"]
+        windows.append(PF.channel(rng, iq_tx[i], ntx, S, off, cfo * M / L, snr_db))
+        reports.append(dnrp.SyncReport(off, float(-cfo), 0.0, ps_t[0], ps_t[1], sz["N_eff_TX"]))
+    iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(n, ntx, S, 2)).to(dev)
+    pcc_llr = torch.zeros((n, 196), dtype=torch.int16, device=dev)
+    pdc_llr = torch.zeros((n, sz["G"]), dtype=torch.int16, device=dev)
+    phy.rx_pcc_batch(reports, iq, pcc_llr)
+    phy.rx_pdc_batch([dnrp.PdcReq(ps, i, 100 + i, plcf_types[i]) for i in range(n)], iq, pdc_llr)
+    phy.sync()
+    g_pcc, g_pdc = pcc_llr.cpu().numpy(), pdc_llr.cpu().numpy()
+    ocf = O.cfg(u_max, b_max, os_min, L, M)
+    ops = O.psdef(*ps_t)
+    res = []
+    for i in range(n):
+        r = O.rx(ocf, ops, windows[i], reports[i].fine_peak_time, float(np.float32(reports[i].cfo_fractional_rad)),
+                 100 + i, plcf_types[i])
+        for src, lp, ld in (("gpu", g_pcc[i], g_pdc[i]), ("oracle", r["pcc_llr"], r["pdc_llr"])):
+            ok_c, got_plcf, cl, bf, _ = FE.pcc_decode(lp, plcf_types[i])
+            ok_d, got_tb, _ = FE.pdc_decode(fcfg, ld)
+            res.append((src, i, ok_c, ok_c and (got_plcf == plcfs[i]).all() and (cl, bf) == tuple(map(bool, masks[i])),
+                        ok_d, ok_d and (got_tb == tbs[i]).all()))
+    return res
+
+
+@pytest.mark.parametrize("name", sorted(LOOPS))
+def test_fec_loopback_crc_pass(name):
+    for src, i, ok_c, good_c, ok_d, good_d in _loop(name, 30.0):
+        assert ok_c and good_c, (name, src, i, "PLCF")
+        assert ok_d and good_d, (name, src, i, "TB")
+
+
+def test_fec_loopback_crc_fail_far_below_threshold():
+    for src, i, ok_c, good_c, ok_d, good_d in _loop("u2b4_tm5_mcs6", -8.0, seed=2):
+        assert not ok_d, (src, i)           # 64-QAM rate-3/4-class TB at -8 dB: undecodable
+        assert ok_c == good_c, (src, i)     # a PLCF CRC pass must carry the transmitted PLCF
