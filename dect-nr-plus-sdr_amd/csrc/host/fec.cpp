@@ -15,7 +15,9 @@
 #include <memory>
 #include <mutex>
 
+#include "ctx_internal.hpp"
 #include "dnrp.h"
+#include "fec_dev.hpp"
 
 namespace dnrp::fec {
 
@@ -107,6 +109,27 @@ static const SizeTables& tables(uint32_t idx) {
 }
 
 const std::vector<uint32_t>& qpp(uint32_t idx) { return tables(idx).pi; }
+
+static uint32_t rm_k0(const SizeTables& t, uint32_t rv);
+
+// circular-buffer list of a size (non-dummy positions in buffer order: stream << 16 | index) and
+// the list index where soft bit 0 of redundancy version rv lands
+static std::vector<uint32_t> valid_list(uint32_t idx) {
+    const SizeTables& t = tables(idx);
+    const uint32_t D = cb_size(idx) + 4;
+    std::vector<uint32_t> v;
+    v.reserve(3 * D);
+    for (int32_t m : t.wmap)
+        if (m >= 0) v.push_back(((uint32_t)m / D) << 16 | ((uint32_t)m % D));
+    return v;
+}
+static uint32_t valid_start(uint32_t idx, uint32_t rv) {
+    const SizeTables& t = tables(idx);
+    const uint32_t k0 = rm_k0(t, rv) % (3 * t.Kpi);
+    uint32_t n = 0;
+    for (uint32_t pos = 0; pos < k0; ++pos) n += t.wmap[pos] >= 0;
+    return n;
+}
 
 int cbsegm(uint32_t tbs, uint32_t Z, Segm* s) {
     std::memset(s, 0, sizeof(*s));
@@ -310,7 +333,7 @@ static void map_decode(uint32_t K, const int32_t* A, const int32_t* B, const int
         }
         llr[k] = m1 - m0;
         const int32_t e = llr[k] - A[k];
-        le[k] = std::min(1 << 20, std::max(-(1 << 20), (e * 3) >> 2));  // extrinsic scaled by 3/4
+        le[k] = std::min(32767, std::max(-32767, (e * 3) >> 2));  // extrinsic x3/4, int16 range
         int32_t mx = bn[0];
         for (int s = 1; s < 8; ++s) mx = std::max(mx, bn[s]);
         for (int s = 0; s < 8; ++s) be[s] = std::max(bn[s] - mx, kNeg);
@@ -607,3 +630,168 @@ int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* ll
 }
 
 }  // extern "C"
+
+// ---- device turbo decoding -----------------------------------------------------------------------
+static int fec_tables(dnrp_ctx* ctx) {
+    if (!ctx->fec_valid_off.empty()) return DNRP_OK;
+    std::vector<uint32_t> tab, voff(kNofCbSizes), poff(kNofCbSizes), ioff(kNofCbSizes), st(kNofCbSizes * 4);
+    for (uint32_t idx = 0; idx < kNofCbSizes; ++idx) {
+        const auto v = valid_list(idx);
+        voff[idx] = (uint32_t)tab.size();
+        tab.insert(tab.end(), v.begin(), v.end());
+        const auto& pi = tables(idx).pi;
+        poff[idx] = (uint32_t)tab.size();
+        tab.insert(tab.end(), pi.begin(), pi.end());
+        ioff[idx] = (uint32_t)tab.size();
+        tab.resize(tab.size() + pi.size());
+        for (uint32_t i = 0; i < pi.size(); ++i) tab[ioff[idx] + pi[i]] = i;
+        for (uint32_t rv = 0; rv < 4; ++rv) st[idx * 4 + rv] = valid_start(idx, rv);
+    }
+    if (!ctx->fec_tab.upload(tab)) return DNRP_ENOMEM;
+    ctx->fec_valid_off = voff, ctx->fec_pi_off = poff, ctx->fec_pinv_off = ioff, ctx->fec_start = st;
+    return DNRP_OK;
+}
+
+extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr,
+                                     uint32_t llr_stride, uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok,
+                                     uint32_t* iterations, void* stream) {
+    using namespace dnrp::dev;
+    if (!ctx || (m && (!cfg || !llr || !tb || !crc_ok))) return DNRP_EINVAL;
+    if (m == 0) return DNRP_OK;
+    (void)hipSetDevice(ctx->cfg.device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rc = fec_tables(ctx);
+    if (rc) return rc;
+    // plan: code blocks of every packet (pdc_enc.cpp:316-332), grouped by size
+    std::vector<Segm> sg(m);
+    std::vector<std::vector<FecCb>> by_idx(kNofCbSizes);
+    std::vector<std::vector<uint32_t>> pkt_of(kNofCbSizes);
+    for (uint32_t i = 0; i < m; ++i) {
+        if ((rc = segm_of(&cfg[i], &sg[i]))) return rc;
+        const Segm& g = sg[i];
+        const uint32_t tbs = cfg[i].N_TB_bits, Qm = cfg[i].N_bps, G = cfg[i].G;
+        if (llr_stride < G || tb_stride < tbs / 8 + 3) return DNRP_EINVAL;
+        const uint32_t Gp = G / Qm, gamma = Gp % g.C, n_e = Qm * (Gp / g.C);
+        uint32_t wp = 0;
+        for (uint32_t r = 0; r < g.C; ++r) {
+            const uint32_t K = r < g.C2 ? g.K2 : g.K1, idx = r < g.C2 ? g.K2_idx : g.K1_idx;
+            uint32_t rpos = r * n_e, n_e2 = n_e;
+            if (r > g.C - gamma) {
+                n_e2 = n_e + Qm;
+                rpos = (g.C - gamma) * n_e + (r - (g.C - gamma)) * n_e2;
+            }
+            FecCb cb{};
+            cb.llr_off = (uint64_t)i * llr_stride + rpos;
+            cb.tb_off = (uint64_t)i * tb_stride + wp / 8;
+            cb.E = n_e2;
+            cb.start = ctx->fec_start[idx * 4 + cfg[i].rv];
+            cb.poly = g.C > 1 ? kCrc24B : kCrc24A;
+            cb.out_bytes = g.C > 1 ? (K - 24) / 8 : K / 8;
+            by_idx[idx].push_back(cb);
+            pkt_of[idx].push_back(i);
+            wp += g.C > 1 ? K - 24 : K;
+        }
+    }
+    std::vector<FecCb> cbs;
+    std::vector<uint32_t> cb_pkt;
+    std::vector<FecWave> waves;
+    std::vector<uint32_t> grp_first_wave{0}, grp_first_cb{0};
+    uint64_t data = 0, ck = 0;
+    const uint64_t kMaxGroupBytes = 3ull << 30;
+    for (uint32_t idx = 0; idx < kNofCbSizes; ++idx) {
+        const auto& v = by_idx[idx];
+        const uint32_t K = cb_size(idx);
+        const uint64_t wave_bytes = (uint64_t)K * 64 * 5 * 3 + (uint64_t)(K / FEC_WIN) * 8 * 64 * 4;
+        for (size_t c0 = 0; c0 < v.size(); c0 += 64) {
+            if (data * 3 + ck * 4 + wave_bytes > kMaxGroupBytes) {  // start a new group (work16 + bits + ck)
+                grp_first_wave.push_back((uint32_t)waves.size());
+                grp_first_cb.push_back((uint32_t)cbs.size());
+                data = ck = 0;
+            }
+            FecWave w{};
+            w.data_off = data, w.ck_off = ck, w.K = K;
+            w.n = (uint32_t)std::min<size_t>(64, v.size() - c0);
+            w.valid_off = ctx->fec_valid_off[idx], w.pi_off = ctx->fec_pi_off[idx], w.pinv_off = ctx->fec_pinv_off[idx];
+            w.first_cb = (uint32_t)cbs.size() - grp_first_cb.back();
+            const uint32_t wrel = (uint32_t)waves.size() - grp_first_wave.back();
+            for (uint32_t l = 0; l < w.n; ++l) {
+                FecCb cb = v[c0 + l];
+                cb.wave = wrel, cb.lane = l;
+                cbs.push_back(cb);
+                cb_pkt.push_back(pkt_of[idx][c0 + l]);
+            }
+            waves.push_back(w);
+            data += (uint64_t)5 * K * 64;
+            ck += (uint64_t)(K / FEC_WIN) * 8 * 64;
+        }
+    }
+    grp_first_wave.push_back((uint32_t)waves.size());
+    grp_first_cb.push_back((uint32_t)cbs.size());
+    // per-group scratch sized for the largest group
+    uint64_t max_data = 0, max_ck = 0;
+    for (size_t g = 0; g + 1 < grp_first_wave.size(); ++g) {
+        const uint32_t w1 = grp_first_wave[g + 1] - 1;
+        if (grp_first_wave[g + 1] == grp_first_wave[g]) continue;
+        max_data = std::max<uint64_t>(max_data, waves[w1].data_off + (uint64_t)5 * waves[w1].K * 64);
+        max_ck = std::max<uint64_t>(max_ck, waves[w1].ck_off + (uint64_t)(waves[w1].K / FEC_WIN) * 8 * 64);
+    }
+    const uint32_t n_grp_waves_max = [&] {
+        uint32_t mx = 0;
+        for (size_t g = 0; g + 1 < grp_first_wave.size(); ++g) mx = std::max(mx, grp_first_wave[g + 1] - grp_first_wave[g]);
+        return mx;
+    }();
+    if (!ctx->fec_cbs.upload(cbs) || !ctx->fec_waves.upload(waves) || !ctx->fec_work16.ensure(max_data * 2) ||
+        !ctx->fec_bits.ensure(max_data) || !ctx->fec_ck.ensure(max_ck * 4 + 16) ||
+        !ctx->fec_tail.ensure((size_t)n_grp_waves_max * 12 * 64 * 4 + 16) || !ctx->fec_cbout.ensure(cbs.size() * 4 + 16))
+        return DNRP_ENOMEM;
+    for (size_t g = 0; g + 1 < grp_first_wave.size(); ++g) {
+        FecArgs A{};
+        A.llr = llr, A.tb = tb, A.tab = ctx->fec_tab.as<uint32_t>();
+        A.cbs = ctx->fec_cbs.as<FecCb>() + grp_first_cb[g];
+        A.waves = ctx->fec_waves.as<FecWave>() + grp_first_wave[g];
+        A.work16 = ctx->fec_work16.as<int16_t>(), A.tail = ctx->fec_tail.as<int32_t>();
+        A.bits = ctx->fec_bits.as<uint8_t>(), A.ck = ctx->fec_ck.as<int32_t>();
+        A.cb_out = ctx->fec_cbout.as<uint32_t>() + grp_first_cb[g];
+        A.n_cb = grp_first_cb[g + 1] - grp_first_cb[g];
+        A.max_iter = kPdcMaxIter, A.min_iter = kPdcMinIter;
+        ctx->tic("fec_dematch", s);
+        if (launch_fec_dematch(A, s)) return DNRP_EDEVICE;
+        ctx->toc("fec_dematch", s);
+        ctx->tic("fec_tdec", s);
+        if (launch_fec_tdec(A, grp_first_wave[g + 1] - grp_first_wave[g], s)) return DNRP_EDEVICE;
+        ctx->toc("fec_tdec", s);
+    }
+    // transport-block CRC of the packets with several code blocks
+    std::vector<uint64_t> tb_off;
+    std::vector<uint32_t> nbytes, multi;
+    for (uint32_t i = 0; i < m; ++i)
+        if (sg[i].C > 1) tb_off.push_back((uint64_t)i * tb_stride), nbytes.push_back(cfg[i].N_TB_bits / 8), multi.push_back(i);
+    const size_t nm = multi.size();
+    std::vector<uint8_t> argbuf(nm * 12 + nm * 4 + 16);
+    if (nm) {
+        std::memcpy(argbuf.data(), tb_off.data(), nm * 8);
+        std::memcpy(argbuf.data() + nm * 8, nbytes.data(), nm * 4);
+        if (!ctx->fec_tbarg.upload(argbuf)) return DNRP_ENOMEM;
+        FecTbArgs T{};
+        T.tb = tb, T.tb_off = ctx->fec_tbarg.as<uint64_t>();
+        T.nbytes = reinterpret_cast<const uint32_t*>(ctx->fec_tbarg.as<uint8_t>() + nm * 8);
+        T.ok = reinterpret_cast<uint32_t*>(ctx->fec_tbarg.as<uint8_t>() + nm * 12);
+        T.n = (uint32_t)nm;
+        if (launch_fec_tbcrc(T, s)) return DNRP_EDEVICE;
+    }
+    std::vector<uint32_t> cb_out(cbs.size()), tb_ok(nm);
+    HIPCHK(hipMemcpyAsync(cb_out.data(), ctx->fec_cbout.p, cbs.size() * 4, hipMemcpyDeviceToHost, s));
+    if (nm) HIPCHK(hipMemcpyAsync(tb_ok.data(), ctx->fec_tbarg.as<uint8_t>() + nm * 12, nm * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<uint32_t> it(m, 0);
+    for (uint32_t i = 0; i < m; ++i) crc_ok[i] = 1;
+    for (size_t c = 0; c < cbs.size(); ++c) {
+        it[cb_pkt[c]] += cb_out[c] >> 1;
+        if (!(cb_out[c] & 1)) crc_ok[cb_pkt[c]] = 0;
+    }
+    for (size_t j = 0; j < nm; ++j)
+        if (!tb_ok[j]) crc_ok[multi[j]] = 0;
+    if (iterations)
+        for (uint32_t i = 0; i < m; ++i) iterations[i] = it[i];
+    return DNRP_OK;
+}

@@ -1,0 +1,264 @@
+// Batched turbo decoding of PDC code blocks on gfx950 (see fec_dev.hpp). Three kernels:
+//   fec_dematch_kernel  workgroup = code block: rate de-matching (srsran_rm_turbo_rx_lut_ role,
+//                       pdc_enc.cpp:359-360) straight into the wave's [k][lane] soft streams
+//   fec_tdec_kernel     wavefront = up to 64 code blocks of one size K, lane = code block: the
+//                       iterations of the host decoder (fec.cpp Tdec / map_decode) with CRC early stop
+//   fec_tbcrc_kernel    wavefront = packet with C > 1: transport-block CRC24A (pdc_enc.cpp:478-488),
+//                       segment CRCs per lane joined by GF(2) shifts
+#include "fec_dev.hpp"
+
+namespace dnrp::dev {
+
+__global__ void __launch_bounds__(256) fec_dematch_kernel(FecArgs A) {
+    const FecCb cb = A.cbs[blockIdx.x];
+    const FecWave w = A.waves[cb.wave];
+    const uint32_t K = w.K, nvalid = 3 * (K + 4), l = cb.lane;
+    const uint32_t* valid = A.tab + w.valid_off;
+    int16_t* base = A.work16 + w.data_off;
+    const int16_t* llr = A.llr + cb.llr_off;
+    // tail slot of (stream, t = index - K), as fec.cpp Tdec::load orders them
+    const uint8_t tslot[3][4] = {{0, 4, 6, 10}, {3, 2, 9, 8}, {1, 5, 7, 11}};
+    for (uint32_t q = threadIdx.x; q < nvalid; q += blockDim.x) {
+        // soft bits j = j0, j0 + nvalid, ... land on list entry q; summed in j order with int16
+        // saturation like the host's sequential accumulation
+        uint32_t j = q >= cb.start ? q - cb.start : q + nvalid - cb.start;
+        int32_t sum = 0;
+        for (; j < cb.E; j += nvalid) sum = min(32767, max(-32768, sum + (int32_t)llr[j]));
+        const uint32_t e = valid[q], st = e >> 16, idx = e & 0xFFFF;
+        if (idx < K) base[(size_t)st * K * 64 + (size_t)idx * 64 + l] = (int16_t)sum;
+        else A.tail[(size_t)cb.wave * 12 * 64 + tslot[st][idx - K] * 64 + l] = sum;
+    }
+    int16_t* le2 = base + (size_t)4 * K * 64;
+    for (uint32_t k = threadIdx.x; k < K; k += blockDim.x) le2[(size_t)k * 64 + l] = 0;
+}
+
+// One trellis step of the forward recursion (state s = 4 s1 + 2 s2 + s3; next n = (a, s1, s2),
+// predecessors s = (s1, s2, s3) for s3 = 0, 1 with input u = a ^ s2 ^ s3, parity p = a ^ s1 ^ s3).
+__device__ __forceinline__ void fwd_step(int32_t (&a)[8], int32_t A, int32_t B) {
+    int32_t nxt[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+        const int an = n >> 2, s1 = (n >> 1) & 1, s2 = n & 1;
+        int32_t best = FEC_NEG;
+#pragma unroll
+        for (int s3 = 0; s3 < 2; ++s3) {
+            const int s = (s1 << 2) | (s2 << 1) | s3;
+            const int u = an ^ s2 ^ s3, p = an ^ s1 ^ s3;
+            best = max(best, a[s] + (u ? A : 0) + (p ? B : 0));
+        }
+        nxt[n] = best;
+    }
+    int32_t mx = nxt[0];
+#pragma unroll
+    for (int n = 1; n < 8; ++n) mx = max(mx, nxt[n]);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) a[n] = max(nxt[n] - mx, FEC_NEG);
+}
+
+template <int DEC>
+__device__ __forceinline__ void inputs(const FecArgs& A, const FecWave& w, const int16_t* base, uint32_t k, uint32_t l,
+                                       int32_t* a, int32_t* b) {
+    const uint32_t K = w.K;
+    const int16_t *sys = base, *p1 = base + (size_t)K * 64, *p2 = base + (size_t)2 * K * 64;
+    const int16_t *le1 = base + (size_t)3 * K * 64, *le2 = base + (size_t)4 * K * 64;
+    if (DEC == 1) {
+        const uint32_t j = A.tab[w.pinv_off + k];
+        *a = (int32_t)sys[(size_t)k * 64 + l] + le2[(size_t)j * 64 + l];
+        *b = p1[(size_t)k * 64 + l];
+    } else {
+        const uint32_t j = A.tab[w.pi_off + k];
+        *a = (int32_t)sys[(size_t)j * 64 + l] + le1[(size_t)j * 64 + l];
+        *b = p2[(size_t)k * 64 + l];
+    }
+}
+
+// One constituent decoder (fec.cpp map_decode): forward pass with checkpoints, backward pass with
+// the windows' forward metrics recomputed in registers; extrinsic out (and, for decoder 2, the
+// hard decisions of the full LLR at the de-interleaved positions).
+template <int DEC>
+__device__ void map_decode(const FecArgs& A, const FecWave& w, int16_t* base, uint32_t l) {
+    const uint32_t K = w.K, nw = K / FEC_WIN;
+    int32_t* ck = A.ck + w.ck_off;
+    int32_t a[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) a[s] = s == 0 ? 0 : FEC_NEG;
+    for (uint32_t k = 0; k < K; ++k) {
+        if (k % FEC_WIN == 0) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) ck[((size_t)(k / FEC_WIN) * 8 + s) * 64 + l] = a[s];
+        }
+        int32_t Ak, Bk;
+        inputs<DEC>(A, w, base, k, l, &Ak, &Bk);
+        fwd_step(a, Ak, Bk);
+    }
+    // backward through the termination
+    const int32_t* tl = A.tail + (size_t)(&w - A.waves) * 12 * 64 + (DEC == 1 ? 0 : 6) * 64 + l;
+    int32_t be[8], bn[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) be[s] = s == 0 ? 0 : FEC_NEG;
+    for (int t = 2; t >= 0; --t) {
+        const int32_t tx = tl[t * 64], tz = tl[(3 + t) * 64];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int s1 = (s >> 2) & 1, s2 = (s >> 1) & 1, s3 = s & 1;
+            const int u = s2 ^ s3;  // input = feedback: a = 0
+            const int p = s1 ^ s3;
+            const int nx = (s1 << 1) | s2;
+            bn[s] = be[nx] + (u ? tx : 0) + (p ? tz : 0);
+        }
+        int32_t mx = bn[0];
+#pragma unroll
+        for (int s = 1; s < 8; ++s) mx = max(mx, bn[s]);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) be[s] = max(bn[s] - mx, FEC_NEG);
+    }
+    int16_t* le_out = base + (size_t)(DEC == 1 ? 3 : 4) * K * 64;
+    uint8_t* bits = A.bits + w.data_off;
+    for (int32_t wi = (int32_t)nw - 1; wi >= 0; --wi) {
+        int32_t aw[FEC_WIN][8], Aw[FEC_WIN], Bw[FEC_WIN];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) aw[0][s] = ck[((size_t)wi * 8 + s) * 64 + l];
+#pragma unroll
+        for (int t = 0; t < (int)FEC_WIN; ++t) {
+            inputs<DEC>(A, w, base, wi * FEC_WIN + t, l, &Aw[t], &Bw[t]);
+            if (t + 1 < (int)FEC_WIN) {
+#pragma unroll
+                for (int s = 0; s < 8; ++s) aw[t + 1][s] = aw[t][s];
+                fwd_step(aw[t + 1], Aw[t], Bw[t]);
+            }
+        }
+#pragma unroll
+        for (int t = FEC_WIN - 1; t >= 0; --t) {
+            const uint32_t k = wi * FEC_WIN + t;
+            const int32_t Ak = Aw[t], Bk = Bw[t];
+            int32_t m1 = INT32_MIN, m0 = INT32_MIN;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int s1 = (s >> 2) & 1, s2 = (s >> 1) & 1, s3 = s & 1;
+                int32_t b = INT32_MIN;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int an = u ^ s2 ^ s3, p = an ^ s1 ^ s3;
+                    const int nx = (an << 2) | (s1 << 1) | s2;
+                    const int32_t g = (u ? Ak : 0) + (p ? Bk : 0);
+                    const int32_t v = aw[t][s] + g + be[nx];
+                    if (u) m1 = max(m1, v); else m0 = max(m0, v);
+                    b = max(b, g + be[nx]);
+                }
+                bn[s] = b;
+            }
+            const int32_t llr = m1 - m0;
+            const int32_t e = min(32767, max(-32767, ((llr - Ak) * 3) >> 2));
+            le_out[(size_t)k * 64 + l] = (int16_t)e;
+            if (DEC == 2) bits[(size_t)A.tab[w.pi_off + k] * 64 + l] = llr > 0;
+            int32_t mx = bn[0];
+#pragma unroll
+            for (int s = 1; s < 8; ++s) mx = max(mx, bn[s]);
+#pragma unroll
+            for (int s = 0; s < 8; ++s) be[s] = max(bn[s] - mx, FEC_NEG);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) fec_tdec_kernel(FecArgs A) {
+    const FecWave& w = A.waves[blockIdx.x];
+    const uint32_t l = threadIdx.x;
+    const bool active = l < w.n;
+    const FecCb cb = A.cbs[w.first_cb + (active ? l : 0)];
+    int16_t* base = A.work16 + w.data_off;
+    const uint8_t* bits = A.bits + w.data_off;
+    bool done = !active, ok = false;
+    uint32_t used = 0;
+    for (uint32_t it = 1; it <= A.max_iter; ++it) {
+        if (__all(done)) break;
+        if (!done) {
+            map_decode<1>(A, w, base, l);
+            map_decode<2>(A, w, base, l);
+            used = it;
+            uint32_t reg = 0;
+            for (uint32_t k = 0; k < w.K; ++k) {
+                const uint32_t top = (reg >> 23) & 1;
+                reg = (reg << 1) & 0xFFFFFF;
+                if (top ^ bits[(size_t)k * 64 + l]) reg ^= cb.poly;
+            }
+            ok = reg == 0;
+            if (ok && it >= A.min_iter) done = true;
+        }
+    }
+    if (!active) return;
+    ok = done && ok;
+    for (uint32_t j = 0; j < cb.out_bytes; ++j) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v = (v << 1) | bits[(size_t)(8 * j + t) * 64 + l];
+        A.tb[cb.tb_off + j] = (uint8_t)v;
+    }
+    A.cb_out[w.first_cb + l] = (used << 1) | (ok ? 1u : 0u);
+}
+
+// GF(2)[x] / CRC24A helpers for joining segment CRCs: crc(A || B) = crc(A) x^{|B|} + crc(B)
+__device__ __forceinline__ uint32_t mulmod24(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    for (int i = 23; i >= 0; --i) {
+        const uint32_t top = (r >> 23) & 1;
+        r = (r << 1) & 0xFFFFFF;
+        if (top) r ^= 0x864CFB;
+        if ((b >> i) & 1) r ^= a;
+    }
+    return r;
+}
+__device__ uint32_t xpow24(uint64_t n) {  // x^n mod g
+    uint32_t r = 1, b = 2;  // 1 and x
+    while (n) {
+        if (n & 1) r = mulmod24(r, b);
+        b = mulmod24(b, b);
+        n >>= 1;
+    }
+    return r;
+}
+
+__global__ void __launch_bounds__(64) fec_tbcrc_kernel(FecTbArgs A) {
+    const uint32_t p = blockIdx.x, l = threadIdx.x;
+    const uint8_t* d = A.tb + A.tb_off[p];
+    const uint32_t nb = A.nbytes[p], seg = (nb + 63) / 64;
+    const uint32_t lo = min(nb, l * seg), hi = min(nb, lo + seg);
+    uint32_t reg = 0;
+    for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t byte = d[i];
+        for (int t = 7; t >= 0; --t) {
+            const uint32_t top = (reg >> 23) & 1;
+            reg = (reg << 1) & 0xFFFFFF;
+            if (top ^ ((byte >> t) & 1)) reg ^= 0x864CFB;
+        }
+    }
+    __shared__ uint32_t part[64];
+    part[l] = reg;
+    __syncthreads();
+    if (l == 0) {
+        uint32_t crc = 0;
+        for (uint32_t j = 0; j < 64; ++j) {
+            const uint32_t a = min(nb, j * seg), b = min(nb, a + seg);
+            if (b > a) crc = mulmod24(crc, xpow24(8ull * (b - a))) ^ part[j];
+        }
+        const uint32_t rx = ((uint32_t)d[nb] << 16) | ((uint32_t)d[nb + 1] << 8) | d[nb + 2];
+        A.ok[p] = crc == rx;
+    }
+}
+
+int launch_fec_dematch(const FecArgs& a, hipStream_t s) {
+    if (a.n_cb == 0) return 0;
+    hipLaunchKernelGGL(fec_dematch_kernel, dim3(a.n_cb), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_fec_tdec(const FecArgs& a, uint32_t n_waves, hipStream_t s) {
+    if (n_waves == 0) return 0;
+    hipLaunchKernelGGL(fec_tdec_kernel, dim3(n_waves), dim3(64), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_fec_tbcrc(const FecTbArgs& a, hipStream_t s) {
+    if (a.n == 0) return 0;
+    hipLaunchKernelGGL(fec_tbcrc_kernel, dim3(a.n), dim3(64), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace dnrp::dev

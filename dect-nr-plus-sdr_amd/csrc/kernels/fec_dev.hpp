@@ -1,0 +1,67 @@
+// fec_dev.hpp — device-side turbo decoding of PDC transport blocks (dnrp_pdc_decode_batch):
+// the batched form of fec_t::decode_tb (phy/fec/pdc_enc.cpp:291-492) with the arithmetic of the
+// host decoder in csrc/host/fec.cpp (integer max-log-MAP, extrinsic x3/4, CRC early stop), so a code
+// block decodes to the same bits after the same number of iterations on both.
+//
+// Layout: code blocks of equal size K are grouped 64 to a wavefront, one code block per lane; the
+// wave's soft streams are stored [k][lane] (int16), so the QPP-interleaved accesses of a wave — the
+// interleaver depends only on K — are coalesced 128-B rows. Forward state metrics are kept only at
+// every 8th step (checkpoints [k/8][state][lane]); the backward pass recomputes each 8-step window's
+// metrics in registers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dnrp::dev {
+
+constexpr uint32_t FEC_WIN = 8;      // backward-pass window (steps); every K is a multiple of 8
+constexpr int32_t FEC_NEG = -(1 << 28);
+
+struct FecCb {           // one code block
+    uint64_t llr_off;    // element offset of its first soft bit in the LLR input
+    uint64_t tb_off;     // byte offset of its decoded data in the TB output
+    uint32_t E;          // soft bits read (n_e2, pdc_enc.cpp:322-332)
+    uint32_t start;      // index into the size's circular-buffer list where soft bit 0 lands (rv)
+    uint32_t wave, lane;
+    uint32_t poly;       // CRC over the K decoded bits: CRC24B (C > 1) or CRC24A (C == 1)
+    uint32_t out_bytes;  // decoded bytes written (K/8 for C == 1, (K-24)/8 otherwise)
+};
+
+struct FecWave {
+    uint64_t data_off;   // element offset of the wave's [k][64] arrays in the work buffer
+    uint64_t ck_off;     // element offset of its checkpoints
+    uint32_t K, n;       // code-block size, lanes in use
+    uint32_t valid_off;  // offsets into the size tables: circular-buffer list (3 (K + 4) entries:
+    uint32_t pi_off;     //   stream << 16 | index), QPP pi, inverse pi
+    uint32_t pinv_off;
+    uint32_t first_cb;   // FecCb index of lane 0 (lanes are consecutive)
+};
+
+struct FecArgs {
+    const int16_t* llr;
+    uint8_t* tb;
+    const uint32_t* tab;
+    const FecCb* cbs;
+    const FecWave* waves;
+    int16_t* work16;     // sys, p1, p2, le1, le2: 5 x K x 64 per wave (data_off)
+    int32_t* tail;       // [wave][12][64]
+    uint8_t* bits;       // [wave][K][64] hard decisions (data_off)
+    int32_t* ck;         // checkpoints (ck_off)
+    uint32_t* cb_out;    // per code block: iterations << 1 | crc ok
+    uint32_t n_cb, max_iter, min_iter;
+};
+
+struct FecTbArgs {       // transport-block CRC24A of packets with C > 1
+    const uint8_t* tb;
+    const uint64_t* tb_off;
+    const uint32_t* nbytes;  // N_TB_bits / 8 (the CRC follows)
+    uint32_t* ok;
+    uint32_t n;
+};
+
+int launch_fec_dematch(const FecArgs& a, hipStream_t s);
+int launch_fec_tdec(const FecArgs& a, uint32_t n_waves, hipStream_t s);
+int launch_fec_tbcrc(const FecTbArgs& a, hipStream_t s);
+
+}  // namespace dnrp::dev

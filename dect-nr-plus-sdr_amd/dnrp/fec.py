@@ -5,6 +5,7 @@
   pcc_decode  <- fec_t::decode_plcf_test (pcc_enc.cpp:215-364)
   pdc_encode  <- fec_t::encode_tb        (pdc_enc.cpp:127-229)
   pdc_decode  <- fec_t::decode_tb        (pdc_enc.cpp:291-492), HarqRx <- harq::buffer_rx_t
+  pdc_decode_batch: decode_tb of many packets on the GPU (kernels/fec.hip), same arithmetic
   cbsegm      <- sp3::fix::srsran_cbsegm_FIX (sections_part3/fix/cbsegm.cpp:65-123)
 
 Bits are numpy uint8 arrays packed MSB first, LLRs numpy int16 (positive = bit 1).
@@ -50,6 +51,7 @@ def lib():
         L.dnrp_harq_rx_create.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(P)]
         L.dnrp_harq_rx_reset.argtypes = [P]
         L.dnrp_harq_rx_destroy.argtypes = [P]
+        L.dnrp_pdc_decode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P]
         _ready = True
     return L
 
@@ -141,3 +143,22 @@ def pdc_decode(cfg, llr, hb=None, n_llr=None):
     ok = _chk(lib().dnrp_pdc_decode(hb.h if hb else None, C.byref(cfg), _ptr(llr), n_llr, _ptr(tb), C.byref(it)),
               "dnrp_pdc_decode")
     return bool(ok), tb, it.value
+
+
+def pdc_decode_batch(phy, cfgs, llr, tb, stream=None):
+    """GPU turbo decoding of len(cfgs) transport blocks (one-shot). llr: int16 device tensor [m][>= G],
+    tb: uint8 device tensor [m][>= N_TB_bits/8 + 3] (decoded TB + its CRC24A).
+    -> (crc_ok bool array [m], iterations array [m])"""
+    import torch
+    from . import _stream_ptr
+    m = len(cfgs)
+    assert llr.dtype == torch.int16 and llr.dim() == 2 and llr.is_contiguous() and llr.shape[0] >= m and llr.is_cuda
+    assert tb.dtype == torch.uint8 and tb.dim() == 2 and tb.is_contiguous() and tb.shape[0] >= m and tb.is_cuda
+    assert all(c.G <= llr.shape[1] and c.N_TB_bits // 8 + 3 <= tb.shape[1] for c in cfgs)
+    arr = (FecCfg * max(m, 1))(*cfgs)
+    ok = np.zeros(m, np.uint8)
+    it = np.zeros(m, np.uint32)
+    _chk(lib().dnrp_pdc_decode_batch(phy._ctx, m, arr, C.c_void_p(llr.data_ptr()), llr.shape[1],
+                                     C.c_void_p(tb.data_ptr()), tb.shape[1], _ptr(ok), _ptr(it), _stream_ptr(stream)),
+         "dnrp_pdc_decode_batch")
+    return ok.astype(bool), it

@@ -411,6 +411,20 @@ int dnrp_pdc_encode(const dnrp_fec_cfg* cfg, const uint8_t* tb, uint8_t* d);
  * Up to 10 iterations per code block, CRC early stop after at least 2. */
 int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* llr, uint32_t n_llr, uint8_t* tb,
                     uint32_t* iterations);
+/*
+ * Device turbo decoding of m transport blocks <- fec_t::decode_tb for many packets at once (one-shot:
+ * a fresh softbuffer, all G soft bits present), with the host decoder's arithmetic: each code block
+ * decodes to the same bits after the same number of iterations as dnrp_pdc_decode.
+ *   cfg         host [m]: N_TB_bits, N_bps, rv, G, Z of each packet
+ *   llr         device, row i at llr + i*llr_stride (>= G_i): descrambled LLRs (dnrp_rx_pdc_batch output)
+ *   tb          device, row i at tb + i*tb_stride (>= N_TB_bits_i/8 + 3): decoded transport block
+ *               followed by its received CRC24A
+ *   crc_ok      host [m]: 1 if every code block and the transport block passed their CRCs
+ *   iterations  host [m] (optional): turbo iterations summed over the packet's code blocks
+ * Blocking: returns after the work on the stream has completed.
+ */
+int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr, uint32_t llr_stride,
+                          uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok, uint32_t* iterations, void* stream);
 int dnrp_harq_rx_create(uint32_t N_TB_bits_max, uint32_t Z, dnrp_harq_rx** out);
 int dnrp_harq_rx_reset(dnrp_harq_rx* hb);
 int dnrp_harq_rx_destroy(dnrp_harq_rx* hb);

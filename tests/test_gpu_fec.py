@@ -6,9 +6,13 @@ decode_tb), as worker_tx_rx_t does per packet (worker_tx_rx.cpp:126-201). Checks
 transport block passes its CRC with the transmitted contents at SNRs well above threshold, the
 closed-loop/beamforming CRC mask is recovered, and at an SNR far below threshold every CRC fails
 (no false passes) — for the GPU LLRs and for the oracle RX's LLRs of the same windows alike."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
 import oracle_py as O
 import phy_fixtures as PF
 
@@ -63,6 +67,10 @@ def _loop(name, snr_db, n=4, seed=1):
     phy.rx_pdc_batch([dnrp.PdcReq(ps, i, 100 + i, plcf_types[i]) for i in range(n)], iq, pdc_llr)
     phy.sync()
     g_pcc, g_pdc = pcc_llr.cpu().numpy(), pdc_llr.cpu().numpy()
+    # GPU turbo decoding of the GPU LLRs (dnrp_pdc_decode_batch)
+    tb_dev = torch.zeros((n, sz["N_TB_bits"] // 8 + 3), dtype=torch.uint8, device=dev)
+    g_ok, _ = FE.pdc_decode_batch(phy, [fcfg] * n, pdc_llr, tb_dev)
+    g_tb = tb_dev.cpu().numpy()
     ocf = O.cfg(u_max, b_max, os_min, L, M)
     ops = O.psdef(*ps_t)
     res = []
@@ -74,6 +82,8 @@ def _loop(name, snr_db, n=4, seed=1):
             ok_d, got_tb, _ = FE.pdc_decode(fcfg, ld)
             res.append((src, i, ok_c, ok_c and (got_plcf == plcfs[i]).all() and (cl, bf) == tuple(map(bool, masks[i])),
                         ok_d, ok_d and (got_tb == tbs[i]).all()))
+        res.append(("gpu-decoder", i, True, True, bool(g_ok[i]),
+                    bool(g_ok[i]) and (g_tb[i, : sz["N_TB_bits"] // 8] == tbs[i]).all()))
     return res
 
 
@@ -88,3 +98,53 @@ def test_fec_loopback_crc_fail_far_below_threshold():
     for src, i, ok_c, good_c, ok_d, good_d in _loop("u2b4_tm5_mcs6", -8.0, seed=2):
         assert not ok_d, (src, i)           # 64-QAM rate-3/4-class TB at -8 dB: undecodable
         assert ok_c == good_c, (src, i)     # a PLCF CRC pass must carry the transmitted PLCF
+
+
+# (N_TB_bits, Qm, G, Z, rv, Es/N0 dB of BPSK-equivalent LLRs): C = 1 / C > 1, several sizes per
+# call, the C4 transport block (58 + 2 code blocks: waves of 64 same-size blocks, partial waves),
+# clean inputs (2 iterations), marginal ones (more iterations, some blocks failing at 10), rv 2 / 3
+# (SNR = 1/sigma^2 of the +-1 soft bits)
+DEC_CASES = [(296, 2, 644, 6144, 0, 30.0), (363464, 8, 486640, 6144, 0, 30.0), (363464, 8, 486640, 6144, 0, 30.0),
+             (14560, 6, 19572, 6144, 0, 4.0), (5000 * 8, 4, 60000, 2048, 0, 3.5), (1000 * 8, 2, 12000, 6144, 3, 3.5),
+             (363464, 8, 486640, 6144, 0, 4.5), (296, 2, 644, 6144, 0, -1.0), (40 * 8, 1, 2000, 2048, 0, -6.0),
+             (4136, 2, 16000, 6144, 2, 1.0)]
+
+
+def test_gpu_turbo_decoder_matches_host():
+    """dnrp_pdc_decode_batch against the host decoder dnrp_pdc_decode (the reference's per-packet
+    decode_tb role): identical CRC status, iteration counts and decoded bytes for every packet."""
+    import dnrp
+    import dnrp.fec as FE
+    import fec_np as ON  # noqa: F401  (oracle/ on sys.path above)
+    phy = dnrp.Phy(1, 1, 1, max_batch=1)
+    rng = np.random.default_rng(9)
+    cfgs, llrs, tbs = [], [], []
+    for tbs_bits, Qm, G, Z, rv, snr in DEC_CASES:
+        while ON.cbsegm(tbs_bits, Z)[2] != 0:
+            tbs_bits += 8
+        G -= G % Qm
+        cfg = FE.fec_cfg(tbs_bits, Qm, G, Z=Z, rv=rv)
+        tb = rng.integers(0, 256, tbs_bits // 8, dtype=np.uint8)
+        x = 2.0 * np.unpackbits(FE.pdc_encode(cfg, tb))[:G] - 1
+        y = x + rng.normal(0, 10 ** (-snr / 20), G)
+        llrs.append(np.round(np.clip(y * 300, -32768, 32767)).astype(np.int16))
+        cfgs.append(cfg)
+        tbs.append(tb)
+    m = len(cfgs)
+    g_max = max(c.G for c in cfgs)
+    llr = np.zeros((m, g_max + 5), np.int16)
+    for i in range(m):
+        llr[i, : cfgs[i].G] = llrs[i]
+    dev = torch.device("cuda:0")
+    tb_dev = torch.full((m, max(c.N_TB_bits for c in cfgs) // 8 + 7), 0xEE, dtype=torch.uint8, device=dev)
+    ok, it = FE.pdc_decode_batch(phy, cfgs, torch.from_numpy(llr).to(dev), tb_dev)
+    g_tb = tb_dev.cpu().numpy()
+    n_fail = 0
+    for i in range(m):
+        h_ok, h_tb, h_it = FE.pdc_decode(cfgs[i], llrs[i])
+        assert (bool(ok[i]), int(it[i])) == (h_ok, h_it), (i, DEC_CASES[i], ok[i], it[i], h_ok, h_it)
+        assert (g_tb[i, : cfgs[i].N_TB_bits // 8] == h_tb).all(), (i, DEC_CASES[i])
+        if h_ok:
+            assert (h_tb == tbs[i]).all()
+        n_fail += not h_ok
+    assert ok[0] and ok[1] and ok[2] and 1 <= n_fail <= m - 3
