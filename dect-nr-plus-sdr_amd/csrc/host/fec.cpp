@@ -753,12 +753,13 @@ extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
         A.bits = ctx->fec_bits.as<uint8_t>(), A.ck = ctx->fec_ck.as<int32_t>();
         A.cb_out = ctx->fec_cbout.as<uint32_t>() + grp_first_cb[g];
         A.n_cb = grp_first_cb[g + 1] - grp_first_cb[g];
+        A.n_waves = grp_first_wave[g + 1] - grp_first_wave[g];
         A.max_iter = kPdcMaxIter, A.min_iter = kPdcMinIter;
         ctx->tic("fec_dematch", s);
         if (launch_fec_dematch(A, s)) return DNRP_EDEVICE;
         ctx->toc("fec_dematch", s);
         ctx->tic("fec_tdec", s);
-        if (launch_fec_tdec(A, grp_first_wave[g + 1] - grp_first_wave[g], s)) return DNRP_EDEVICE;
+        if (launch_fec_tdec(A, A.n_waves, s)) return DNRP_EDEVICE;
         ctx->toc("fec_tdec", s);
     }
     // transport-block CRC of the packets with several code blocks

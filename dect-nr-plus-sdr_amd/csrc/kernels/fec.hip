@@ -1,5 +1,5 @@
 // Batched turbo decoding of PDC code blocks on gfx950 (see fec_dev.hpp). Three kernels:
-//   fec_dematch_kernel  workgroup = code block: rate de-matching (srsran_rm_turbo_rx_lut_ role,
+//   fec_dematch_kernel  workgroup = wave of code blocks: rate de-matching (srsran_rm_turbo_rx_lut_ role,
 //                       pdc_enc.cpp:359-360) straight into the wave's [k][lane] soft streams
 //   fec_tdec_kernel     wavefront = up to 64 code blocks of one size K, lane = code block: the
 //                       iterations of the host decoder (fec.cpp Tdec / map_decode) with CRC early stop
@@ -10,26 +10,33 @@
 namespace dnrp::dev {
 
 __global__ void __launch_bounds__(256) fec_dematch_kernel(FecArgs A) {
-    const FecCb cb = A.cbs[blockIdx.x];
-    const FecWave w = A.waves[cb.wave];
-    const uint32_t K = w.K, nvalid = 3 * (K + 4), l = cb.lane;
+    // workgroup = wave of up to 64 same-size code blocks; thread (row r, lane l): list entries
+    // q = r, r + 4, ... of code block l. The 64 lanes of a wavefront write one 128-B [k][lane] row
+    // per entry; their reads walk 64 LLR rows in step (L1-resident lines).
+    const FecWave w = A.waves[blockIdx.x];
+    const uint32_t l = threadIdx.x & 63u, r = threadIdx.x >> 6;
+    const uint32_t K = w.K, nvalid = 3 * (K + 4);
+    const bool active = l < w.n;
+    const FecCb cb = A.cbs[w.first_cb + (active ? l : 0)];
     const uint32_t* valid = A.tab + w.valid_off;
     int16_t* base = A.work16 + w.data_off;
     const int16_t* llr = A.llr + cb.llr_off;
     // tail slot of (stream, t = index - K), as fec.cpp Tdec::load orders them
     const uint8_t tslot[3][4] = {{0, 4, 6, 10}, {3, 2, 9, 8}, {1, 5, 7, 11}};
-    for (uint32_t q = threadIdx.x; q < nvalid; q += blockDim.x) {
+    for (uint32_t q = r; q < nvalid; q += 4) {
         // soft bits j = j0, j0 + nvalid, ... land on list entry q; summed in j order with int16
         // saturation like the host's sequential accumulation
-        uint32_t j = q >= cb.start ? q - cb.start : q + nvalid - cb.start;
         int32_t sum = 0;
-        for (; j < cb.E; j += nvalid) sum = min(32767, max(-32768, sum + (int32_t)llr[j]));
+        if (active) {
+            uint32_t j = q >= cb.start ? q - cb.start : q + nvalid - cb.start;
+            for (; j < cb.E; j += nvalid) sum = min(32767, max(-32768, sum + (int32_t)llr[j]));
+        }
         const uint32_t e = valid[q], st = e >> 16, idx = e & 0xFFFF;
         if (idx < K) base[(size_t)st * K * 64 + (size_t)idx * 64 + l] = (int16_t)sum;
-        else A.tail[(size_t)cb.wave * 12 * 64 + tslot[st][idx - K] * 64 + l] = sum;
+        else A.tail[(size_t)blockIdx.x * 12 * 64 + tslot[st][idx - K] * 64 + l] = sum;
     }
     int16_t* le2 = base + (size_t)4 * K * 64;
-    for (uint32_t k = threadIdx.x; k < K; k += blockDim.x) le2[(size_t)k * 64 + l] = 0;
+    for (uint32_t k = r; k < K; k += 4) le2[(size_t)k * 64 + l] = 0;
 }
 
 // One trellis step of the forward recursion (state s = 4 s1 + 2 s2 + s3; next n = (a, s1, s2),
@@ -82,14 +89,14 @@ __device__ void map_decode(const FecArgs& A, const FecWave& w, int16_t* base, ui
     int32_t a[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) a[s] = s == 0 ? 0 : FEC_NEG;
-    for (uint32_t k = 0; k < K; ++k) {
-        if (k % FEC_WIN == 0) {
+    for (uint32_t k0 = 0; k0 < K; k0 += FEC_WIN) {
 #pragma unroll
-            for (int s = 0; s < 8; ++s) ck[((size_t)(k / FEC_WIN) * 8 + s) * 64 + l] = a[s];
-        }
-        int32_t Ak, Bk;
-        inputs<DEC>(A, w, base, k, l, &Ak, &Bk);
-        fwd_step(a, Ak, Bk);
+        for (int s = 0; s < 8; ++s) ck[((size_t)(k0 / FEC_WIN) * 8 + s) * 64 + l] = a[s];
+        int32_t Ak[FEC_WIN], Bk[FEC_WIN];  // the window's loads in flight together
+#pragma unroll
+        for (int t = 0; t < (int)FEC_WIN; ++t) inputs<DEC>(A, w, base, k0 + t, l, &Ak[t], &Bk[t]);
+#pragma unroll
+        for (int t = 0; t < (int)FEC_WIN; ++t) fwd_step(a, Ak[t], Bk[t]);
     }
     // backward through the termination
     const int32_t* tl = A.tail + (size_t)(&w - A.waves) * 12 * 64 + (DEC == 1 ? 0 : 6) * 64 + l;
@@ -247,7 +254,7 @@ __global__ void __launch_bounds__(64) fec_tbcrc_kernel(FecTbArgs A) {
 
 int launch_fec_dematch(const FecArgs& a, hipStream_t s) {
     if (a.n_cb == 0) return 0;
-    hipLaunchKernelGGL(fec_dematch_kernel, dim3(a.n_cb), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(fec_dematch_kernel, dim3(a.n_waves), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_fec_tdec(const FecArgs& a, uint32_t n_waves, hipStream_t s) {

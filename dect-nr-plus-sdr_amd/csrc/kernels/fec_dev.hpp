@@ -49,7 +49,7 @@ struct FecArgs {
     uint8_t* bits;       // [wave][K][64] hard decisions (data_off)
     int32_t* ck;         // checkpoints (ck_off)
     uint32_t* cb_out;    // per code block: iterations << 1 | crc ok
-    uint32_t n_cb, max_iter, min_iter;
+    uint32_t n_cb, n_waves, max_iter, min_iter;
 };
 
 struct FecTbArgs {       // transport-block CRC24A of packets with C > 1
