@@ -198,9 +198,9 @@ struct dnrp_ctx {
     };
     std::map<std::string, ev_pool> ev;
     // device turbo decoding (fec.cpp dnrp_pdc_decode_batch, kernels/fec.hip): per-size tables
-    // (circular-buffer lists, QPP pi / inverse) built at the first call, plan and work buffers
+    // (circular-buffer lists) built at the first call, plan and work buffers
     dbuf fec_tab, fec_cbs, fec_waves, fec_work16, fec_tail, fec_bits, fec_ck, fec_cbout, fec_tbarg;
-    std::vector<uint32_t> fec_valid_off, fec_pi_off, fec_pinv_off, fec_start;  // per K index ([idx][rv] for start)
+    std::vector<uint32_t> fec_valid_off, fec_start;  // per K index ([idx][rv] for start)
     ~dnrp_ctx() {
         for (auto& e : ev)
             for (auto& p : e.second.ev) {

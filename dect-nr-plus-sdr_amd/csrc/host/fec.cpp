@@ -634,21 +634,15 @@ int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* ll
 // ---- device turbo decoding -----------------------------------------------------------------------
 static int fec_tables(dnrp_ctx* ctx) {
     if (!ctx->fec_valid_off.empty()) return DNRP_OK;
-    std::vector<uint32_t> tab, voff(kNofCbSizes), poff(kNofCbSizes), ioff(kNofCbSizes), st(kNofCbSizes * 4);
+    std::vector<uint32_t> tab, voff(kNofCbSizes), st(kNofCbSizes * 4);
     for (uint32_t idx = 0; idx < kNofCbSizes; ++idx) {
         const auto v = valid_list(idx);
         voff[idx] = (uint32_t)tab.size();
         tab.insert(tab.end(), v.begin(), v.end());
-        const auto& pi = tables(idx).pi;
-        poff[idx] = (uint32_t)tab.size();
-        tab.insert(tab.end(), pi.begin(), pi.end());
-        ioff[idx] = (uint32_t)tab.size();
-        tab.resize(tab.size() + pi.size());
-        for (uint32_t i = 0; i < pi.size(); ++i) tab[ioff[idx] + pi[i]] = i;
         for (uint32_t rv = 0; rv < 4; ++rv) st[idx * 4 + rv] = valid_start(idx, rv);
     }
     if (!ctx->fec_tab.upload(tab)) return DNRP_ENOMEM;
-    ctx->fec_valid_off = voff, ctx->fec_pi_off = poff, ctx->fec_pinv_off = ioff, ctx->fec_start = st;
+    ctx->fec_valid_off = voff, ctx->fec_start = st;
     return DNRP_OK;
 }
 
@@ -711,7 +705,8 @@ extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
             FecWave w{};
             w.data_off = data, w.ck_off = ck, w.K = K;
             w.n = (uint32_t)std::min<size_t>(64, v.size() - c0);
-            w.valid_off = ctx->fec_valid_off[idx], w.pi_off = ctx->fec_pi_off[idx], w.pinv_off = ctx->fec_pinv_off[idx];
+            w.valid_off = ctx->fec_valid_off[idx];
+            qpp_params(idx, &w.f1, &w.f2);
             w.first_cb = (uint32_t)cbs.size() - grp_first_cb.back();
             const uint32_t wrel = (uint32_t)waves.size() - grp_first_wave.back();
             for (uint32_t l = 0; l < w.n; ++l) {

@@ -62,20 +62,49 @@ __device__ __forceinline__ void fwd_step(int32_t (&a)[8], int32_t A, int32_t B) 
     for (int n = 0; n < 8; ++n) a[n] = max(nxt[n] - mx, FEC_NEG);
 }
 
+// QPP interleaver pi(i) = (f1 i + f2 i^2) mod K on wave-uniform values: direct evaluation at a
+// window start, then pi(i+1) = pi(i) + d(i), d(i+1) = d(i) + 2 f2 (mod K)
+struct Qpp {
+    uint32_t K, f1, f2;
+    __device__ uint32_t at(uint32_t i) const {
+        return (uint32_t)(((uint64_t)f1 * i + (uint64_t)f2 * ((uint64_t)i * i % K)) % K);
+    }
+    __device__ uint32_t delta(uint32_t i) const {  // pi(i+1) - pi(i) mod K = f1 + f2 (2 i + 1)
+        return (uint32_t)(((uint64_t)f1 + (uint64_t)f2 * (2ull * i + 1)) % K);
+    }
+};
+
+// inputs of step k: decoder 1 reads natural order (its a priori = decoder 2's extrinsic, stored in
+// natural order), decoder 2 the QPP row pi = pi(k)
 template <int DEC>
-__device__ __forceinline__ void inputs(const FecArgs& A, const FecWave& w, const int16_t* base, uint32_t k, uint32_t l,
-                                       int32_t* a, int32_t* b) {
-    const uint32_t K = w.K;
+__device__ __forceinline__ void inputs(const int16_t* base, uint32_t K, uint32_t k, uint32_t pi, uint32_t l, int32_t* a,
+                                       int32_t* b) {
     const int16_t *sys = base, *p1 = base + (size_t)K * 64, *p2 = base + (size_t)2 * K * 64;
     const int16_t *le1 = base + (size_t)3 * K * 64, *le2 = base + (size_t)4 * K * 64;
     if (DEC == 1) {
-        const uint32_t j = A.tab[w.pinv_off + k];
-        *a = (int32_t)sys[(size_t)k * 64 + l] + le2[(size_t)j * 64 + l];
+        *a = (int32_t)sys[(size_t)k * 64 + l] + le2[(size_t)k * 64 + l];
         *b = p1[(size_t)k * 64 + l];
     } else {
-        const uint32_t j = A.tab[w.pi_off + k];
-        *a = (int32_t)sys[(size_t)j * 64 + l] + le1[(size_t)j * 64 + l];
+        *a = (int32_t)sys[(size_t)pi * 64 + l] + le1[(size_t)pi * 64 + l];
         *b = p2[(size_t)k * 64 + l];
+    }
+}
+
+// loads of the FEC_WIN steps from k0 (pi values of the window in pis[] for decoder 2)
+template <int DEC>
+__device__ __forceinline__ void load_win(const int16_t* base, const Qpp& q, uint32_t k0, uint32_t l, int32_t* a,
+                                         int32_t* b, uint32_t* pis) {
+    uint32_t pi = DEC == 2 ? q.at(k0) : 0, d = DEC == 2 ? q.delta(k0) : 0;
+#pragma unroll
+    for (int t = 0; t < (int)FEC_WIN; ++t) {
+        pis[t] = pi;
+        inputs<DEC>(base, q.K, k0 + t, pi, l, &a[t], &b[t]);
+        if (DEC == 2) {
+            pi += d;
+            pi = pi >= q.K ? pi - q.K : pi;
+            d += 2 * q.f2 % q.K;
+            d = d >= q.K ? d - q.K : d;
+        }
     }
 }
 
@@ -83,23 +112,29 @@ __device__ __forceinline__ void inputs(const FecArgs& A, const FecWave& w, const
 // the windows' forward metrics recomputed in registers; extrinsic out (and, for decoder 2, the
 // hard decisions of the full LLR at the de-interleaved positions).
 template <int DEC>
-__device__ void map_decode(const FecArgs& A, const FecWave& w, int16_t* base, uint32_t l) {
+__device__ void map_decode(const FecArgs& A, const FecWave& w, uint32_t wave, int16_t* base, uint32_t l) {
     const uint32_t K = w.K, nw = K / FEC_WIN;
     int32_t* ck = A.ck + w.ck_off;
     int32_t a[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) a[s] = s == 0 ? 0 : FEC_NEG;
+    // software pipeline: the next window's inputs are loaded while this window is computed
+    const Qpp q{K, w.f1, w.f2};
+    uint32_t pis[FEC_WIN];
+    int32_t An[FEC_WIN], Bn[FEC_WIN];
+    load_win<DEC>(base, q, 0, l, An, Bn, pis);
     for (uint32_t k0 = 0; k0 < K; k0 += FEC_WIN) {
+        int32_t Ak[FEC_WIN], Bk[FEC_WIN];
+#pragma unroll
+        for (int t = 0; t < (int)FEC_WIN; ++t) Ak[t] = An[t], Bk[t] = Bn[t];
+        if (k0 + FEC_WIN < K) load_win<DEC>(base, q, k0 + FEC_WIN, l, An, Bn, pis);
 #pragma unroll
         for (int s = 0; s < 8; ++s) ck[((size_t)(k0 / FEC_WIN) * 8 + s) * 64 + l] = a[s];
-        int32_t Ak[FEC_WIN], Bk[FEC_WIN];  // the window's loads in flight together
-#pragma unroll
-        for (int t = 0; t < (int)FEC_WIN; ++t) inputs<DEC>(A, w, base, k0 + t, l, &Ak[t], &Bk[t]);
 #pragma unroll
         for (int t = 0; t < (int)FEC_WIN; ++t) fwd_step(a, Ak[t], Bk[t]);
     }
     // backward through the termination
-    const int32_t* tl = A.tail + (size_t)(&w - A.waves) * 12 * 64 + (DEC == 1 ? 0 : 6) * 64 + l;
+    const int32_t* tl = A.tail + (size_t)wave * 12 * 64 + (DEC == 1 ? 0 : 6) * 64 + l;
     int32_t be[8], bn[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) be[s] = s == 0 ? 0 : FEC_NEG;
@@ -121,13 +156,24 @@ __device__ void map_decode(const FecArgs& A, const FecWave& w, int16_t* base, ui
     }
     int16_t* le_out = base + (size_t)(DEC == 1 ? 3 : 4) * K * 64;
     uint8_t* bits = A.bits + w.data_off;
+    int32_t cn[8], An2[FEC_WIN], Bn2[FEC_WIN];  // the previous window's checkpoint and inputs, prefetched
+#pragma unroll
+    for (int s = 0; s < 8; ++s) cn[s] = ck[((size_t)(nw - 1) * 8 + s) * 64 + l];
+    uint32_t pn[FEC_WIN], pw[FEC_WIN];
+    load_win<DEC>(base, q, (nw - 1) * FEC_WIN, l, An2, Bn2, pn);
     for (int32_t wi = (int32_t)nw - 1; wi >= 0; --wi) {
         int32_t aw[FEC_WIN][8], Aw[FEC_WIN], Bw[FEC_WIN];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) aw[0][s] = ck[((size_t)wi * 8 + s) * 64 + l];
+        for (int s = 0; s < 8; ++s) aw[0][s] = cn[s];
+#pragma unroll
+        for (int t = 0; t < (int)FEC_WIN; ++t) Aw[t] = An2[t], Bw[t] = Bn2[t], pw[t] = pn[t];
+        if (wi > 0) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) cn[s] = ck[((size_t)(wi - 1) * 8 + s) * 64 + l];
+            load_win<DEC>(base, q, (wi - 1) * FEC_WIN, l, An2, Bn2, pn);
+        }
 #pragma unroll
         for (int t = 0; t < (int)FEC_WIN; ++t) {
-            inputs<DEC>(A, w, base, wi * FEC_WIN + t, l, &Aw[t], &Bw[t]);
             if (t + 1 < (int)FEC_WIN) {
 #pragma unroll
                 for (int s = 0; s < 8; ++s) aw[t + 1][s] = aw[t][s];
@@ -156,8 +202,12 @@ __device__ void map_decode(const FecArgs& A, const FecWave& w, int16_t* base, ui
             }
             const int32_t llr = m1 - m0;
             const int32_t e = min(32767, max(-32767, ((llr - Ak) * 3) >> 2));
-            le_out[(size_t)k * 64 + l] = (int16_t)e;
-            if (DEC == 2) bits[(size_t)A.tab[w.pi_off + k] * 64 + l] = llr > 0;
+            if (DEC == 1) {
+                le_out[(size_t)k * 64 + l] = (int16_t)e;
+            } else {  // natural order: decoder 1's a priori and the hard decisions at pi(k)
+                le_out[(size_t)pw[t] * 64 + l] = (int16_t)e;
+                bits[(size_t)pw[t] * 64 + l] = llr > 0;
+            }
             int32_t mx = bn[0];
 #pragma unroll
             for (int s = 1; s < 8; ++s) mx = max(mx, bn[s]);
@@ -167,8 +217,13 @@ __device__ void map_decode(const FecArgs& A, const FecWave& w, int16_t* base, ui
     }
 }
 
-__global__ void __launch_bounds__(64) fec_tdec_kernel(FecArgs A) {
-    const FecWave& w = A.waves[blockIdx.x];
+#ifndef DNRP_FEC_WPE
+#define DNRP_FEC_WPE 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FEC_WPE))) fec_tdec_kernel(FecArgs A) {
+    // by value: the stores below may alias A.waves as far as the compiler knows, a reference would
+    // make it reload the wave's fields after every store
+    const FecWave w = A.waves[blockIdx.x];
     const uint32_t l = threadIdx.x;
     const bool active = l < w.n;
     const FecCb cb = A.cbs[w.first_cb + (active ? l : 0)];
@@ -179,8 +234,8 @@ __global__ void __launch_bounds__(64) fec_tdec_kernel(FecArgs A) {
     for (uint32_t it = 1; it <= A.max_iter; ++it) {
         if (__all(done)) break;
         if (!done) {
-            map_decode<1>(A, w, base, l);
-            map_decode<2>(A, w, base, l);
+            map_decode<1>(A, w, blockIdx.x, base, l);
+            map_decode<2>(A, w, blockIdx.x, base, l);
             used = it;
             uint32_t reg = 0;
             for (uint32_t k = 0; k < w.K; ++k) {

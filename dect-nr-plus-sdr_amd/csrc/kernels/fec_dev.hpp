@@ -7,7 +7,8 @@
 // wave's soft streams are stored [k][lane] (int16), so the QPP-interleaved accesses of a wave — the
 // interleaver depends only on K — are coalesced 128-B rows. Forward state metrics are kept only at
 // every 8th step (checkpoints [k/8][state][lane]); the backward pass recomputes each 8-step window's
-// metrics in registers.
+// metrics in registers. The interleaver addresses are computed by the QPP recurrence on the scalar
+// unit (no index loads in the dependency chain); decoder 2 writes its extrinsic back in natural order.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -32,9 +33,8 @@ struct FecWave {
     uint64_t data_off;   // element offset of the wave's [k][64] arrays in the work buffer
     uint64_t ck_off;     // element offset of its checkpoints
     uint32_t K, n;       // code-block size, lanes in use
-    uint32_t valid_off;  // offsets into the size tables: circular-buffer list (3 (K + 4) entries:
-    uint32_t pi_off;     //   stream << 16 | index), QPP pi, inverse pi
-    uint32_t pinv_off;
+    uint32_t valid_off;  // offset of the size's circular-buffer list (3 (K + 4) entries: stream << 16 | index)
+    uint32_t f1, f2;     // QPP coefficients: pi(i) = (f1 i + f2 i^2) mod K, stepped with scalar ops
     uint32_t first_cb;   // FecCb index of lane 0 (lanes are consecutive)
 };
 
