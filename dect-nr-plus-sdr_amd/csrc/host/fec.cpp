@@ -791,3 +791,86 @@ extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
         for (uint32_t i = 0; i < m; ++i) iterations[i] = it[i];
     return DNRP_OK;
 }
+
+extern "C" int dnrp_pdc_encode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const uint8_t* tb,
+                                     uint32_t tb_stride, uint8_t* d, uint32_t d_stride, void* stream) {
+    using namespace dnrp::dev;
+    if (!ctx || (m && (!cfg || !tb || !d))) return DNRP_EINVAL;
+    if (m == 0) return DNRP_OK;
+    (void)hipSetDevice(ctx->cfg.device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rc = fec_tables(ctx);
+    if (rc) return rc;
+    std::vector<std::vector<FecEncCb>> by_idx(kNofCbSizes);
+    std::vector<uint64_t> e_off(m), tb_off_all(m);
+    std::vector<uint32_t> Gs(m), nbytes(m);
+    uint64_t e_total = 0;
+    uint32_t max_bytes = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+        Segm g;
+        if ((rc = segm_of(&cfg[i], &g))) return rc;
+        const uint32_t tbs = cfg[i].N_TB_bits, Qm = cfg[i].N_bps, G = cfg[i].G;
+        if (tb_stride < tbs / 8 || d_stride < (G + 7) / 8) return DNRP_EINVAL;
+        e_off[i] = e_total, Gs[i] = G, nbytes[i] = tbs / 8, tb_off_all[i] = (uint64_t)i * tb_stride;
+        max_bytes = std::max(max_bytes, (G + 7) / 8);
+        uint32_t rp = 0, wp = 0;
+        for (uint32_t r = 0; r < g.C; ++r) {
+            const uint32_t K = r < g.C2 ? g.K2 : g.K1, idx = r < g.C2 ? g.K2_idx : g.K1_idx;
+            FecEncCb cb{};
+            cb.tb_off = (uint64_t)i * tb_stride, cb.e_off = e_total + wp, cb.pkt = i, cb.tbs = tbs;
+            cb.rp = rp, cb.rlen = g.C > 1 ? K - 24 : K, cb.E = cb_E(g, r, Qm, G);
+            cb.start = ctx->fec_start[idx * 4 + cfg[i].rv], cb.crc24b = g.C > 1;
+            by_idx[idx].push_back(cb);
+            rp += cb.rlen;
+            wp += cb.E;
+        }
+        e_total += G;
+    }
+    std::vector<FecEncCb> cbs;
+    std::vector<FecWave> waves;
+    uint64_t cd = 0;
+    for (uint32_t idx = 0; idx < kNofCbSizes; ++idx) {
+        const auto& v = by_idx[idx];
+        const uint32_t K = cb_size(idx);
+        for (size_t c0 = 0; c0 < v.size(); c0 += 64) {
+            FecWave w{};
+            w.data_off = cd, w.K = K, w.n = (uint32_t)std::min<size_t>(64, v.size() - c0);
+            w.valid_off = ctx->fec_valid_off[idx];
+            qpp_params(idx, &w.f1, &w.f2);
+            w.first_cb = (uint32_t)cbs.size();
+            cbs.insert(cbs.end(), v.begin() + c0, v.begin() + c0 + w.n);
+            waves.push_back(w);
+            cd += (uint64_t)(K + 3 * (K + 4)) * 64;
+        }
+    }
+    // scratch: c/d streams per wave, unpacked bits, TB CRCs; argument arrays
+    std::vector<uint8_t> args(m * (8 + 8 + 4 + 4 + 4) + 64);
+    uint8_t* ap = args.data();
+    std::memcpy(ap, tb_off_all.data(), m * 8);
+    std::memcpy(ap + m * 8, e_off.data(), m * 8);
+    std::memcpy(ap + m * 16, nbytes.data(), m * 4);
+    std::memcpy(ap + m * 20, Gs.data(), m * 4);
+    if (!ctx->fec_cbs.upload(cbs) || !ctx->fec_waves.upload(waves) || !ctx->fec_work16.ensure(cd + 16) ||
+        !ctx->fec_bits.ensure(e_total + 16) || !ctx->fec_tbarg.upload(args))
+        return DNRP_ENOMEM;
+    uint8_t* dargs = ctx->fec_tbarg.as<uint8_t>();
+    uint32_t* tbcrc = reinterpret_cast<uint32_t*>(dargs + m * 24);
+    FecTbArgs T{};
+    T.tb = tb, T.tb_off = reinterpret_cast<const uint64_t*>(dargs), T.nbytes = reinterpret_cast<const uint32_t*>(dargs + m * 16);
+    T.crc_out = tbcrc, T.n = m;
+    if (launch_fec_tbcrc(T, s)) return DNRP_EDEVICE;
+    FecEncArgs E{};
+    E.tb = tb, E.tab = ctx->fec_tab.as<uint32_t>(), E.cbs = ctx->fec_cbs.as<FecEncCb>();
+    E.waves = ctx->fec_waves.as<FecWave>(), E.tbcrc = tbcrc;
+    E.cd = ctx->fec_work16.as<uint8_t>(), E.ebits = ctx->fec_bits.as<uint8_t>();
+    ctx->tic("fec_encode", s);
+    if (launch_fec_encode(E, (uint32_t)waves.size(), s)) return DNRP_EDEVICE;
+    ctx->toc("fec_encode", s);
+    FecPackArgs P{};
+    P.ebits = E.ebits, P.e_off = reinterpret_cast<const uint64_t*>(dargs + m * 8);
+    P.G = reinterpret_cast<const uint32_t*>(dargs + m * 20), P.d = d, P.d_stride = d_stride, P.n = m;
+    P.max_bytes = max_bytes;
+    if (launch_fec_pack(P, s)) return DNRP_EDEVICE;
+    HIPCHK(hipStreamSynchronize(s));
+    return DNRP_OK;
+}

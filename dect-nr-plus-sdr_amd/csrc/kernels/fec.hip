@@ -302,9 +302,115 @@ __global__ void __launch_bounds__(64) fec_tbcrc_kernel(FecTbArgs A) {
             const uint32_t a = min(nb, j * seg), b = min(nb, a + seg);
             if (b > a) crc = mulmod24(crc, xpow24(8ull * (b - a))) ^ part[j];
         }
-        const uint32_t rx = ((uint32_t)d[nb] << 16) | ((uint32_t)d[nb + 1] << 8) | d[nb + 2];
-        A.ok[p] = crc == rx;
+        if (A.crc_out) {
+            A.crc_out[p] = crc;
+        } else {
+            const uint32_t rx = ((uint32_t)d[nb] << 16) | ((uint32_t)d[nb + 1] << 8) | d[nb + 2];
+            A.ok[p] = crc == rx;
+        }
     }
+}
+
+// ---- encoder (fec.cpp dnrp_pdc_encode: pdc_enc.cpp:148-229) ---------------------------------------
+// wavefront = up to 64 code blocks of one size, lane = code block: b bits -> CRC24B -> both
+// constituent encoders (the second on the QPP rows, addresses by the scalar recurrence) with trellis
+// termination -> rate matching into the unpacked bit scratch
+__global__ void __launch_bounds__(64) fec_encode_kernel(FecEncArgs A) {
+    const FecWave w = A.waves[blockIdx.x];
+    const uint32_t l = threadIdx.x, K = w.K, D = K + 4;
+    const bool active = l < w.n;
+    const FecEncCb cb = A.cbs[w.first_cb + (active ? l : 0)];
+    uint8_t* c = A.cd + w.data_off;
+    uint8_t* d0 = c + (size_t)K * 64;
+    uint8_t* d1 = d0 + (size_t)D * 64;
+    uint8_t* d2 = d1 + (size_t)D * 64;
+    const uint8_t* tb = A.tb + cb.tb_off;
+    const uint32_t tcrc = A.tbcrc[cb.pkt];
+    // c = b[rp, rp + rlen) (+ CRC24B), encoder 1 on the fly
+    uint32_t reg = 0, s1 = 0, s2 = 0, s3 = 0;
+    for (uint32_t k = 0; k < K; ++k) {
+        uint32_t bit;
+        if (k < cb.rlen) {
+            const uint32_t pos = cb.rp + k;
+            bit = pos < cb.tbs ? (tb[pos >> 3] >> (7 - (pos & 7))) & 1u : (tcrc >> (23 - (pos - cb.tbs))) & 1u;
+            const uint32_t top = (reg >> 23) & 1u;
+            reg = (reg << 1) & 0xFFFFFF;
+            if (top ^ bit) reg ^= 0x800063;
+        } else {
+            bit = (reg >> (23 - (k - cb.rlen))) & 1u;  // the code-block CRC (crc24b blocks only)
+        }
+        c[(size_t)k * 64 + l] = (uint8_t)bit;
+        d0[(size_t)k * 64 + l] = (uint8_t)bit;
+        const uint32_t a = bit ^ s2 ^ s3;
+        d1[(size_t)k * 64 + l] = (uint8_t)(a ^ s1 ^ s3);
+        s3 = s2, s2 = s1, s1 = a;
+    }
+    uint32_t x1[3], z1[3];
+    for (int t = 0; t < 3; ++t) {
+        x1[t] = s2 ^ s3, z1[t] = s1 ^ s3;
+        s3 = s2, s2 = s1, s1 = 0;
+    }
+    // encoder 2 on c[pi(i)] (each lane reads back only its own column)
+    const Qpp q{K, w.f1, w.f2};
+    uint32_t pi = 0, dl = q.delta(0);
+    const uint32_t f2x2 = 2 * w.f2 % K;
+    s1 = s2 = s3 = 0;
+    for (uint32_t i = 0; i < K; ++i) {
+        const uint32_t a = c[(size_t)pi * 64 + l] ^ s2 ^ s3;
+        d2[(size_t)i * 64 + l] = (uint8_t)(a ^ s1 ^ s3);
+        s3 = s2, s2 = s1, s1 = a;
+        pi += dl;
+        pi = pi >= K ? pi - K : pi;
+        dl += f2x2;
+        dl = dl >= K ? dl - K : dl;
+    }
+    uint32_t x2[3], z2[3];
+    for (int t = 0; t < 3; ++t) {
+        x2[t] = s2 ^ s3, z2[t] = s1 ^ s3;
+        s3 = s2, s2 = s1, s1 = 0;
+    }
+    // tails (TS 36.212 §5.1.3.2.2; fec.cpp turbo_encode)
+    const uint32_t t0[4] = {x1[0], z1[1], x2[0], z2[1]}, t1[4] = {z1[0], x1[2], z2[0], x2[2]},
+                   t2[4] = {x1[1], z1[2], x2[1], z2[2]};
+    for (int t = 0; t < 4; ++t) {
+        d0[(size_t)(K + t) * 64 + l] = (uint8_t)t0[t];
+        d1[(size_t)(K + t) * 64 + l] = (uint8_t)t1[t];
+        d2[(size_t)(K + t) * 64 + l] = (uint8_t)t2[t];
+    }
+    if (!active) return;
+    // rate matching: bit j <- circular-buffer list entry (start + j) mod 3 (K + 4)
+    const uint32_t* valid = A.tab + w.valid_off;
+    const uint32_t nvalid = 3 * D;
+    uint8_t* e = A.ebits + cb.e_off;
+    uint32_t qv = cb.start;
+    for (uint32_t j = 0; j < cb.E; ++j) {
+        const uint32_t ent = valid[qv], st = ent >> 16, idx = ent & 0xFFFF;
+        e[j] = d0[(size_t)st * D * 64 + (size_t)idx * 64 + l];
+        if (++qv == nvalid) qv = 0;
+    }
+}
+
+__global__ void __launch_bounds__(256) fec_pack_kernel(FecPackArgs A) {
+    const uint32_t p = blockIdx.y;
+    const uint32_t G = A.G[p], nb = (G + 7) / 8;
+    const uint8_t* e = A.ebits + A.e_off[p];
+    for (uint32_t B = blockIdx.x * blockDim.x + threadIdx.x; B < nb; B += gridDim.x * blockDim.x) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v = (v << 1) | (8 * B + t < G ? e[8 * B + t] : 0u);
+        A.d[(size_t)p * A.d_stride + B] = (uint8_t)v;
+    }
+}
+
+int launch_fec_encode(const FecEncArgs& a, uint32_t n_waves, hipStream_t s) {
+    if (n_waves == 0) return 0;
+    hipLaunchKernelGGL(fec_encode_kernel, dim3(n_waves), dim3(64), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_fec_pack(const FecPackArgs& a, hipStream_t s) {
+    if (a.n == 0) return 0;
+    hipLaunchKernelGGL(fec_pack_kernel, dim3((a.max_bytes + 255) / 256 < 256 ? (a.max_bytes + 255) / 256 : 256, a.n), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_fec_dematch(const FecArgs& a, hipStream_t s) {

@@ -56,12 +56,44 @@ struct FecTbArgs {       // transport-block CRC24A of packets with C > 1
     const uint8_t* tb;
     const uint64_t* tb_off;
     const uint32_t* nbytes;  // N_TB_bits / 8 (the CRC follows)
-    uint32_t* ok;
+    uint32_t* ok;            // decoder: 1 if the CRC after the TB matches
+    uint32_t* crc_out;       // encoder (non-null): the computed CRC instead
     uint32_t n;
+};
+
+struct FecEncCb {        // one code block of dnrp_pdc_encode_batch
+    uint64_t tb_off;     // byte offset of the packet's transport block
+    uint64_t e_off;      // offset of its first rate-matched bit in the unpacked bit scratch
+    uint32_t pkt;        // packet index (TB CRC)
+    uint32_t tbs;        // N_TB_bits of the packet
+    uint32_t rp;         // first bit of b = a || CRC24A the block takes
+    uint32_t rlen;       // bits taken (K - 24 with a CRC24B, K otherwise)
+    uint32_t E, start;   // rate-matched bits, circular-buffer list start of the redundancy version
+    uint32_t crc24b;     // 1: append a code-block CRC
+};
+
+struct FecEncArgs {
+    const uint8_t* tb;
+    const uint32_t* tab;
+    const FecEncCb* cbs;
+    const FecWave* waves;     // K, n, valid_off, f1, f2, first_cb; data_off = offset in cd (bytes)
+    const uint32_t* tbcrc;    // per packet
+    uint8_t* cd;              // per wave: c [K][64] then d0, d1, d2 [K + 4][64]
+    uint8_t* ebits;           // unpacked rate-matched bits
+};
+
+struct FecPackArgs {          // ebits -> packed MSB-first d rows
+    const uint8_t* ebits;
+    const uint64_t* e_off;    // per packet
+    const uint32_t* G;
+    uint8_t* d;
+    uint32_t d_stride, n, max_bytes;
 };
 
 int launch_fec_dematch(const FecArgs& a, hipStream_t s);
 int launch_fec_tdec(const FecArgs& a, uint32_t n_waves, hipStream_t s);
 int launch_fec_tbcrc(const FecTbArgs& a, hipStream_t s);
+int launch_fec_encode(const FecEncArgs& a, uint32_t n_waves, hipStream_t s);
+int launch_fec_pack(const FecPackArgs& a, hipStream_t s);
 
 }  // namespace dnrp::dev

@@ -6,6 +6,7 @@
   pdc_encode  <- fec_t::encode_tb        (pdc_enc.cpp:127-229)
   pdc_decode  <- fec_t::decode_tb        (pdc_enc.cpp:291-492), HarqRx <- harq::buffer_rx_t
   pdc_decode_batch: decode_tb of many packets on the GPU (kernels/fec.hip), same arithmetic
+  pdc_encode_batch: encode_tb of many packets on the GPU, bit-exact with pdc_encode
   cbsegm      <- sp3::fix::srsran_cbsegm_FIX (sections_part3/fix/cbsegm.cpp:65-123)
 
 Bits are numpy uint8 arrays packed MSB first, LLRs numpy int16 (positive = bit 1).
@@ -52,6 +53,7 @@ def lib():
         L.dnrp_harq_rx_reset.argtypes = [P]
         L.dnrp_harq_rx_destroy.argtypes = [P]
         L.dnrp_pdc_decode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P]
+        L.dnrp_pdc_encode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P]
         _ready = True
     return L
 
@@ -162,3 +164,17 @@ def pdc_decode_batch(phy, cfgs, llr, tb, stream=None):
                                      C.c_void_p(tb.data_ptr()), tb.shape[1], _ptr(ok), _ptr(it), _stream_ptr(stream)),
          "dnrp_pdc_decode_batch")
     return ok.astype(bool), it
+
+
+def pdc_encode_batch(phy, cfgs, tb, d, stream=None):
+    """GPU channel encoding of len(cfgs) transport blocks: tb uint8 device tensor [m][>= N_TB_bits/8]
+    -> d uint8 device tensor [m][>= ceil(G/8)] (unscrambled d-bits, dnrp_tx_batch's pdc_d rows)."""
+    import torch
+    from . import _stream_ptr
+    m = len(cfgs)
+    assert tb.dtype == torch.uint8 and tb.dim() == 2 and tb.is_contiguous() and tb.shape[0] >= m and tb.is_cuda
+    assert d.dtype == torch.uint8 and d.dim() == 2 and d.is_contiguous() and d.shape[0] >= m and d.is_cuda
+    assert all(c.N_TB_bits // 8 <= tb.shape[1] and (c.G + 7) // 8 <= d.shape[1] for c in cfgs)
+    arr = (FecCfg * max(m, 1))(*cfgs)
+    _chk(lib().dnrp_pdc_encode_batch(phy._ctx, m, arr, C.c_void_p(tb.data_ptr()), tb.shape[1],
+                                     C.c_void_p(d.data_ptr()), d.shape[1], _stream_ptr(stream)), "dnrp_pdc_encode_batch")

@@ -425,6 +425,15 @@ int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* ll
  */
 int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr, uint32_t llr_stride,
                           uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok, uint32_t* iterations, void* stream);
+/*
+ * Device channel encoding of m transport blocks <- fec_t::encode_tb for many packets at once
+ * (without the scrambling): bit-exact with dnrp_pdc_encode.
+ *   tb  device, row i at tb + i*tb_stride (>= N_TB_bits_i/8)
+ *   d   device, row i at d + i*d_stride (>= ceil(G_i/8)): the pdc_d rows dnrp_tx_batch takes
+ * Blocking: returns after the work on the stream has completed.
+ */
+int dnrp_pdc_encode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const uint8_t* tb, uint32_t tb_stride,
+                          uint8_t* d, uint32_t d_stride, void* stream);
 int dnrp_harq_rx_create(uint32_t N_TB_bits_max, uint32_t Z, dnrp_harq_rx** out);
 int dnrp_harq_rx_reset(dnrp_harq_rx* hb);
 int dnrp_harq_rx_destroy(dnrp_harq_rx* hb);

@@ -49,9 +49,13 @@ def _loop(name, snr_db, n=4, seed=1):
     pcc = np.stack([FE.pcc_encode(plcfs[i], plcf_types[i], *masks[i]) for i in range(n)])
     pdc = np.stack([FE.pdc_encode(fcfg, tbs[i]) for i in range(n)])
     dev = torch.device("cuda:0")
+    # the GPU encoder produces the same d-bits (dnrp_pdc_encode_batch); TX from its output
+    pdc_dev = torch.zeros((n, pdc.shape[1]), dtype=torch.uint8, device=dev)
+    FE.pdc_encode_batch(phy, [fcfg] * n, torch.from_numpy(np.stack(tbs)).to(dev), pdc_dev)
+    assert (pdc_dev.cpu().numpy() == pdc).all(), name
     descs = [dnrp.TxDesc(0, 100 + i, plcf_types[i], 5, 1.0, 0.0, 0.0, 0) for i in range(n)]
     out = torch.empty((n, sz["N_TX"], S, 2), dtype=torch.float32, device=dev)
-    phy.tx_batch(ps, descs, torch.from_numpy(pcc).to(dev), torch.from_numpy(pdc).to(dev), out)
+    phy.tx_batch(ps, descs, torch.from_numpy(pcc).to(dev), pdc_dev, out)
     phy.sync()
     iq_tx = out.cpu().numpy().view(np.complex64)[..., 0]
     windows, reports = [], []
@@ -148,3 +152,32 @@ def test_gpu_turbo_decoder_matches_host():
             assert (h_tb == tbs[i]).all()
         n_fail += not h_ok
     assert ok[0] and ok[1] and ok[2] and 1 <= n_fail <= m - 3
+
+
+def test_gpu_encoder_matches_host():
+    """dnrp_pdc_encode_batch against dnrp_pdc_encode (itself bit-exact against the numpy oracle):
+    mixed sizes, Z, modulation orders and redundancy versions in one call."""
+    import dnrp
+    import dnrp.fec as FE
+    import fec_np as ON  # noqa: F401
+    phy = dnrp.Phy(1, 1, 1, max_batch=1)
+    rng = np.random.default_rng(4)
+    cfgs, tbs = [], []
+    for tbs_bits, Qm, G, Z, rv, _ in DEC_CASES + [(2960, 1, 7001, 2048, 1, 0), (6144 * 3, 6, 60000, 2048, 2, 0),
+                                                  (48000, 8, 97000, 6144, 3, 0)]:
+        while ON.cbsegm(tbs_bits, Z)[2] != 0:
+            tbs_bits += 8
+        G -= G % Qm
+        cfgs.append(FE.fec_cfg(tbs_bits, Qm, G, Z=Z, rv=rv))
+        tbs.append(rng.integers(0, 256, tbs_bits // 8, dtype=np.uint8))
+    m = len(cfgs)
+    dev = torch.device("cuda:0")
+    tb = np.zeros((m, max(c.N_TB_bits for c in cfgs) // 8 + 1), np.uint8)
+    for i in range(m):
+        tb[i, : len(tbs[i])] = tbs[i]
+    d = torch.full((m, max((c.G + 7) // 8 for c in cfgs) + 3), 0xAB, dtype=torch.uint8, device=dev)
+    FE.pdc_encode_batch(phy, cfgs, torch.from_numpy(tb).to(dev), d)
+    g = d.cpu().numpy()
+    for i in range(m):
+        ref = FE.pdc_encode(cfgs[i], tbs[i])
+        assert (g[i, : len(ref)] == ref).all(), (i, cfgs[i].N_TB_bits, cfgs[i].G)
