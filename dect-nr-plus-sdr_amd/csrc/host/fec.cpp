@@ -646,48 +646,14 @@ static int fec_tables(dnrp_ctx* ctx) {
     return DNRP_OK;
 }
 
-extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr,
-                                     uint32_t llr_stride, uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok,
-                                     uint32_t* iterations, void* stream) {
+// Groups code blocks of equal size into waves (up to ~3 GB of scratch per launch group) and runs
+// de-matching + turbo iterations; cb_pkt receives the packet of each code block in launch order
+// (the order of ctx->fec_cbout).
+static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecCb>>& by_idx,
+                    const std::vector<std::vector<uint32_t>>& pkt_of, const int16_t* llr, uint8_t* tb,
+                    uint32_t max_iter, uint32_t min_iter, hipStream_t s, std::vector<uint32_t>& cb_pkt) {
     using namespace dnrp::dev;
-    if (!ctx || (m && (!cfg || !llr || !tb || !crc_ok))) return DNRP_EINVAL;
-    if (m == 0) return DNRP_OK;
-    (void)hipSetDevice(ctx->cfg.device);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    int rc = fec_tables(ctx);
-    if (rc) return rc;
-    // plan: code blocks of every packet (pdc_enc.cpp:316-332), grouped by size
-    std::vector<Segm> sg(m);
-    std::vector<std::vector<FecCb>> by_idx(kNofCbSizes);
-    std::vector<std::vector<uint32_t>> pkt_of(kNofCbSizes);
-    for (uint32_t i = 0; i < m; ++i) {
-        if ((rc = segm_of(&cfg[i], &sg[i]))) return rc;
-        const Segm& g = sg[i];
-        const uint32_t tbs = cfg[i].N_TB_bits, Qm = cfg[i].N_bps, G = cfg[i].G;
-        if (llr_stride < G || tb_stride < tbs / 8 + 3) return DNRP_EINVAL;
-        const uint32_t Gp = G / Qm, gamma = Gp % g.C, n_e = Qm * (Gp / g.C);
-        uint32_t wp = 0;
-        for (uint32_t r = 0; r < g.C; ++r) {
-            const uint32_t K = r < g.C2 ? g.K2 : g.K1, idx = r < g.C2 ? g.K2_idx : g.K1_idx;
-            uint32_t rpos = r * n_e, n_e2 = n_e;
-            if (r > g.C - gamma) {
-                n_e2 = n_e + Qm;
-                rpos = (g.C - gamma) * n_e + (r - (g.C - gamma)) * n_e2;
-            }
-            FecCb cb{};
-            cb.llr_off = (uint64_t)i * llr_stride + rpos;
-            cb.tb_off = (uint64_t)i * tb_stride + wp / 8;
-            cb.E = n_e2;
-            cb.start = ctx->fec_start[idx * 4 + cfg[i].rv];
-            cb.poly = g.C > 1 ? kCrc24B : kCrc24A;
-            cb.out_bytes = g.C > 1 ? (K - 24) / 8 : K / 8;
-            by_idx[idx].push_back(cb);
-            pkt_of[idx].push_back(i);
-            wp += g.C > 1 ? K - 24 : K;
-        }
-    }
     std::vector<FecCb> cbs;
-    std::vector<uint32_t> cb_pkt;
     std::vector<FecWave> waves;
     std::vector<uint32_t> grp_first_wave{0}, grp_first_cb{0};
     uint64_t data = 0, ck = 0;
@@ -749,7 +715,7 @@ extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
         A.cb_out = ctx->fec_cbout.as<uint32_t>() + grp_first_cb[g];
         A.n_cb = grp_first_cb[g + 1] - grp_first_cb[g];
         A.n_waves = grp_first_wave[g + 1] - grp_first_wave[g];
-        A.max_iter = kPdcMaxIter, A.min_iter = kPdcMinIter;
+        A.max_iter = max_iter, A.min_iter = min_iter;
         ctx->tic("fec_dematch", s);
         if (launch_fec_dematch(A, s)) return DNRP_EDEVICE;
         ctx->toc("fec_dematch", s);
@@ -757,6 +723,51 @@ extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
         if (launch_fec_tdec(A, A.n_waves, s)) return DNRP_EDEVICE;
         ctx->toc("fec_tdec", s);
     }
+    return DNRP_OK;
+}
+
+extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr,
+                                     uint32_t llr_stride, uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok,
+                                     uint32_t* iterations, void* stream) {
+    using namespace dnrp::dev;
+    if (!ctx || (m && (!cfg || !llr || !tb || !crc_ok))) return DNRP_EINVAL;
+    if (m == 0) return DNRP_OK;
+    (void)hipSetDevice(ctx->cfg.device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rc = fec_tables(ctx);
+    if (rc) return rc;
+    // plan: code blocks of every packet (pdc_enc.cpp:316-332), grouped by size
+    std::vector<Segm> sg(m);
+    std::vector<std::vector<FecCb>> by_idx(kNofCbSizes);
+    std::vector<std::vector<uint32_t>> pkt_of(kNofCbSizes);
+    for (uint32_t i = 0; i < m; ++i) {
+        if ((rc = segm_of(&cfg[i], &sg[i]))) return rc;
+        const Segm& g = sg[i];
+        const uint32_t tbs = cfg[i].N_TB_bits, Qm = cfg[i].N_bps, G = cfg[i].G;
+        if (llr_stride < G || tb_stride < tbs / 8 + 3) return DNRP_EINVAL;
+        const uint32_t Gp = G / Qm, gamma = Gp % g.C, n_e = Qm * (Gp / g.C);
+        uint32_t wp = 0;
+        for (uint32_t r = 0; r < g.C; ++r) {
+            const uint32_t K = r < g.C2 ? g.K2 : g.K1, idx = r < g.C2 ? g.K2_idx : g.K1_idx;
+            uint32_t rpos = r * n_e, n_e2 = n_e;
+            if (r > g.C - gamma) {
+                n_e2 = n_e + Qm;
+                rpos = (g.C - gamma) * n_e + (r - (g.C - gamma)) * n_e2;
+            }
+            FecCb cb{};
+            cb.llr_off = (uint64_t)i * llr_stride + rpos;
+            cb.tb_off = (uint64_t)i * tb_stride + wp / 8;
+            cb.E = n_e2;
+            cb.start = ctx->fec_start[idx * 4 + cfg[i].rv];
+            cb.poly = g.C > 1 ? kCrc24B : kCrc24A;
+            cb.out_bytes = g.C > 1 ? (K - 24) / 8 : K / 8;
+            by_idx[idx].push_back(cb);
+            pkt_of[idx].push_back(i);
+            wp += g.C > 1 ? K - 24 : K;
+        }
+    }
+    std::vector<uint32_t> cb_pkt, cb_out;
+    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, tb, kPdcMaxIter, kPdcMinIter, s, cb_pkt))) return rc;
     // transport-block CRC of the packets with several code blocks
     std::vector<uint64_t> tb_off;
     std::vector<uint32_t> nbytes, multi;
@@ -775,14 +786,15 @@ extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
         T.n = (uint32_t)nm;
         if (launch_fec_tbcrc(T, s)) return DNRP_EDEVICE;
     }
-    std::vector<uint32_t> cb_out(cbs.size()), tb_ok(nm);
-    HIPCHK(hipMemcpyAsync(cb_out.data(), ctx->fec_cbout.p, cbs.size() * 4, hipMemcpyDeviceToHost, s));
+    std::vector<uint32_t> tb_ok(nm);
+    cb_out.resize(cb_pkt.size());
+    HIPCHK(hipMemcpyAsync(cb_out.data(), ctx->fec_cbout.p, cb_out.size() * 4, hipMemcpyDeviceToHost, s));
     if (nm) HIPCHK(hipMemcpyAsync(tb_ok.data(), ctx->fec_tbarg.as<uint8_t>() + nm * 12, nm * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     std::vector<uint32_t> it(m, 0);
     for (uint32_t i = 0; i < m; ++i) crc_ok[i] = 1;
-    for (size_t c = 0; c < cbs.size(); ++c) {
-        it[cb_pkt[c]] += cb_out[c] >> 1;
+    for (size_t c = 0; c < cb_out.size(); ++c) {
+        it[cb_pkt[c]] += cb_out[c] >> 3;
         if (!(cb_out[c] & 1)) crc_ok[cb_pkt[c]] = 0;
     }
     for (size_t j = 0; j < nm; ++j)
@@ -872,5 +884,45 @@ extern "C" int dnrp_pdc_encode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
     P.max_bytes = max_bytes;
     if (launch_fec_pack(P, s)) return DNRP_EDEVICE;
     HIPCHK(hipStreamSynchronize(s));
+    return DNRP_OK;
+}
+
+extern "C" int dnrp_pcc_decode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* plcf_type_test, const int16_t* llr,
+                                     uint32_t llr_stride, uint8_t* plcf, uint32_t plcf_stride, uint8_t* result,
+                                     uint32_t* iterations, void* stream) {
+    using namespace dnrp::dev;
+    if (!ctx || (n && (!plcf_type_test || !llr || !plcf || !result))) return DNRP_EINVAL;
+    if (n == 0) return DNRP_OK;
+    if (llr_stride < kPccBits || plcf_stride < kPlcfType2Bits / 8) return DNRP_EINVAL;
+    (void)hipSetDevice(ctx->cfg.device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rc = fec_tables(ctx);
+    if (rc) return rc;
+    std::vector<std::vector<FecCb>> by_idx(kNofCbSizes);
+    std::vector<std::vector<uint32_t>> pkt_of(kNofCbSizes);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t t = plcf_type_test[i];
+        if (t != 1 && t != 2) return DNRP_EINVAL;
+        const uint32_t nb = t == 1 ? kPlcfType1Bits : kPlcfType2Bits, idx = (uint32_t)cb_index(nb + 16);
+        FecCb cb{};
+        cb.llr_off = (uint64_t)i * llr_stride;
+        cb.tb_off = (uint64_t)i * plcf_stride;
+        cb.E = kPccBits;
+        cb.start = ctx->fec_start[idx * 4];  // rv 0 (TS 103 636-3 §7.5.3)
+        cb.poly = kCrc16;                    // CRC16 under the four masks (pcc_enc.cpp:329-349)
+        cb.out_bytes = nb / 8;
+        by_idx[idx].push_back(cb);
+        pkt_of[idx].push_back(i);
+    }
+    std::vector<uint32_t> cb_pkt, cb_out;
+    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, plcf, kPccMaxIter, 1, s, cb_pkt))) return rc;
+    cb_out.resize(cb_pkt.size());
+    HIPCHK(hipMemcpyAsync(cb_out.data(), ctx->fec_cbout.p, cb_out.size() * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (size_t c = 0; c < cb_out.size(); ++c) {
+        const uint32_t i = cb_pkt[c];
+        result[i] = (cb_out[c] & 1) ? (uint8_t)(1 + ((cb_out[c] >> 1) & 3)) : 0;
+        if (iterations) iterations[i] = cb_out[c] >> 3;
+    }
     return DNRP_OK;
 }

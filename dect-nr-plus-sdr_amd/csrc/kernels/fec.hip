@@ -230,20 +230,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
     int16_t* base = A.work16 + w.data_off;
     const uint8_t* bits = A.bits + w.data_off;
     bool done = !active, ok = false;
-    uint32_t used = 0;
+    uint32_t used = 0, mask = 0;
     for (uint32_t it = 1; it <= A.max_iter; ++it) {
         if (__all(done)) break;
         if (!done) {
             map_decode<1>(A, w, blockIdx.x, base, l);
             map_decode<2>(A, w, blockIdx.x, base, l);
             used = it;
+            // CRC remainder over all K bits: 0 for a CRC24 block; for the PLCF's CRC16 the mask it
+            // was sent with (none / closed loop / beamforming / both, pcc_enc.cpp:170-183)
+            const uint32_t W = cb.poly == 0x1021u ? 16u : 24u, msk = (1u << W) - 1;
             uint32_t reg = 0;
             for (uint32_t k = 0; k < w.K; ++k) {
-                const uint32_t top = (reg >> 23) & 1;
-                reg = (reg << 1) & 0xFFFFFF;
+                const uint32_t top = (reg >> (W - 1)) & 1;
+                reg = (reg << 1) & msk;
                 if (top ^ bits[(size_t)k * 64 + l]) reg ^= cb.poly;
             }
-            ok = reg == 0;
+            ok = W == 24 ? reg == 0 : (reg == 0 || reg == 0x5555u || reg == 0xAAAAu || reg == 0xFFFFu);
+            mask = reg == 0x5555u ? 1u : (reg == 0xAAAAu ? 2u : (reg == 0xFFFFu ? 3u : 0u));
             if (ok && it >= A.min_iter) done = true;
         }
     }
@@ -255,7 +259,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
         for (int t = 0; t < 8; ++t) v = (v << 1) | bits[(size_t)(8 * j + t) * 64 + l];
         A.tb[cb.tb_off + j] = (uint8_t)v;
     }
-    A.cb_out[w.first_cb + l] = (used << 1) | (ok ? 1u : 0u);
+    A.cb_out[w.first_cb + l] = (used << 3) | (mask << 1) | (ok ? 1u : 0u);
 }
 
 // GF(2)[x] / CRC24A helpers for joining segment CRCs: crc(A || B) = crc(A) x^{|B|} + crc(B)

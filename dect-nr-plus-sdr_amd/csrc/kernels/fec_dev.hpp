@@ -25,7 +25,7 @@ struct FecCb {           // one code block
     uint32_t E;          // soft bits read (n_e2, pdc_enc.cpp:322-332)
     uint32_t start;      // index into the size's circular-buffer list where soft bit 0 lands (rv)
     uint32_t wave, lane;
-    uint32_t poly;       // CRC over the K decoded bits: CRC24B (C > 1) or CRC24A (C == 1)
+    uint32_t poly;       // CRC over the K decoded bits: CRC24B (C > 1), CRC24A (C == 1), CRC16 (PLCF)
     uint32_t out_bytes;  // decoded bytes written (K/8 for C == 1, (K-24)/8 otherwise)
 };
 
@@ -48,7 +48,7 @@ struct FecArgs {
     int32_t* tail;       // [wave][12][64]
     uint8_t* bits;       // [wave][K][64] hard decisions (data_off)
     int32_t* ck;         // checkpoints (ck_off)
-    uint32_t* cb_out;    // per code block: iterations << 1 | crc ok
+    uint32_t* cb_out;    // per code block: iterations << 3 | CRC16 mask << 1 | crc ok
     uint32_t n_cb, n_waves, max_iter, min_iter;
 };
 

@@ -7,6 +7,7 @@
   pdc_decode  <- fec_t::decode_tb        (pdc_enc.cpp:291-492), HarqRx <- harq::buffer_rx_t
   pdc_decode_batch: decode_tb of many packets on the GPU (kernels/fec.hip), same arithmetic
   pdc_encode_batch: encode_tb of many packets on the GPU, bit-exact with pdc_encode
+  pcc_decode_batch: decode_plcf_test of many packets on the GPU, same arithmetic as pcc_decode
   cbsegm      <- sp3::fix::srsran_cbsegm_FIX (sections_part3/fix/cbsegm.cpp:65-123)
 
 Bits are numpy uint8 arrays packed MSB first, LLRs numpy int16 (positive = bit 1).
@@ -54,6 +55,7 @@ def lib():
         L.dnrp_harq_rx_destroy.argtypes = [P]
         L.dnrp_pdc_decode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P]
         L.dnrp_pdc_encode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P]
+        L.dnrp_pcc_decode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P]
         _ready = True
     return L
 
@@ -178,3 +180,22 @@ def pdc_encode_batch(phy, cfgs, tb, d, stream=None):
     arr = (FecCfg * max(m, 1))(*cfgs)
     _chk(lib().dnrp_pdc_encode_batch(phy._ctx, m, arr, C.c_void_p(tb.data_ptr()), tb.shape[1],
                                      C.c_void_p(d.data_ptr()), d.shape[1], _stream_ptr(stream)), "dnrp_pdc_encode_batch")
+
+
+def pcc_decode_batch(phy, plcf_types, llr, plcf, stream=None):
+    """GPU PLCF decoding: llr int16 device tensor [n][>= 196] (dnrp_rx_pcc_batch's pcc_llr), plcf uint8
+    device tensor [n][>= 10]. -> (result uint8 [n]: 0 = no PLCF, 1 + CRC mask index; iterations [n])"""
+    import torch
+    from . import _stream_ptr
+    n = len(plcf_types)
+    assert llr.dtype == torch.int16 and llr.dim() == 2 and llr.is_contiguous() and llr.shape[0] >= n and llr.is_cuda
+    assert llr.shape[1] >= 196
+    assert plcf.dtype == torch.uint8 and plcf.dim() == 2 and plcf.is_contiguous() and plcf.shape[0] >= n and plcf.is_cuda
+    assert plcf.shape[1] >= 10
+    types = np.ascontiguousarray(plcf_types, dtype=np.uint32)
+    res = np.zeros(n, np.uint8)
+    it = np.zeros(n, np.uint32)
+    _chk(lib().dnrp_pcc_decode_batch(phy._ctx, n, _ptr(types), C.c_void_p(llr.data_ptr()), llr.shape[1],
+                                     C.c_void_p(plcf.data_ptr()), plcf.shape[1], _ptr(res), _ptr(it),
+                                     _stream_ptr(stream)), "dnrp_pcc_decode_batch")
+    return res, it

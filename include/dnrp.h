@@ -434,6 +434,21 @@ int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, co
  */
 int dnrp_pdc_encode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const uint8_t* tb, uint32_t tb_stride,
                           uint8_t* d, uint32_t d_stride, void* stream);
+/*
+ * Device PLCF decoding of n PCCs <- fec_t::decode_plcf_test for many packets at once (after the
+ * descrambling): turbo decoding (K = 56 / 96, up to 5 iterations, stop at the first CRC match) and
+ * the CRC16 check under the four masks, with the host decoder's arithmetic (same bits, iterations).
+ *   plcf_type_test  host [n]: 1 or 2 per packet
+ *   llr             device, row i at llr + i*llr_stride (>= 196): dnrp_rx_pcc_batch's pcc_llr
+ *   plcf            device, row i at plcf + i*plcf_stride (>= 10): the decoded PLCF (5 or 10 bytes)
+ *   result          host [n]: 0 = no PLCF of that type; 1 + m for a CRC match under mask m
+ *                   (0 none, 1 closed loop, 2 beamforming, 3 both: pcc_enc.cpp:170-183)
+ *   iterations      host [n] (optional)
+ * Blocking: returns after the work on the stream has completed.
+ */
+int dnrp_pcc_decode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* plcf_type_test, const int16_t* llr,
+                          uint32_t llr_stride, uint8_t* plcf, uint32_t plcf_stride, uint8_t* result, uint32_t* iterations,
+                          void* stream);
 int dnrp_harq_rx_create(uint32_t N_TB_bits_max, uint32_t Z, dnrp_harq_rx** out);
 int dnrp_harq_rx_reset(dnrp_harq_rx* hb);
 int dnrp_harq_rx_destroy(dnrp_harq_rx* hb);

@@ -75,6 +75,9 @@ def _loop(name, snr_db, n=4, seed=1):
     tb_dev = torch.zeros((n, sz["N_TB_bits"] // 8 + 3), dtype=torch.uint8, device=dev)
     g_ok, _ = FE.pdc_decode_batch(phy, [fcfg] * n, pdc_llr, tb_dev)
     g_tb = tb_dev.cpu().numpy()
+    plcf_dev = torch.zeros((n, 10), dtype=torch.uint8, device=dev)
+    g_res, _ = FE.pcc_decode_batch(phy, plcf_types, pcc_llr, plcf_dev)  # dnrp_pcc_decode_batch
+    g_plcf = plcf_dev.cpu().numpy()
     ocf = O.cfg(u_max, b_max, os_min, L, M)
     ops = O.psdef(*ps_t)
     res = []
@@ -86,7 +89,9 @@ def _loop(name, snr_db, n=4, seed=1):
             ok_d, got_tb, _ = FE.pdc_decode(fcfg, ld)
             res.append((src, i, ok_c, ok_c and (got_plcf == plcfs[i]).all() and (cl, bf) == tuple(map(bool, masks[i])),
                         ok_d, ok_d and (got_tb == tbs[i]).all()))
-        res.append(("gpu-decoder", i, True, True, bool(g_ok[i]),
+        m_exp = 1 + masks[i][0] + 2 * masks[i][1]
+        res.append(("gpu-decoder", i, g_res[i] > 0, g_res[i] == m_exp and (g_plcf[i, : 5 * plcf_types[i]] == plcfs[i]).all(),
+                    bool(g_ok[i]),
                     bool(g_ok[i]) and (g_tb[i, : sz["N_TB_bits"] // 8] == tbs[i]).all()))
     return res
 
@@ -181,3 +186,38 @@ def test_gpu_encoder_matches_host():
     for i in range(m):
         ref = FE.pdc_encode(cfgs[i], tbs[i])
         assert (g[i, : len(ref)] == ref).all(), (i, cfgs[i].N_TB_bits, cfgs[i].G)
+
+
+def test_gpu_plcf_decoder_matches_host():
+    """dnrp_pcc_decode_batch against dnrp_pcc_decode: both PLCF types, all four CRC masks, blind
+    tests of the wrong type, clean to marginal SNRs: same result, iterations and PLCF bytes."""
+    import dnrp
+    import dnrp.fec as FE
+    phy = dnrp.Phy(1, 1, 1, max_batch=1)
+    rng = np.random.default_rng(12)
+    n = 96
+    types, tests, plcfs, llrs = [], [], [], []
+    for i in range(n):
+        t = 1 + i % 2
+        pl = rng.integers(0, 256, 5 * t, dtype=np.uint8)
+        d = FE.pcc_encode(pl, t, (i // 2) % 2, (i // 4) % 2)
+        snr = [30.0, 4.0, 2.0, 0.0, -3.0][i % 5]
+        y = 2.0 * np.unpackbits(d)[:196] - 1 + rng.normal(0, 10 ** (-snr / 20), 196)
+        llrs.append(np.round(np.clip(y * 300, -32768, 32767)).astype(np.int16))
+        types.append(t)
+        tests.append(t if i % 7 else 3 - t)  # every 7th packet tested for the other type
+        plcfs.append(pl)
+    dev = torch.device("cuda:0")
+    llr = torch.from_numpy(np.stack(llrs)).to(dev)
+    plcf = torch.full((n, 12), 0xCD, dtype=torch.uint8, device=dev)
+    res, it = FE.pcc_decode_batch(phy, tests, llr, plcf)
+    g = plcf.cpu().numpy()
+    n_ok = 0
+    for i in range(n):
+        ok, h_pl, cl, bf, h_it = FE.pcc_decode(llrs[i], tests[i])
+        assert (res[i] > 0) == ok and it[i] == h_it, (i, res[i], it[i], ok, h_it)
+        if ok:
+            assert res[i] == 1 + int(cl) + 2 * int(bf)
+            assert (g[i, : 5 * tests[i]] == h_pl).all()
+            n_ok += 1
+    assert 30 <= n_ok < n
