@@ -237,8 +237,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
             map_decode<1>(A, w, blockIdx.x, base, l);
             map_decode<2>(A, w, blockIdx.x, base, l);
             used = it;
-            // CRC remainder over all K bits: 0 for a CRC24 block; for the PLCF's CRC16 the mask it
-            // was sent with (none / closed loop / beamforming / both, pcc_enc.cpp:170-183)
+            // register after all K bits: 0 for a CRC24 block; for the PLCF's CRC16 the register the
+            // mask it was sent with leaves (none / closed loop 0x5555 / beamforming 0xAAAA / both
+            // 0xFFFF, pcc_enc.cpp:170-183) = mask * x^16 mod g: 0, 0xFB1A, 0xE615, 0x1D0F
             const uint32_t W = cb.poly == 0x1021u ? 16u : 24u, msk = (1u << W) - 1;
             uint32_t reg = 0;
             for (uint32_t k = 0; k < w.K; ++k) {
@@ -246,8 +247,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
                 reg = (reg << 1) & msk;
                 if (top ^ bits[(size_t)k * 64 + l]) reg ^= cb.poly;
             }
-            ok = W == 24 ? reg == 0 : (reg == 0 || reg == 0x5555u || reg == 0xAAAAu || reg == 0xFFFFu);
-            mask = reg == 0x5555u ? 1u : (reg == 0xAAAAu ? 2u : (reg == 0xFFFFu ? 3u : 0u));
+            ok = W == 24 ? reg == 0 : (reg == 0 || reg == 0xFB1Au || reg == 0xE615u || reg == 0x1D0Fu);
+            mask = W == 24 ? 0u : (reg == 0xFB1Au ? 1u : (reg == 0xE615u ? 2u : (reg == 0x1D0Fu ? 3u : 0u)));
             if (ok && it >= A.min_iter) done = true;
         }
     }
