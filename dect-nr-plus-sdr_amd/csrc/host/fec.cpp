@@ -657,13 +657,17 @@ static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecC
     std::vector<FecWave> waves;
     std::vector<uint32_t> grp_first_wave{0}, grp_first_cb{0};
     uint64_t data = 0, ck = 0;
-    const uint64_t kMaxGroupBytes = 3ull << 30;
+    // one launch should hold every wave (the kernel is latency-bound: waves resident together
+    // overlap): scratch per launch group up to half the free device memory, at most 32 GiB
+    size_t mem_free = 0, mem_total = 0;
+    (void)hipMemGetInfo(&mem_free, &mem_total);
+    const uint64_t kMaxGroupBytes = std::min<uint64_t>(32ull << 30, std::max<uint64_t>(1ull << 30, mem_free / 2));
     for (uint32_t idx = 0; idx < kNofCbSizes; ++idx) {
         const auto& v = by_idx[idx];
         const uint32_t K = cb_size(idx);
-        const uint64_t wave_bytes = (uint64_t)K * 64 * 5 * 3 + (uint64_t)(K / FEC_WIN) * 8 * 64 * 4;
+        const uint64_t wave_bytes = (uint64_t)K * 64 * 11 + (uint64_t)(K / FEC_WIN) * 8 * 64 * 4;
         for (size_t c0 = 0; c0 < v.size(); c0 += 64) {
-            if (data * 3 + ck * 4 + wave_bytes > kMaxGroupBytes) {  // start a new group (work16 + bits + ck)
+            if (data * 11 / 5 + ck * 4 + wave_bytes > kMaxGroupBytes) {  // new group (work16 + bits + ck)
                 grp_first_wave.push_back((uint32_t)waves.size());
                 grp_first_cb.push_back((uint32_t)cbs.size());
                 data = ck = 0;
@@ -702,7 +706,7 @@ static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecC
         return mx;
     }();
     if (!ctx->fec_cbs.upload(cbs) || !ctx->fec_waves.upload(waves) || !ctx->fec_work16.ensure(max_data * 2) ||
-        !ctx->fec_bits.ensure(max_data) || !ctx->fec_ck.ensure(max_ck * 4 + 16) ||
+        !ctx->fec_bits.ensure(max_data / 5 + 16) || !ctx->fec_ck.ensure(max_ck * 4 + 16) ||
         !ctx->fec_tail.ensure((size_t)n_grp_waves_max * 12 * 64 * 4 + 16) || !ctx->fec_cbout.ensure(cbs.size() * 4 + 16))
         return DNRP_ENOMEM;
     for (size_t g = 0; g + 1 < grp_first_wave.size(); ++g) {

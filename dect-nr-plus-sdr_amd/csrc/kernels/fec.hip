@@ -155,7 +155,7 @@ __device__ void map_decode(const FecArgs& A, const FecWave& w, uint32_t wave, in
         for (int s = 0; s < 8; ++s) be[s] = max(bn[s] - mx, FEC_NEG);
     }
     int16_t* le_out = base + (size_t)(DEC == 1 ? 3 : 4) * K * 64;
-    uint8_t* bits = A.bits + w.data_off;
+    uint8_t* bits = A.bits + w.data_off / 5;
     int32_t cn[8], An2[FEC_WIN], Bn2[FEC_WIN];  // the previous window's checkpoint and inputs, prefetched
 #pragma unroll
     for (int s = 0; s < 8; ++s) cn[s] = ck[((size_t)(nw - 1) * 8 + s) * 64 + l];
@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
     const bool active = l < w.n;
     const FecCb cb = A.cbs[w.first_cb + (active ? l : 0)];
     int16_t* base = A.work16 + w.data_off;
-    const uint8_t* bits = A.bits + w.data_off;
+    const uint8_t* bits = A.bits + w.data_off / 5;
     bool done = !active, ok = false;
     uint32_t used = 0, mask = 0;
     for (uint32_t it = 1; it <= A.max_iter; ++it) {

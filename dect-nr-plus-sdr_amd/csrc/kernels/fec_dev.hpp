@@ -46,7 +46,7 @@ struct FecArgs {
     const FecWave* waves;
     int16_t* work16;     // sys, p1, p2, le1, le2: 5 x K x 64 per wave (data_off)
     int32_t* tail;       // [wave][12][64]
-    uint8_t* bits;       // [wave][K][64] hard decisions (data_off)
+    uint8_t* bits;       // [wave][K][64] hard decisions (at data_off / 5)
     int32_t* ck;         // checkpoints (ck_off)
     uint32_t* cb_out;    // per code block: iterations << 3 | CRC16 mask << 1 | crc ok
     uint32_t n_cb, n_waves, max_iter, min_iter;
