@@ -7,6 +7,9 @@
 //                       segment CRCs per lane joined by GF(2) shifts
 #include "fec_dev.hpp"
 
+#ifndef FEC_BWD_AHEAD
+#define FEC_BWD_AHEAD 1  // backward-pass windows prefetched (2: 256 VGPRs + spills, no gain)
+#endif
 #ifndef FEC_FWD_AHEAD
 #define FEC_FWD_AHEAD 2  // forward-pass windows prefetched (A/B: 1 -> 2 tdec 54.6 -> 46.3 ms, 3 no gain)
 #endif
@@ -168,21 +171,36 @@ __device__ void map_decode(const FecArgs& A, const FecWave& w, uint32_t wave, in
     }
     int16_t* le_out = base + (size_t)(DEC == 1 ? 3 : 4) * K * 64;
     uint8_t* bits = A.bits + w.data_off / 5;
-    int32_t cn[8], An2[FEC_WIN], Bn2[FEC_WIN];  // the previous window's checkpoint and inputs, prefetched
+    // the checkpoints and inputs of the FEC_BWD_AHEAD windows below the current one, prefetched
+    int32_t cb_[FEC_BWD_AHEAD][8], Ab2[FEC_BWD_AHEAD][FEC_WIN], Bb2[FEC_BWD_AHEAD][FEC_WIN];
+    uint32_t pb[FEC_BWD_AHEAD][FEC_WIN], pw[FEC_WIN];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) cn[s] = ck[((size_t)(nw - 1) * 8 + s) * 64 + l];
-    uint32_t pn[FEC_WIN], pw[FEC_WIN];
-    load_win<DEC>(base, q, (nw - 1) * FEC_WIN, l, An2, Bn2, pn);
+    for (int d = 0; d < FEC_BWD_AHEAD; ++d) {
+        const int32_t wd = (int32_t)nw - 1 - d;
+        if (wd >= 0) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) cb_[d][s] = ck[((size_t)wd * 8 + s) * 64 + l];
+            load_win<DEC>(base, q, wd * FEC_WIN, l, Ab2[d], Bb2[d], pb[d]);
+        }
+    }
     for (int32_t wi = (int32_t)nw - 1; wi >= 0; --wi) {
         int32_t aw[FEC_WIN][8], Aw[FEC_WIN], Bw[FEC_WIN];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) aw[0][s] = cn[s];
+        for (int s = 0; s < 8; ++s) aw[0][s] = cb_[0][s];
 #pragma unroll
-        for (int t = 0; t < (int)FEC_WIN; ++t) Aw[t] = An2[t], Bw[t] = Bn2[t], pw[t] = pn[t];
-        if (wi > 0) {
+        for (int t = 0; t < (int)FEC_WIN; ++t) Aw[t] = Ab2[0][t], Bw[t] = Bb2[0][t], pw[t] = pb[0][t];
 #pragma unroll
-            for (int s = 0; s < 8; ++s) cn[s] = ck[((size_t)(wi - 1) * 8 + s) * 64 + l];
-            load_win<DEC>(base, q, (wi - 1) * FEC_WIN, l, An2, Bn2, pn);
+        for (int d = 0; d + 1 < FEC_BWD_AHEAD; ++d) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) cb_[d][s] = cb_[d + 1][s];
+#pragma unroll
+            for (int t = 0; t < (int)FEC_WIN; ++t) Ab2[d][t] = Ab2[d + 1][t], Bb2[d][t] = Bb2[d + 1][t], pb[d][t] = pb[d + 1][t];
+        }
+        if (wi - FEC_BWD_AHEAD >= 0) {
+            const int32_t wd = wi - FEC_BWD_AHEAD;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) cb_[FEC_BWD_AHEAD - 1][s] = ck[((size_t)wd * 8 + s) * 64 + l];
+            load_win<DEC>(base, q, wd * FEC_WIN, l, Ab2[FEC_BWD_AHEAD - 1], Bb2[FEC_BWD_AHEAD - 1], pb[FEC_BWD_AHEAD - 1]);
         }
 #pragma unroll
         for (int t = 0; t < (int)FEC_WIN; ++t) {
