@@ -651,7 +651,8 @@ static int fec_tables(dnrp_ctx* ctx) {
 // (the order of ctx->fec_cbout).
 static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecCb>>& by_idx,
                     const std::vector<std::vector<uint32_t>>& pkt_of, const int16_t* llr, uint8_t* tb,
-                    uint32_t max_iter, uint32_t min_iter, hipStream_t s, std::vector<uint32_t>& cb_pkt) {
+                    uint32_t max_iter, uint32_t min_iter, hipStream_t s, std::vector<uint32_t>& cb_pkt,
+                    int16_t* sb = nullptr, uint8_t* flags = nullptr) {
     using namespace dnrp::dev;
     std::vector<FecCb> cbs;
     std::vector<FecWave> waves;
@@ -720,6 +721,7 @@ static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecC
         A.n_cb = grp_first_cb[g + 1] - grp_first_cb[g];
         A.n_waves = grp_first_wave[g + 1] - grp_first_wave[g];
         A.max_iter = max_iter, A.min_iter = min_iter;
+        A.sb = sb, A.flags = flags;
         ctx->tic("fec_dematch", s);
         if (launch_fec_dematch(A, s)) return DNRP_EDEVICE;
         ctx->toc("fec_dematch", s);
@@ -730,9 +732,9 @@ static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecC
     return DNRP_OK;
 }
 
-extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr,
-                                     uint32_t llr_stride, uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok,
-                                     uint32_t* iterations, void* stream) {
+static int pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr, uint32_t llr_stride,
+                            uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok, uint32_t* iterations, void* stream,
+                            int16_t* sb, uint64_t sb_stride, uint8_t* flags, uint32_t flag_stride) {
     using namespace dnrp::dev;
     if (!ctx || (m && (!cfg || !llr || !tb || !crc_ok))) return DNRP_EINVAL;
     if (m == 0) return DNRP_OK;
@@ -749,6 +751,7 @@ extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
         const Segm& g = sg[i];
         const uint32_t tbs = cfg[i].N_TB_bits, Qm = cfg[i].N_bps, G = cfg[i].G;
         if (llr_stride < G || tb_stride < tbs / 8 + 3) return DNRP_EINVAL;
+        if (sb && (sb_stride < (uint64_t)g.C * 3 * (g.K1 + 4) || flag_stride < g.C)) return DNRP_EINVAL;
         const uint32_t Gp = G / Qm, gamma = Gp % g.C, n_e = Qm * (Gp / g.C);
         uint32_t wp = 0;
         for (uint32_t r = 0; r < g.C; ++r) {
@@ -765,13 +768,15 @@ extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
             cb.start = ctx->fec_start[idx * 4 + cfg[i].rv];
             cb.poly = g.C > 1 ? kCrc24B : kCrc24A;
             cb.out_bytes = g.C > 1 ? (K - 24) / 8 : K / 8;
+            cb.sb_off = (uint64_t)i * sb_stride + (uint64_t)r * 3 * (g.K1 + 4);
+            cb.flag_off = (uint64_t)i * flag_stride + r;
             by_idx[idx].push_back(cb);
             pkt_of[idx].push_back(i);
             wp += g.C > 1 ? K - 24 : K;
         }
     }
     std::vector<uint32_t> cb_pkt, cb_out;
-    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, tb, kPdcMaxIter, kPdcMinIter, s, cb_pkt))) return rc;
+    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, tb, kPdcMaxIter, kPdcMinIter, s, cb_pkt, sb, flags))) return rc;
     // transport-block CRC of the packets with several code blocks
     std::vector<uint64_t> tb_off;
     std::vector<uint32_t> nbytes, multi;
@@ -802,9 +807,39 @@ extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
         if (!(cb_out[c] & 1)) crc_ok[cb_pkt[c]] = 0;
     }
     for (size_t j = 0; j < nm; ++j)
-        if (!tb_ok[j]) crc_ok[multi[j]] = 0;
+        if (!tb_ok[j]) {
+            // every code block passed but the transport block did not: a false alarm, the HARQ flags
+            // of the packet are reset (pdc_enc.cpp:484-488)
+            if (flags && crc_ok[multi[j]]) HIPCHK(hipMemsetAsync(flags + (size_t)multi[j] * flag_stride, 0, sg[multi[j]].C, s));
+            crc_ok[multi[j]] = 0;
+        }
+    HIPCHK(hipStreamSynchronize(s));
     if (iterations)
         for (uint32_t i = 0; i < m; ++i) iterations[i] = it[i];
+    return DNRP_OK;
+}
+
+extern "C" int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr,
+                                     uint32_t llr_stride, uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok,
+                                     uint32_t* iterations, void* stream) {
+    return pdc_decode_batch(ctx, m, cfg, llr, llr_stride, tb, tb_stride, crc_ok, iterations, stream, nullptr, 0,
+                            nullptr, 0);
+}
+
+extern "C" int dnrp_pdc_decode_batch_harq(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr,
+                                          uint32_t llr_stride, int16_t* softbuf, uint64_t sb_stride, uint8_t* cb_crc,
+                                          uint32_t crc_stride, uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok,
+                                          uint32_t* iterations, void* stream) {
+    if (!softbuf || !cb_crc) return DNRP_EINVAL;
+    return pdc_decode_batch(ctx, m, cfg, llr, llr_stride, tb, tb_stride, crc_ok, iterations, stream, softbuf,
+                            sb_stride, cb_crc, crc_stride);
+}
+
+extern "C" int dnrp_pdc_softbuffer_size(uint32_t N_TB_bits, uint32_t Z, uint64_t* entries, uint32_t* n_cb) {
+    Segm g;
+    if (!entries || cbsegm(N_TB_bits, Z, &g) != 0) return DNRP_EINVAL;
+    *entries = (uint64_t)g.C * 3 * (g.K1 + 4);
+    if (n_cb) *n_cb = g.C;
     return DNRP_OK;
 }
 

@@ -30,15 +30,20 @@ __global__ void __launch_bounds__(256) fec_dematch_kernel(FecArgs A) {
     const int16_t* llr = A.llr + cb.llr_off;
     // tail slot of (stream, t = index - K), as fec.cpp Tdec::load orders them
     const uint8_t tslot[3][4] = {{0, 4, 6, 10}, {3, 2, 9, 8}, {1, 5, 7, 11}};
+    // HARQ: a block that passed its CRC in an earlier transmission is neither combined nor decoded
+    // (pdc_enc.cpp:346-406); the others add the new soft bits to their softbuffer
+    const bool harq = A.sb != nullptr && active && !A.flags[cb.flag_off];
     for (uint32_t q = r; q < nvalid; q += 4) {
+        const uint32_t e = valid[q], st = e >> 16, idx = e & 0xFFFF;
         // soft bits j = j0, j0 + nvalid, ... land on list entry q; summed in j order with int16
-        // saturation like the host's sequential accumulation
-        int32_t sum = 0;
+        // saturation like the host's sequential accumulation (starting from the softbuffer value)
+        int16_t* sbe = harq ? A.sb + cb.sb_off + (size_t)st * (K + 4) + idx : nullptr;
+        int32_t sum = harq ? *sbe : 0;
         if (active) {
             uint32_t j = q >= cb.start ? q - cb.start : q + nvalid - cb.start;
             for (; j < cb.E; j += nvalid) sum = min(32767, max(-32768, sum + (int32_t)llr[j]));
         }
-        const uint32_t e = valid[q], st = e >> 16, idx = e & 0xFFFF;
+        if (harq) *sbe = (int16_t)sum;
         if (idx < K) base[(size_t)st * K * 64 + (size_t)idx * 64 + l] = (int16_t)sum;
         else A.tail[(size_t)blockIdx.x * 12 * 64 + tslot[st][idx - K] * 64 + l] = sum;
     }
@@ -259,7 +264,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
     const FecCb cb = A.cbs[w.first_cb + (active ? l : 0)];
     int16_t* base = A.work16 + w.data_off;
     const uint8_t* bits = A.bits + w.data_off / 5;
-    bool done = !active, ok = false;
+    const bool kept = A.sb != nullptr && active && A.flags[cb.flag_off];  // HARQ: decoded earlier
+    bool done = !active || kept, ok = kept;
     uint32_t used = 0, mask = 0;
     for (uint32_t it = 1; it <= A.max_iter; ++it) {
         if (__all(done)) break;
@@ -284,6 +290,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
     }
     if (!active) return;
     ok = done && ok;
+    if (kept) {  // its bytes from the earlier decode stay in the output row
+        A.cb_out[w.first_cb + l] = 1u;
+        return;
+    }
+    if (A.sb != nullptr && ok) A.flags[cb.flag_off] = 1;
     for (uint32_t j = 0; j < cb.out_bytes; ++j) {
         uint32_t v = 0;
 #pragma unroll

@@ -27,6 +27,8 @@ struct FecCb {           // one code block
     uint32_t wave, lane;
     uint32_t poly;       // CRC over the K decoded bits: CRC24B (C > 1), CRC24A (C == 1), CRC16 (PLCF)
     uint32_t out_bytes;  // decoded bytes written (K/8 for C == 1, (K-24)/8 otherwise)
+    uint64_t sb_off;     // HARQ: element offset of its softbuffer (3 streams x (K + 4), stream-major)
+    uint64_t flag_off;   // HARQ: its code-block CRC flag
 };
 
 struct FecWave {
@@ -49,6 +51,8 @@ struct FecArgs {
     uint8_t* bits;       // [wave][K][64] hard decisions (at data_off / 5)
     int32_t* ck;         // checkpoints (ck_off)
     uint32_t* cb_out;    // per code block: iterations << 3 | CRC16 mask << 1 | crc ok
+    int16_t* sb;         // HARQ softbuffers (nullptr: one-shot decoding)
+    uint8_t* flags;      // HARQ code-block CRC flags (softbuffer->cb_crc)
     uint32_t n_cb, n_waves, max_iter, min_iter;
 };
 

@@ -56,6 +56,9 @@ def lib():
         L.dnrp_pdc_decode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P]
         L.dnrp_pdc_encode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P]
         L.dnrp_pcc_decode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P]
+        L.dnrp_pdc_decode_batch_harq.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint64, P, C.c_uint32, P,
+                                                 C.c_uint32, P, P, P]
+        L.dnrp_pdc_softbuffer_size.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
         _ready = True
     return L
 
@@ -199,3 +202,30 @@ def pcc_decode_batch(phy, plcf_types, llr, plcf, stream=None):
                                      C.c_void_p(plcf.data_ptr()), plcf.shape[1], _ptr(res), _ptr(it),
                                      _stream_ptr(stream)), "dnrp_pcc_decode_batch")
     return res, it
+
+
+def softbuffer_size(N_TB_bits, Z=6144):
+    """-> (softbuffer entries, code blocks) of one transport block"""
+    e, c = C.c_uint64(), C.c_uint32()
+    _chk(lib().dnrp_pdc_softbuffer_size(N_TB_bits, Z, C.byref(e), C.byref(c)), "dnrp_pdc_softbuffer_size")
+    return e.value, c.value
+
+
+def pdc_decode_batch_harq(phy, cfgs, llr, softbuf, cb_crc, tb, stream=None):
+    """GPU turbo decoding with HARQ soft combining: softbuf int16 [m][>= entries], cb_crc uint8 [m][>= C]
+    device tensors zeroed for a new transport block and kept across its redundancy versions; tb as for
+    pdc_decode_batch (same rows every redundancy version). -> (crc_ok [m], iterations [m])"""
+    import torch
+    from . import _stream_ptr
+    m = len(cfgs)
+    for t, dt in ((llr, torch.int16), (softbuf, torch.int16), (cb_crc, torch.uint8), (tb, torch.uint8)):
+        assert t.dtype == dt and t.dim() == 2 and t.is_contiguous() and t.shape[0] >= m and t.is_cuda
+    arr = (FecCfg * max(m, 1))(*cfgs)
+    ok = np.zeros(m, np.uint8)
+    it = np.zeros(m, np.uint32)
+    _chk(lib().dnrp_pdc_decode_batch_harq(phy._ctx, m, arr, C.c_void_p(llr.data_ptr()), llr.shape[1],
+                                          C.c_void_p(softbuf.data_ptr()), softbuf.shape[1],
+                                          C.c_void_p(cb_crc.data_ptr()), cb_crc.shape[1], C.c_void_p(tb.data_ptr()),
+                                          tb.shape[1], _ptr(ok), _ptr(it), _stream_ptr(stream)),
+         "dnrp_pdc_decode_batch_harq")
+    return ok.astype(bool), it

@@ -425,6 +425,19 @@ int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* ll
  */
 int dnrp_pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr, uint32_t llr_stride,
                           uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok, uint32_t* iterations, void* stream);
+/* The same with HARQ soft combining (harq::buffer_rx_t on the device): per packet a softbuffer row
+ * (softbuf + i*sb_stride int16, >= dnrp_pdc_softbuffer_size entries) and code-block CRC flags
+ * (cb_crc + i*crc_stride, >= C bytes), both zeroed by the caller for a new transport block and kept
+ * across its redundancy versions, like the host dnrp_pdc_decode with a dnrp_harq_rx: blocks that
+ * passed earlier are neither combined nor decoded again (their bytes stay in the tb row, so pass the
+ * same tb rows for every redundancy version), the others add the new soft bits; a transport-block
+ * CRC failure after all block CRCs passed resets the packet's flags. Same results as the host path. */
+int dnrp_pdc_decode_batch_harq(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const int16_t* llr,
+                               uint32_t llr_stride, int16_t* softbuf, uint64_t sb_stride, uint8_t* cb_crc,
+                               uint32_t crc_stride, uint8_t* tb, uint32_t tb_stride, uint8_t* crc_ok, uint32_t* iterations,
+                               void* stream);
+/* softbuffer entries (C * 3 * (K+ + 4)) and code blocks of a transport block (host only) */
+int dnrp_pdc_softbuffer_size(uint32_t N_TB_bits, uint32_t Z, uint64_t* entries, uint32_t* n_cb);
 /*
  * Device channel encoding of m transport blocks <- fec_t::encode_tb for many packets at once
  * (without the scrambling): bit-exact with dnrp_pdc_encode.

@@ -221,3 +221,56 @@ def test_gpu_plcf_decoder_matches_host():
             assert (g[i, : 5 * tests[i]] == h_pl).all()
             n_ok += 1
     assert 30 <= n_ok < n
+
+
+def test_gpu_harq_combining_matches_host():
+    """dnrp_pdc_decode_batch_harq over redundancy versions 0, 2, 3, 1 of the same transport blocks at
+    an SNR where one transmission is not enough, against the host decoder with a dnrp_harq_rx per
+    packet (pdc_decode_codeblocks' softbuffer semantics): identical CRC status, iterations and bytes
+    after every redundancy version."""
+    import dnrp
+    import dnrp.fec as FE
+    import fec_np as ON  # noqa: F401
+    phy = dnrp.Phy(1, 1, 1, max_batch=1)
+    rng = np.random.default_rng(21)
+    cases = [(4136, 2, 6000, -3.0), (14560, 4, 19572, -1.0), (14560, 4, 19572, 6.0), (45432, 8, 60000, 0.0),
+             (296, 2, 644, -4.0), (2960, 1, 7000, -2.0)]
+    cfgs, tbs, snrs = [], [], []
+    for tbs_bits, Qm, G, snr in cases:
+        while ON.cbsegm(tbs_bits, 6144)[2] != 0:
+            tbs_bits += 8
+        G -= G % Qm
+        cfgs.append(FE.fec_cfg(tbs_bits, Qm, G))
+        tbs.append(rng.integers(0, 256, tbs_bits // 8, dtype=np.uint8))
+        snrs.append(snr)
+    m = len(cfgs)
+    dev = torch.device("cuda:0")
+    ent = max(FE.softbuffer_size(c.N_TB_bits)[0] for c in cfgs)
+    ncb = max(FE.softbuffer_size(c.N_TB_bits)[1] for c in cfgs)
+    sb = torch.zeros((m, ent), dtype=torch.int16, device=dev)
+    flags = torch.zeros((m, ncb), dtype=torch.uint8, device=dev)
+    tb_dev = torch.zeros((m, max(c.N_TB_bits for c in cfgs) // 8 + 3), dtype=torch.uint8, device=dev)
+    hbs = [FE.HarqRx(c.N_TB_bits) for c in cfgs]
+    g_max = max(c.G for c in cfgs)
+    n_ok_first = None
+    for rv in (0, 2, 3, 1):
+        llr = np.zeros((m, g_max), np.int16)
+        rows = []
+        for i, c in enumerate(cfgs):
+            ci = FE.fec_cfg(c.N_TB_bits, c.N_bps, c.G, rv=rv)
+            cfgs[i] = ci
+            x = 2.0 * np.unpackbits(FE.pdc_encode(ci, tbs[i]))[: c.G] - 1
+            y = x + rng.normal(0, 10 ** (-snrs[i] / 20), c.G)
+            rows.append(np.round(np.clip(y * 200, -32768, 32767)).astype(np.int16))
+            llr[i, : c.G] = rows[-1]
+        ok, it = FE.pdc_decode_batch_harq(phy, cfgs, torch.from_numpy(llr).to(dev), sb, flags, tb_dev)
+        g_tb = tb_dev.cpu().numpy()
+        for i in range(m):
+            h_ok, h_tb, h_it = FE.pdc_decode(cfgs[i], rows[i], hbs[i])
+            assert (bool(ok[i]), int(it[i])) == (h_ok, h_it), (rv, i, ok[i], it[i], h_ok, h_it)
+            assert (g_tb[i, : cfgs[i].N_TB_bits // 8] == h_tb).all(), (rv, i)
+            if h_ok:
+                assert (h_tb == tbs[i]).all()
+        if n_ok_first is None:
+            n_ok_first = int(ok.sum())
+    assert n_ok_first < m and int(ok.sum()) > n_ok_first
