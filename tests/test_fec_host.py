@@ -212,3 +212,16 @@ def test_pdc_noise_harq_and_crc_failure():
 def test_pdc_filler_bits_rejected():
     with pytest.raises(dnrp.DnrpError):
         F.pdc_encode(F.fec_cfg(2048, 4, 5000), np.zeros(256, np.uint8))
+
+
+def test_device_entry_points_validate_before_device():
+    """The GPU FEC entry points reject bad arguments before touching a device (no GPU here)."""
+    L = F.lib()
+    assert L.dnrp_pdc_decode_batch(None, 1, None, None, 0, None, 0, None, None, None) == -1
+    assert L.dnrp_pdc_decode_batch_harq(None, 1, None, None, 0, None, 0, None, 0, None, 0, None, None, None) == -1
+    assert L.dnrp_pdc_encode_batch(None, 1, None, None, 0, None, 0, None) == -1
+    assert L.dnrp_pcc_decode_batch(None, 1, None, None, 0, None, 0, None, None, None) == -1
+    e, c = F.softbuffer_size(363464)
+    assert c == 60 and e == 60 * 3 * (6144 + 4)
+    with pytest.raises(dnrp.DnrpError):
+        F.softbuffer_size(363464, Z=0)
