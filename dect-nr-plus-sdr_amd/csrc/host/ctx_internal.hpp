@@ -200,6 +200,7 @@ struct dnrp_ctx {
     // device turbo decoding (fec.cpp dnrp_pdc_decode_batch, kernels/fec.hip): per-size tables
     // (circular-buffer lists) built at the first call, plan and work buffers
     dbuf fec_tab, fec_cbs, fec_waves, fec_work16, fec_tail, fec_bits, fec_ck, fec_cbout, fec_tbarg;
+    dbuf fec_cbs2, fec_waves2, fec_map2, fec_work16b, fec_tailb, fec_cbout2;  // continuation of undecided blocks
     std::vector<uint32_t> fec_valid_off, fec_start;  // per K index ([idx][rv] for start)
     ~dnrp_ctx() {
         for (auto& e : ev)

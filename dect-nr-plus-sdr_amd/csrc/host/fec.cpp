@@ -632,6 +632,10 @@ int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* ll
 }  // extern "C"
 
 // ---- device turbo decoding -----------------------------------------------------------------------
+// PDC decoding runs the first kPdcSplit iterations for every code block, then continues the undecided
+// ones in dense waves (run_tdec)
+static constexpr uint32_t kPdcSplit = 3;
+
 static int fec_tables(dnrp_ctx* ctx) {
     if (!ctx->fec_valid_off.empty()) return DNRP_OK;
     std::vector<uint32_t> tab, voff(kNofCbSizes), st(kNofCbSizes * 4);
@@ -651,8 +655,8 @@ static int fec_tables(dnrp_ctx* ctx) {
 // (the order of ctx->fec_cbout).
 static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecCb>>& by_idx,
                     const std::vector<std::vector<uint32_t>>& pkt_of, const int16_t* llr, uint8_t* tb,
-                    uint32_t max_iter, uint32_t min_iter, hipStream_t s, std::vector<uint32_t>& cb_pkt,
-                    int16_t* sb = nullptr, uint8_t* flags = nullptr) {
+                    uint32_t max_iter, uint32_t min_iter, uint32_t split, hipStream_t s, std::vector<uint32_t>& cb_pkt,
+                    std::vector<uint32_t>& cb_out, int16_t* sb = nullptr, uint8_t* flags = nullptr) {
     using namespace dnrp::dev;
     std::vector<FecCb> cbs;
     std::vector<FecWave> waves;
@@ -710,6 +714,11 @@ static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecC
         !ctx->fec_bits.ensure(max_data / 5 + 16) || !ctx->fec_ck.ensure(max_ck * 4 + 16) ||
         !ctx->fec_tail.ensure((size_t)n_grp_waves_max * 12 * 64 * 4 + 16) || !ctx->fec_cbout.ensure(cbs.size() * 4 + 16))
         return DNRP_ENOMEM;
+    // Every launch group runs the first `split` iterations for all its code blocks, then the blocks
+    // still undecided are gathered densely into new waves and continue from their state (a wave
+    // otherwise runs until its slowest lane stops: at marginal SNR one failing block in 64 held
+    // the other 63 to the maximum). Same iterations, same results as one pass.
+    cb_out.assign(cbs.size(), 0);
     for (size_t g = 0; g + 1 < grp_first_wave.size(); ++g) {
         FecArgs A{};
         A.llr = llr, A.tb = tb, A.tab = ctx->fec_tab.as<uint32_t>();
@@ -720,7 +729,8 @@ static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecC
         A.cb_out = ctx->fec_cbout.as<uint32_t>() + grp_first_cb[g];
         A.n_cb = grp_first_cb[g + 1] - grp_first_cb[g];
         A.n_waves = grp_first_wave[g + 1] - grp_first_wave[g];
-        A.max_iter = max_iter, A.min_iter = min_iter;
+        const bool two = split > 0 && split < max_iter;
+        A.max_iter = two ? split : max_iter, A.min_iter = min_iter, A.it_first = 1, A.final_pass = two ? 0 : 1;
         A.sb = sb, A.flags = flags;
         ctx->tic("fec_dematch", s);
         if (launch_fec_dematch(A, s)) return DNRP_EDEVICE;
@@ -728,6 +738,57 @@ static int run_tdec(dnrp_ctx* ctx, const std::vector<std::vector<dnrp::dev::FecC
         ctx->tic("fec_tdec", s);
         if (launch_fec_tdec(A, A.n_waves, s)) return DNRP_EDEVICE;
         ctx->toc("fec_tdec", s);
+        uint32_t* out = cb_out.data() + grp_first_cb[g];
+        HIPCHK(hipMemcpyAsync(out, A.cb_out, (size_t)A.n_cb * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (!two) continue;
+        // undecided blocks of the group -> dense waves per size (the group's waves are size-ordered)
+        std::vector<FecCb> cbs2;
+        std::vector<FecWave> waves2;
+        std::vector<uint32_t> src_of, slot;
+        uint64_t d2 = 0, c2 = 0;
+        for (uint32_t wi = 0; wi < A.n_waves; ++wi) {
+            const FecWave& ow = waves[grp_first_wave[g] + wi];
+            for (uint32_t l = 0; l < ow.n; ++l) {
+                const uint32_t c = ow.first_cb + l;  // group-relative
+                if (!(out[c] & 8u)) continue;
+                if (waves2.empty() || waves2.back().K != ow.K || waves2.back().n == 64) {
+                    FecWave nw = ow;
+                    nw.data_off = d2, nw.ck_off = c2, nw.n = 0, nw.first_cb = (uint32_t)cbs2.size();
+                    waves2.push_back(nw);
+                    d2 += (uint64_t)5 * ow.K * 64;
+                    c2 += (uint64_t)(ow.K / FEC_WIN) * 8 * 64;
+                }
+                FecCb cb = cbs[grp_first_cb[g] + c];
+                cb.wave = (uint32_t)waves2.size() - 1, cb.lane = waves2.back().n++;
+                cbs2.push_back(cb);
+                src_of.push_back(wi << 6 | l);
+                slot.push_back(c);
+            }
+        }
+        if (cbs2.empty()) continue;
+        if (!ctx->fec_cbs2.upload(cbs2) || !ctx->fec_waves2.upload(waves2) || !ctx->fec_map2.upload(src_of) ||
+            !ctx->fec_work16b.ensure(d2 * 2 + 16) || !ctx->fec_tailb.ensure(waves2.size() * 12 * 64 * 4 + 16) ||
+            !ctx->fec_cbout2.ensure(cbs2.size() * 4 + 16))
+            return DNRP_ENOMEM;
+        FecCompactArgs Cp{};
+        Cp.src16 = A.work16, Cp.src_tail = A.tail, Cp.src_waves = A.waves;
+        Cp.dst16 = ctx->fec_work16b.as<int16_t>(), Cp.dst_tail = ctx->fec_tailb.as<int32_t>();
+        Cp.dst_waves = ctx->fec_waves2.as<FecWave>(), Cp.src_of = ctx->fec_map2.as<uint32_t>();
+        if (launch_fec_compact(Cp, (uint32_t)waves2.size(), s)) return DNRP_EDEVICE;
+        FecArgs B = A;
+        B.cbs = ctx->fec_cbs2.as<FecCb>(), B.waves = ctx->fec_waves2.as<FecWave>();
+        B.work16 = ctx->fec_work16b.as<int16_t>(), B.tail = ctx->fec_tailb.as<int32_t>();
+        B.cb_out = ctx->fec_cbout2.as<uint32_t>();
+        B.n_cb = (uint32_t)cbs2.size(), B.n_waves = (uint32_t)waves2.size();
+        B.max_iter = max_iter, B.it_first = split + 1, B.final_pass = 1;
+        ctx->tic("fec_tdec", s);
+        if (launch_fec_tdec(B, B.n_waves, s)) return DNRP_EDEVICE;
+        ctx->toc("fec_tdec", s);
+        std::vector<uint32_t> o2(cbs2.size());
+        HIPCHK(hipMemcpyAsync(o2.data(), B.cb_out, o2.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (size_t j = 0; j < o2.size(); ++j) out[slot[j]] = o2[j];
     }
     return DNRP_OK;
 }
@@ -776,7 +837,8 @@ static int pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, 
         }
     }
     std::vector<uint32_t> cb_pkt, cb_out;
-    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, tb, kPdcMaxIter, kPdcMinIter, s, cb_pkt, sb, flags))) return rc;
+    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, tb, kPdcMaxIter, kPdcMinIter, kPdcSplit, s, cb_pkt, cb_out, sb, flags)))
+        return rc;
     // transport-block CRC of the packets with several code blocks
     std::vector<uint64_t> tb_off;
     std::vector<uint32_t> nbytes, multi;
@@ -796,14 +858,12 @@ static int pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, 
         if (launch_fec_tbcrc(T, s)) return DNRP_EDEVICE;
     }
     std::vector<uint32_t> tb_ok(nm);
-    cb_out.resize(cb_pkt.size());
-    HIPCHK(hipMemcpyAsync(cb_out.data(), ctx->fec_cbout.p, cb_out.size() * 4, hipMemcpyDeviceToHost, s));
     if (nm) HIPCHK(hipMemcpyAsync(tb_ok.data(), ctx->fec_tbarg.as<uint8_t>() + nm * 12, nm * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     std::vector<uint32_t> it(m, 0);
     for (uint32_t i = 0; i < m; ++i) crc_ok[i] = 1;
     for (size_t c = 0; c < cb_out.size(); ++c) {
-        it[cb_pkt[c]] += cb_out[c] >> 3;
+        it[cb_pkt[c]] += cb_out[c] >> 4;
         if (!(cb_out[c] & 1)) crc_ok[cb_pkt[c]] = 0;
     }
     for (size_t j = 0; j < nm; ++j)
@@ -954,14 +1014,11 @@ extern "C" int dnrp_pcc_decode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* 
         pkt_of[idx].push_back(i);
     }
     std::vector<uint32_t> cb_pkt, cb_out;
-    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, plcf, kPccMaxIter, 1, s, cb_pkt))) return rc;
-    cb_out.resize(cb_pkt.size());
-    HIPCHK(hipMemcpyAsync(cb_out.data(), ctx->fec_cbout.p, cb_out.size() * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, plcf, kPccMaxIter, 1, 0, s, cb_pkt, cb_out))) return rc;
     for (size_t c = 0; c < cb_out.size(); ++c) {
         const uint32_t i = cb_pkt[c];
         result[i] = (cb_out[c] & 1) ? (uint8_t)(1 + ((cb_out[c] >> 1) & 3)) : 0;
-        if (iterations) iterations[i] = cb_out[c] >> 3;
+        if (iterations) iterations[i] = cb_out[c] >> 4;
     }
     return DNRP_OK;
 }

@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
     const bool kept = A.sb != nullptr && active && A.flags[cb.flag_off];  // HARQ: decoded earlier
     bool done = !active || kept, ok = kept;
     uint32_t used = 0, mask = 0;
-    for (uint32_t it = 1; it <= A.max_iter; ++it) {
+    for (uint32_t it = A.it_first; it <= A.max_iter; ++it) {
         if (__all(done)) break;
         if (!done) {
             map_decode<1>(A, w, blockIdx.x, base, l);
@@ -289,6 +289,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
         }
     }
     if (!active) return;
+    if (!done && !A.final_pass) {  // undecided: its streams and extrinsic stay for the continuation
+        A.cb_out[w.first_cb + l] = (used << 4) | 8u;
+        return;
+    }
     ok = done && ok;
     if (kept) {  // its bytes from the earlier decode stay in the output row
         A.cb_out[w.first_cb + l] = 1u;
@@ -301,7 +305,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
         for (int t = 0; t < 8; ++t) v = (v << 1) | bits[(size_t)(8 * j + t) * 64 + l];
         A.tb[cb.tb_off + j] = (uint8_t)v;
     }
-    A.cb_out[w.first_cb + l] = (used << 3) | (mask << 1) | (ok ? 1u : 0u);
+    A.cb_out[w.first_cb + l] = (used << 4) | (mask << 1) | (ok ? 1u : 0u);
 }
 
 // GF(2)[x] / CRC24A helpers for joining segment CRCs: crc(A || B) = crc(A) x^{|B|} + crc(B)
@@ -456,6 +460,34 @@ int launch_fec_encode(const FecEncArgs& a, uint32_t n_waves, hipStream_t s) {
 int launch_fec_pack(const FecPackArgs& a, hipStream_t s) {
     if (a.n == 0) return 0;
     hipLaunchKernelGGL(fec_pack_kernel, dim3((a.max_bytes + 255) / 256 < 256 ? (a.max_bytes + 255) / 256 : 256, a.n), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// continuation gather: the soft streams, decoder 2's extrinsic and the tails of the undecided code
+// blocks, [k][old lane] of their old waves -> [k][new lane] of dense new waves of the same size
+__global__ void __launch_bounds__(256) fec_compact_kernel(FecCompactArgs A) {
+    const FecWave w = A.dst_waves[blockIdx.x];
+    const uint32_t l = threadIdx.x & 63u, r = threadIdx.x >> 6, K = w.K;
+    if (l >= w.n) return;
+    const uint32_t so = A.src_of[w.first_cb + l], sw = so >> 6, sl = so & 63u;
+    const FecWave ow = A.src_waves[sw];
+    const int16_t* src = A.src16 + ow.data_off;
+    int16_t* dst = A.dst16 + w.data_off;
+    for (uint32_t k = r; k < K; k += 4) {
+#pragma unroll
+        for (int st = 0; st < 5; ++st) {
+            if (st == 3) continue;  // decoder 1's extrinsic is recomputed
+            dst[(size_t)st * K * 64 + (size_t)k * 64 + l] = src[(size_t)st * K * 64 + (size_t)k * 64 + sl];
+        }
+    }
+    if (r == 0)
+        for (int t = 0; t < 12; ++t)
+            A.dst_tail[(size_t)blockIdx.x * 12 * 64 + t * 64 + l] = A.src_tail[(size_t)sw * 12 * 64 + t * 64 + sl];
+}
+
+int launch_fec_compact(const FecCompactArgs& a, uint32_t n_waves, hipStream_t s) {
+    if (n_waves == 0) return 0;
+    hipLaunchKernelGGL(fec_compact_kernel, dim3(n_waves), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

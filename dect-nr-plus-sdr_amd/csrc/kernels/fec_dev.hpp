@@ -50,10 +50,22 @@ struct FecArgs {
     int32_t* tail;       // [wave][12][64]
     uint8_t* bits;       // [wave][K][64] hard decisions (at data_off / 5)
     int32_t* ck;         // checkpoints (ck_off)
-    uint32_t* cb_out;    // per code block: iterations << 3 | CRC16 mask << 1 | crc ok
+    uint32_t* cb_out;    // per code block: iterations << 4 | pending << 3 | CRC16 mask << 1 | crc ok
     int16_t* sb;         // HARQ softbuffers (nullptr: one-shot decoding)
     uint8_t* flags;      // HARQ code-block CRC flags (softbuffer->cb_crc)
     uint32_t n_cb, n_waves, max_iter, min_iter;
+    uint32_t it_first;   // first iteration number of this launch (1, or the split + 1 of a continuation)
+    uint32_t final_pass; // 0: blocks still undecided after max_iter keep their state and report pending
+};
+
+struct FecCompactArgs {  // continuation: undecided blocks gathered densely into new waves
+    const int16_t* src16;
+    const int32_t* src_tail;
+    const FecWave* src_waves;
+    int16_t* dst16;
+    int32_t* dst_tail;
+    const FecWave* dst_waves;
+    const uint32_t* src_of;  // per new code block: source wave << 6 | source lane
 };
 
 struct FecTbArgs {       // transport-block CRC24A of packets with C > 1
@@ -96,6 +108,7 @@ struct FecPackArgs {          // ebits -> packed MSB-first d rows
 
 int launch_fec_dematch(const FecArgs& a, hipStream_t s);
 int launch_fec_tdec(const FecArgs& a, uint32_t n_waves, hipStream_t s);
+int launch_fec_compact(const FecCompactArgs& a, uint32_t n_waves, hipStream_t s);
 int launch_fec_tbcrc(const FecTbArgs& a, hipStream_t s);
 int launch_fec_encode(const FecEncArgs& a, uint32_t n_waves, hipStream_t s);
 int launch_fec_pack(const FecPackArgs& a, hipStream_t s);
