@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -634,7 +635,14 @@ int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* ll
 // ---- device turbo decoding -----------------------------------------------------------------------
 // PDC decoding runs the first kPdcSplit iterations for every code block, then continues the undecided
 // ones in dense waves (run_tdec)
-static constexpr uint32_t kPdcSplit = 3;
+// (DNRP_FEC_SPLIT overrides it for A/B runs; 0 = one pass)
+static uint32_t pdc_split() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("DNRP_FEC_SPLIT");
+        return e ? (uint32_t)std::atoi(e) : 3u;
+    }();
+    return v;
+}
 
 static int fec_tables(dnrp_ctx* ctx) {
     if (!ctx->fec_valid_off.empty()) return DNRP_OK;
@@ -837,7 +845,7 @@ static int pdc_decode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, 
         }
     }
     std::vector<uint32_t> cb_pkt, cb_out;
-    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, tb, kPdcMaxIter, kPdcMinIter, kPdcSplit, s, cb_pkt, cb_out, sb, flags)))
+    if ((rc = run_tdec(ctx, by_idx, pkt_of, llr, tb, kPdcMaxIter, kPdcMinIter, pdc_split(), s, cb_pkt, cb_out, sb, flags)))
         return rc;
     // transport-block CRC of the packets with several code blocks
     std::vector<uint64_t> tb_off;
