@@ -47,8 +47,7 @@ __global__ void __launch_bounds__(256) fec_dematch_kernel(FecArgs A) {
         if (idx < K) base[(size_t)st * K * 64 + (size_t)idx * 64 + l] = (int16_t)sum;
         else A.tail[(size_t)blockIdx.x * 12 * 64 + tslot[st][idx - K] * 64 + l] = sum;
     }
-    int16_t* le2 = base + (size_t)4 * K * 64;
-    for (uint32_t k = r; k < K; k += 4) le2[(size_t)k * 64 + l] = 0;
+    // decoder 2's extrinsic needs no zero fill: the first iteration's decoder 1 reads none
 }
 
 // One trellis step of the forward recursion (state s = 4 s1 + 2 s2 + s3; next n = (a, s1, s2),
@@ -93,8 +92,8 @@ __device__ __forceinline__ void inputs(const int16_t* base, uint32_t K, uint32_t
                                        int32_t* b) {
     const int16_t *sys = base, *p1 = base + (size_t)K * 64, *p2 = base + (size_t)2 * K * 64;
     const int16_t *le1 = base + (size_t)3 * K * 64, *le2 = base + (size_t)4 * K * 64;
-    if (DEC == 1) {
-        *a = (int32_t)sys[(size_t)k * 64 + l] + le2[(size_t)k * 64 + l];
+    if (DEC != 2) {  // DEC 0: decoder 1 of the first iteration, whose a priori is zero
+        *a = (int32_t)sys[(size_t)k * 64 + l] + (DEC == 1 ? (int32_t)le2[(size_t)k * 64 + l] : 0);
         *b = p1[(size_t)k * 64 + l];
     } else {
         *a = (int32_t)sys[(size_t)pi * 64 + l] + le1[(size_t)pi * 64 + l];
@@ -154,7 +153,7 @@ __device__ void map_decode(const FecArgs& A, const FecWave& w, uint32_t wave, in
         for (int t = 0; t < (int)FEC_WIN; ++t) fwd_step(a, Ak[t], Bk[t]);
     }
     // backward through the termination
-    const int32_t* tl = A.tail + (size_t)wave * 12 * 64 + (DEC == 1 ? 0 : 6) * 64 + l;
+    const int32_t* tl = A.tail + (size_t)wave * 12 * 64 + (DEC == 2 ? 6 : 0) * 64 + l;
     int32_t be[8], bn[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) be[s] = s == 0 ? 0 : FEC_NEG;
@@ -174,7 +173,7 @@ __device__ void map_decode(const FecArgs& A, const FecWave& w, uint32_t wave, in
 #pragma unroll
         for (int s = 0; s < 8; ++s) be[s] = max(bn[s] - mx, FEC_NEG);
     }
-    int16_t* le_out = base + (size_t)(DEC == 1 ? 3 : 4) * K * 64;
+    int16_t* le_out = base + (size_t)(DEC == 2 ? 4 : 3) * K * 64;
     uint8_t* bits = A.bits + w.data_off / 5;
     // the checkpoints and inputs of the FEC_BWD_AHEAD windows below the current one, prefetched
     int32_t cb_[FEC_BWD_AHEAD][8], Ab2[FEC_BWD_AHEAD][FEC_WIN], Bb2[FEC_BWD_AHEAD][FEC_WIN];
@@ -237,7 +236,7 @@ __device__ void map_decode(const FecArgs& A, const FecWave& w, uint32_t wave, in
             }
             const int32_t llr = m1 - m0;
             const int32_t e = min(32767, max(-32767, ((llr - Ak) * 3) >> 2));
-            if (DEC == 1) {
+            if (DEC != 2) {
                 le_out[(size_t)k * 64 + l] = (int16_t)e;
             } else {  // natural order: decoder 1's a priori and the hard decisions at pi(k)
                 le_out[(size_t)pw[t] * 64 + l] = (int16_t)e;
@@ -270,7 +269,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
     for (uint32_t it = A.it_first; it <= A.max_iter; ++it) {
         if (__all(done)) break;
         if (!done) {
-            map_decode<1>(A, w, blockIdx.x, base, l);
+            if (it == 1)
+                map_decode<0>(A, w, blockIdx.x, base, l);
+            else
+                map_decode<1>(A, w, blockIdx.x, base, l);
             map_decode<2>(A, w, blockIdx.x, base, l);
             used = it;
             // register after all K bits: 0 for a CRC24 block; for the PLCF's CRC16 the register the
