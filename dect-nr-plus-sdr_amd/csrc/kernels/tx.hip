@@ -487,14 +487,15 @@ struct txs_wave {
         const float2 d = cscale(MODE == TXS_TXDIV ? wa_drs : wrow[j & 7u], (j & 8u) ? -1.f : 1.f);
         v = ty == CODE_DRS ? d : v;
         v = (ty == CODE_PDC || ty == CODE_DRS || (PCC && ty == CODE_PCC)) ? v : make_float2(0.f, 0.f);
-        return cscale(v, P.scale_df);
+        return v;  // wrow carries scale_df (one multiply per W entry instead of two per bin)
     }
     // STF bin n (stf.cpp:185-285 values, STF scaling)
     __device__ float2 bin_stf(uint32_t c, uint32_t n) const {
         const uint32_t N = A->N_occ;
         const uint32_t k = n <= N / 2 ? N / 2 + n : n - A->off_lower;
         const float2 v = cmul(wrow[0], A->stf[min(k, N)]);
-        return (c & CODE_MASK) == CODE_STF ? cscale(v, P.scale_stf) : make_float2(0.f, 0.f);
+        const float f = P.scale_df != 0.f ? P.scale_stf / P.scale_df : 0.f;  // wrow carries scale_df
+        return (c & CODE_MASK) == CODE_STF ? cscale(v, f) : make_float2(0.f, 0.f);
     }
 };
 
@@ -526,7 +527,8 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
     uint8_t* pcb = reinterpret_cast<uint8_t*>(T.wrow + 8);
     if (live) {
         T.P = A.pk[T.pkt];
-        if (lane < A.N_TS) T.wrow[lane] = A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS + lane];
+        // the W row pre-scaled by the data-field scaling (tx.cpp:582-594, 864-871)
+        if (lane < A.N_TS) T.wrow[lane] = cscale(A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS + lane], T.P.scale_df);
         if (lane < 32) pcb[lane] = lane < 25 ? static_cast<uint8_t>(A.pcc_d[size_t(T.pkt) * 25 + lane] ^ A.pcc_seq[lane]) : 0u;
     }
     __syncthreads();  // the only workgroup barrier: qtab / wrow visible
