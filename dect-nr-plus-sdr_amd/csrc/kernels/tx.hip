@@ -500,7 +500,10 @@ struct txs_wave {
 };
 
 template <int LR, int MR, int HLR, int MODE, bool Q8>
-__global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_eu(4))) tx_stream_kernel(tx_args A, uint32_t n) {
+#ifndef DNRP_TX_WPE
+#define DNRP_TX_WPE 4  // waves per SIMD (5: 96 VGPRs + 120 B/lane of spills)
+#endif
+__global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_eu(DNRP_TX_WPE))) tx_stream_kernel(tx_args A, uint32_t n) {
     using PD = pp_direct<LR, MR, HLR>;
     static_assert(PD::W == TXS_CARRY + 1, "carry = window - 1");
     static_assert(taps_tx_10_9::L == LR && taps_tx_10_9::M == MR && taps_tx_10_9::HL == HLR, "generated taps");
