@@ -1030,3 +1030,67 @@ extern "C" int dnrp_pcc_decode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* 
     }
     return DNRP_OK;
 }
+
+extern "C" int dnrp_pcc_encode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* plcf_type, const uint32_t* closed_loop,
+                                     const uint32_t* beamforming, const uint8_t* plcf, uint32_t plcf_stride, uint8_t* d,
+                                     uint32_t d_stride, void* stream) {
+    using namespace dnrp::dev;
+    if (!ctx || (n && (!plcf_type || !plcf || !d))) return DNRP_EINVAL;
+    if (n == 0) return DNRP_OK;
+    if (d_stride < 25) return DNRP_EINVAL;
+    (void)hipSetDevice(ctx->cfg.device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rc = fec_tables(ctx);
+    if (rc) return rc;
+    std::vector<std::vector<FecEncCb>> by_idx(kNofCbSizes);
+    std::vector<uint64_t> e_off(n);
+    std::vector<uint32_t> Gs(n, kPccBits);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t t = plcf_type[i];
+        if (t != 1 && t != 2) return DNRP_EINVAL;
+        const uint32_t nb = t == 1 ? kPlcfType1Bits : kPlcfType2Bits, idx = (uint32_t)cb_index(nb + 16);
+        if (plcf_stride < nb / 8) return DNRP_EINVAL;
+        const bool cl = closed_loop && closed_loop[i], bf = beamforming && beamforming[i];
+        FecEncCb cb{};
+        cb.tb_off = (uint64_t)i * plcf_stride, cb.e_off = (uint64_t)i * kPccBits, cb.pkt = i, cb.tbs = nb;
+        cb.rp = 0, cb.rlen = nb + 16, cb.E = kPccBits, cb.start = ctx->fec_start[idx * 4];  // rv 0
+        cb.crc16 = 1, cb.mask = cl ? (bf ? kMaskClBf : kMaskCl) : (bf ? kMaskBf : kMaskNone);
+        by_idx[idx].push_back(cb);
+        e_off[i] = (uint64_t)i * kPccBits;
+    }
+    std::vector<FecEncCb> cbs;
+    std::vector<FecWave> waves;
+    uint64_t cd = 0;
+    for (uint32_t idx = 0; idx < kNofCbSizes; ++idx) {
+        const auto& v = by_idx[idx];
+        const uint32_t K = cb_size(idx);
+        for (size_t c0 = 0; c0 < v.size(); c0 += 64) {
+            FecWave w{};
+            w.data_off = cd, w.K = K, w.n = (uint32_t)std::min<size_t>(64, v.size() - c0);
+            w.valid_off = ctx->fec_valid_off[idx];
+            qpp_params(idx, &w.f1, &w.f2);
+            w.first_cb = (uint32_t)cbs.size();
+            cbs.insert(cbs.end(), v.begin() + c0, v.begin() + c0 + w.n);
+            waves.push_back(w);
+            cd += (uint64_t)(K + 3 * (K + 4)) * 64;
+        }
+    }
+    std::vector<uint8_t> args(n * 12 + 16);
+    std::memcpy(args.data(), e_off.data(), n * 8);
+    std::memcpy(args.data() + n * 8, Gs.data(), n * 4);
+    if (!ctx->fec_cbs.upload(cbs) || !ctx->fec_waves.upload(waves) || !ctx->fec_work16.ensure(cd + 16) ||
+        !ctx->fec_bits.ensure((size_t)n * kPccBits + 16) || !ctx->fec_tbarg.upload(args))
+        return DNRP_ENOMEM;
+    FecEncArgs E{};
+    E.tb = plcf, E.tab = ctx->fec_tab.as<uint32_t>(), E.cbs = ctx->fec_cbs.as<FecEncCb>();
+    E.waves = ctx->fec_waves.as<FecWave>(), E.tbcrc = nullptr;
+    E.cd = ctx->fec_work16.as<uint8_t>(), E.ebits = ctx->fec_bits.as<uint8_t>();
+    if (launch_fec_encode(E, (uint32_t)waves.size(), s)) return DNRP_EDEVICE;
+    FecPackArgs P{};
+    P.ebits = E.ebits, P.e_off = ctx->fec_tbarg.as<uint64_t>();
+    P.G = reinterpret_cast<const uint32_t*>(ctx->fec_tbarg.as<uint8_t>() + n * 8), P.d = d, P.d_stride = d_stride;
+    P.n = n, P.max_bytes = (kPccBits + 7) / 8;
+    if (launch_fec_pack(P, s)) return DNRP_EDEVICE;
+    HIPCHK(hipStreamSynchronize(s));
+    return DNRP_OK;
+}

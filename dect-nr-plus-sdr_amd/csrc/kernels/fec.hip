@@ -377,14 +377,26 @@ __global__ void __launch_bounds__(64) fec_encode_kernel(FecEncArgs A) {
     uint8_t* d1 = d0 + (size_t)D * 64;
     uint8_t* d2 = d1 + (size_t)D * 64;
     const uint8_t* tb = A.tb + cb.tb_off;
-    const uint32_t tcrc = A.tbcrc[cb.pkt];
+    uint32_t tcrc;
+    if (cb.crc16) {  // PLCF CRC16 over its 40 / 80 bits, masked (closed loop / beamforming)
+        uint32_t r16 = 0;
+        for (uint32_t pos = 0; pos < cb.tbs; ++pos) {
+            const uint32_t top = (r16 >> 15) & 1u;
+            r16 = (r16 << 1) & 0xFFFFu;
+            if (top ^ ((tb[pos >> 3] >> (7 - (pos & 7))) & 1u)) r16 ^= 0x1021u;
+        }
+        tcrc = r16 ^ cb.mask;
+    } else {
+        tcrc = A.tbcrc[cb.pkt];
+    }
+    const uint32_t tcrc_top = cb.crc16 ? 15u : 23u;
     // c = b[rp, rp + rlen) (+ CRC24B), encoder 1 on the fly
     uint32_t reg = 0, s1 = 0, s2 = 0, s3 = 0;
     for (uint32_t k = 0; k < K; ++k) {
         uint32_t bit;
         if (k < cb.rlen) {
             const uint32_t pos = cb.rp + k;
-            bit = pos < cb.tbs ? (tb[pos >> 3] >> (7 - (pos & 7))) & 1u : (tcrc >> (23 - (pos - cb.tbs))) & 1u;
+            bit = pos < cb.tbs ? (tb[pos >> 3] >> (7 - (pos & 7))) & 1u : (tcrc >> (tcrc_top - (pos - cb.tbs))) & 1u;
             const uint32_t top = (reg >> 23) & 1u;
             reg = (reg << 1) & 0xFFFFFF;
             if (top ^ bit) reg ^= 0x800063;

@@ -86,6 +86,8 @@ struct FecEncCb {        // one code block of dnrp_pdc_encode_batch
     uint32_t rlen;       // bits taken (K - 24 with a CRC24B, K otherwise)
     uint32_t E, start;   // rate-matched bits, circular-buffer list start of the redundancy version
     uint32_t crc24b;     // 1: append a code-block CRC
+    uint32_t crc16;      // 1: PLCF: b = a || CRC16 ^ mask computed here (pcc_enc.cpp:166-183)
+    uint32_t mask;       // PLCF CRC mask
 };
 
 struct FecEncArgs {

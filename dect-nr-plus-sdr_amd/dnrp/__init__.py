@@ -170,7 +170,8 @@ EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_g
            "dnrp_rx_packet_json", "dnrp_crc", "dnrp_fec_cbsegm", "dnrp_fec_cb_size", "dnrp_pcc_encode",
            "dnrp_pcc_decode", "dnrp_pdc_encode", "dnrp_pdc_decode", "dnrp_harq_rx_create", "dnrp_harq_rx_reset",
            "dnrp_harq_rx_destroy", "dnrp_pdc_decode_batch", "dnrp_pdc_encode_batch",
-           "dnrp_pcc_decode_batch", "dnrp_pdc_decode_batch_harq", "dnrp_pdc_softbuffer_size"]
+           "dnrp_pcc_decode_batch", "dnrp_pdc_decode_batch_harq", "dnrp_pdc_softbuffer_size",
+           "dnrp_pcc_encode_batch"]
 
 _lib = None
 

@@ -58,6 +58,7 @@ def lib():
         L.dnrp_pcc_decode_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P, P, P]
         L.dnrp_pdc_decode_batch_harq.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint64, P, C.c_uint32, P,
                                                  C.c_uint32, P, P, P]
+        L.dnrp_pcc_encode_batch.argtypes = [P, C.c_uint32, P, P, P, P, C.c_uint32, P, C.c_uint32, P]
         L.dnrp_pdc_softbuffer_size.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
         _ready = True
     return L
@@ -229,3 +230,20 @@ def pdc_decode_batch_harq(phy, cfgs, llr, softbuf, cb_crc, tb, stream=None):
                                           tb.shape[1], _ptr(ok), _ptr(it), _stream_ptr(stream)),
          "dnrp_pdc_decode_batch_harq")
     return ok.astype(bool), it
+
+
+def pcc_encode_batch(phy, plcf_types, plcf, d, closed_loop=None, beamforming=None, stream=None):
+    """GPU PLCF encoding: plcf uint8 device tensor [n][>= 5 / 10] -> d uint8 device tensor [n][>= 25]
+    (unscrambled PCC d-bits, dnrp_tx_batch's pcc_d rows)."""
+    import torch
+    from . import _stream_ptr
+    n = len(plcf_types)
+    assert plcf.dtype == torch.uint8 and plcf.dim() == 2 and plcf.is_contiguous() and plcf.shape[0] >= n and plcf.is_cuda
+    assert d.dtype == torch.uint8 and d.dim() == 2 and d.is_contiguous() and d.shape[0] >= n and d.is_cuda
+    assert d.shape[1] >= 25 and plcf.shape[1] >= 5 * max(plcf_types, default=1)
+    t = np.ascontiguousarray(plcf_types, dtype=np.uint32)
+    cl = None if closed_loop is None else np.ascontiguousarray(closed_loop, dtype=np.uint32)
+    bf = None if beamforming is None else np.ascontiguousarray(beamforming, dtype=np.uint32)
+    _chk(lib().dnrp_pcc_encode_batch(phy._ctx, n, _ptr(t), None if cl is None else _ptr(cl),
+                                     None if bf is None else _ptr(bf), C.c_void_p(plcf.data_ptr()), plcf.shape[1],
+                                     C.c_void_p(d.data_ptr()), d.shape[1], _stream_ptr(stream)), "dnrp_pcc_encode_batch")

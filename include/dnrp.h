@@ -462,6 +462,15 @@ int dnrp_pdc_encode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, co
 int dnrp_pcc_decode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* plcf_type_test, const int16_t* llr,
                           uint32_t llr_stride, uint8_t* plcf, uint32_t plcf_stride, uint8_t* result, uint32_t* iterations,
                           void* stream);
+/* Device PLCF encoding of n packets <- fec_t::encode_plcf for many packets at once (without the
+ * scrambling): bit-exact with dnrp_pcc_encode.
+ *   plcf_type host [n] (1 / 2); closed_loop, beamforming host [n] (optional, CRC mask selection)
+ *   plcf      device, row i at plcf + i*plcf_stride (5 or 10 bytes)
+ *   d         device, row i at d + i*d_stride (>= 25): dnrp_tx_batch's pcc_d rows
+ * Blocking: returns after the work on the stream has completed. */
+int dnrp_pcc_encode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* plcf_type, const uint32_t* closed_loop,
+                          const uint32_t* beamforming, const uint8_t* plcf, uint32_t plcf_stride, uint8_t* d,
+                          uint32_t d_stride, void* stream);
 int dnrp_harq_rx_create(uint32_t N_TB_bits_max, uint32_t Z, dnrp_harq_rx** out);
 int dnrp_harq_rx_reset(dnrp_harq_rx* hb);
 int dnrp_harq_rx_destroy(dnrp_harq_rx* hb);

@@ -274,3 +274,23 @@ def test_gpu_harq_combining_matches_host():
         if n_ok_first is None:
             n_ok_first = int(ok.sum())
     assert n_ok_first < m and int(ok.sum()) > n_ok_first
+
+
+def test_gpu_plcf_encoder_matches_host():
+    """dnrp_pcc_encode_batch against dnrp_pcc_encode: both PLCF types, all four CRC masks."""
+    import dnrp
+    import dnrp.fec as FE
+    phy = dnrp.Phy(1, 1, 1, max_batch=1)
+    rng = np.random.default_rng(31)
+    n = 70
+    types = [1 + (i % 3 == 0) for i in range(n)]
+    cl = [(i // 2) % 2 for i in range(n)]
+    bf = [(i // 5) % 2 for i in range(n)]
+    plcf = rng.integers(0, 256, (n, 10), dtype=np.uint8)
+    dev = torch.device("cuda:0")
+    d = torch.full((n, 27), 0x5A, dtype=torch.uint8, device=dev)
+    FE.pcc_encode_batch(phy, types, torch.from_numpy(plcf).to(dev), d, cl, bf)
+    g = d.cpu().numpy()
+    for i in range(n):
+        ref = FE.pcc_encode(plcf[i, : 5 * types[i]], types[i], cl[i], bf[i])
+        assert (g[i, :25] == ref).all(), i
