@@ -391,12 +391,13 @@ __global__ void __launch_bounds__(64) fec_encode_kernel(FecEncArgs A) {
     }
     const uint32_t tcrc_top = cb.crc16 ? 15u : 23u;
     // c = b[rp, rp + rlen) (+ CRC24B), encoder 1 on the fly
-    uint32_t reg = 0, s1 = 0, s2 = 0, s3 = 0;
+    uint32_t reg = 0, s1 = 0, s2 = 0, s3 = 0, byte = 0;
     for (uint32_t k = 0; k < K; ++k) {
         uint32_t bit;
         if (k < cb.rlen) {
             const uint32_t pos = cb.rp + k;
-            bit = pos < cb.tbs ? (tb[pos >> 3] >> (7 - (pos & 7))) & 1u : (tcrc >> (tcrc_top - (pos - cb.tbs))) & 1u;
+            if ((k == 0 || (pos & 7) == 0) && pos < cb.tbs) byte = tb[pos >> 3];  // one load per byte
+            bit = pos < cb.tbs ? (byte >> (7 - (pos & 7))) & 1u : (tcrc >> (tcrc_top - (pos - cb.tbs))) & 1u;
             const uint32_t top = (reg >> 23) & 1u;
             reg = (reg << 1) & 0xFFFFFF;
             if (top ^ bit) reg ^= 0x800063;
