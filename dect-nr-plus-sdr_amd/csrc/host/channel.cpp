@@ -180,6 +180,7 @@ int dnrp_channel_batch(dnrp_ctx* ctx, const dnrp_channel_cfg* cfg, uint32_t n, u
     for (uint32_t w = 0; w < n; ++w)
         realise(*cfg, w, N_TX, N_RX, pdp, coef + size_t(w) * nl, taps + size_t(w) * nl * nt,
                 sins + size_t(w) * nl * nt * N_SIN);
+    HIPCHK(ctx->chan_tab.wait_idle(st));
     HIPCHK(hipMemcpyAsync(ctx->chan_tab.p, h, bytes, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ctx->st_chan.ev, st));
     char* d = static_cast<char*>(ctx->chan_tab.p);
@@ -201,7 +202,8 @@ int dnrp_channel_batch(dnrp_ctx* ctx, const dnrp_channel_cfg* cfg, uint32_t n, u
     a.large_scale = cfg->large_scale;
     a.sigma = noise_sigma(*cfg);
     a.seed = mix64(cfg->seed ^ 0x6E6F697365ull);  // "noise": independent of the link draws
-    return dev::launch_channel(a, n, st) == hipSuccess ? DNRP_OK : DNRP_EDEVICE;
+    if (dev::launch_channel(a, n, st) != hipSuccess) return DNRP_EDEVICE;
+    return ctx->chan_tab.mark_busy(st) == hipSuccess ? DNRP_OK : DNRP_EDEVICE;
 }
 
 }  // extern "C"

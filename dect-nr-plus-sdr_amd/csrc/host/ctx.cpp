@@ -106,21 +106,14 @@ double phasor_arg(double rad) {  // mixer_t::set_phase* builds float phasors (mi
 }
 
 void fill_pairs(uint32_t N_TS, uint32_t* pair, uint32_t& mod) {  // transmit_diversity_precoding.cpp:48-75
-    static const uint32_t P4[6][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {0, 3}, {1, 2}};
-    static const uint32_t P8[12][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 4}, {1, 5},
-                                       {2, 6}, {3, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}};
     std::memset(pair, 0, 12 * sizeof(uint32_t));
-    if (N_TS <= 1) {
-        mod = 1;
-    } else if (N_TS == 2) {
-        mod = 1;
-        pair[0] = 0 | (1u << 4);
-    } else if (N_TS == 4) {
-        mod = 6;
-        for (int i = 0; i < 6; ++i) pair[i] = P4[i][0] | (P4[i][1] << 4);
-    } else {
-        mod = 12;
-        for (int i = 0; i < 12; ++i) pair[i] = P8[i][0] | (P8[i][1] << 4);
+    mod = 1;
+    if (N_TS <= 1) return;
+    mod = geo::txdiv_modulo(N_TS);
+    for (uint32_t i = 0; i < mod; ++i) {
+        uint32_t A, B;
+        geo::txdiv_pair(N_TS, i, A, B);
+        pair[i] = A | (B << 4);
     }
 }
 
@@ -173,6 +166,7 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         float s = 1.0f;
         for (const auto& w : geo::W_matrix(t->tm.N_TS, t->tm.N_TX, cb, &s)) W.push_back(make_float2(w.real(), w.imag()));
         t->wscale.push_back(s);
+        t->wscale_opt.push_back(geo::W_scaling_optimal_DAC(t->tm.N_TS, t->tm.N_TX, cb));
     }
     t->pdc_off_h = m.pdc_sym_off;
     // transmit diversity TS pair (A | B << 4) per PCC/PDC cell into the code words (kernels.hpp CODE_*)
@@ -291,7 +285,8 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
             ok = t->lut_pw[mode][p].upload(L.pilot_weight) && t->lut_w[mode][p].upload(L.weights);
             t->lut_n[mode][p] = L.n;
             t->lut_nw[mode][p] = static_cast<uint32_t>(L.weights.size());
-            t->wcap[mode] = std::max(t->wcap[mode], t->lut_nw[mode][p]);
+            // 16-B slots: the segment table behind both weight tables stays 16-B aligned in LDS
+            t->wcap[mode] = std::max(t->wcap[mode], (t->lut_nw[mode][p] + 3u) & ~3u);
             ok = ok && L.n < (1u << 15);  // eq_work packs the tap count into 15 bits
             t->lut_T[mode] = L.T;
         }
@@ -586,13 +581,13 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
         const auto& d = desc[i];
         if ((d.plcf_type != 1 && d.plcf_type != 2) || d.GI_percentage > 100) return DNRP_EINVAL;
         if (d.codebook_index >= t->wscale.size()) return DNRP_EINVAL;
-        if (d.optimal_scaling_DAC) return DNRP_EUNSUPPORTED;
         auto it = ctx->netid.find(d.network_id);
         if (it == ctx->netid.end()) return DNRP_ENETID;
         if ((err = ensure_seq(ctx, *it->second, d.network_id, t->q.G)) != DNRP_OK) return err;
         pk[i].pdc_seq = (d.plcf_type == 1 ? it->second->t1 : it->second->t2).as<uint8_t>();
         pk[i].codebook = d.codebook_index;
-        const float sc = d.DAC_scale * t->wscale[d.codebook_index];  // tx.cpp:582-594
+        // tx.cpp:582-594: standard W scaling, or the dynamic-range optimised one
+        const float sc = d.DAC_scale * (d.optimal_scaling_DAC ? t->wscale_opt[d.codebook_index] : t->wscale[d.codebook_index]);
         pk[i].scale_stf = 1.0f / std::sqrt(static_cast<float>(t->q.N_b_OCC / 4)) * sc;
         pk[i].scale_df = 1.0f / std::sqrt(static_cast<float>(t->q.N_b_OCC)) * sc;
         pk[i].ph0 = phasor_arg(d.iq_phase_rad);
@@ -601,6 +596,7 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (!ctx->tx_pk.ensure(sizeof(dev::tx_pkt) * ctx->cfg.max_batch)) return DNRP_ENOMEM;
+    HIPCHK(ctx->tx_pk.wait_idle(st));
     HIPCHK(hipMemcpyAsync(ctx->tx_pk.p, pk, sizeof(dev::tx_pkt) * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ctx->st_tx.ev, st));
     dev::tx_args a{};
@@ -710,11 +706,12 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     ctx->tic("tx", st);
     if (dev::launch_tx(a, n, st) != hipSuccess) return DNRP_EDEVICE;
     ctx->toc("tx", st);
+    HIPCHK(ctx->tx_pk.mark_busy(st));
     return DNRP_OK;
 }
 
-int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, const float* iq_in, uint32_t S_in,
-                      int16_t* pcc_llr, dnrp_pcc_report* rep, void* stream) {
+int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, const float* iq_in, uint32_t n_windows,
+                      uint32_t S_in, int16_t* pcc_llr, dnrp_pcc_report* rep, void* stream) {
     if (!ctx || (n > 0 && (!sr || !iq_in || !pcc_llr))) return DNRP_EINVAL;
     ctx->rx_valid = false;
     if (n == 0) return DNRP_OK;
@@ -726,6 +723,7 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
     for (uint32_t i = 0; i < n; ++i) {
         if (sr[i].fine_peak_time >= static_cast<int64_t>(S_in) || sr[i].fine_peak_time <= -static_cast<int64_t>(S_in))
             return DNRP_EINVAL;
+        if (sr[i].window >= n_windows) return DNRP_EINVAL;  // the kernels read iq_in + window * N_RX * S_in
         groups[std::make_tuple(sr[i].u, sr[i].b, sr[i].N_eff_TX)].push_back(i);
     }
     int err = DNRP_OK;
@@ -755,6 +753,8 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
     ctx->rx_Nf_pad = nf_max;
     ctx->rx_S_in = S_in;
     ctx->rx_n = n;
+    ctx->rx_iq = iq_in;
+    ctx->rx_n_windows = n_windows;
     const size_t ybytes = size_t(n) * ctx->cfg.N_TX_max * (ctx->rx_nsym_cap + 1) * ctx->rx_Nf_pad * sizeof(float2);
     if (!ctx->Y.ensure(ybytes) || !ctx->rx_in.ensure(sizeof(dev::rx_pkt_in) * ctx->cfg.max_batch) ||
         !ctx->rx_st.ensure(sizeof(dev::rx_pkt_state) * ctx->cfg.max_batch) ||
@@ -818,11 +818,13 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
     return DNRP_OK;
 }
 
-int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const float* iq_in, uint32_t S_in,
-                      int16_t* pdc_llr, uint32_t llr_stride, dnrp_pdc_report* rep, void* stream) {
+int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const float* iq_in, uint32_t n_windows,
+                      uint32_t S_in, int16_t* pdc_llr, uint32_t llr_stride, dnrp_pdc_report* rep, void* stream) {
     if (!ctx || (m > 0 && (!req || !iq_in || !pdc_llr))) return DNRP_EINVAL;
     if (!ctx->rx_valid) return DNRP_ESTATE;
     if (m == 0) return DNRP_OK;
+    // the PDC symbols are read from the PCC call's windows (the state it kept points into them)
+    if (iq_in != ctx->rx_iq || n_windows != ctx->rx_n_windows) return DNRP_ESTATE;
     if (m > ctx->rx_n || S_in != ctx->rx_S_in) return DNRP_EINVAL;
     (void)hipSetDevice(ctx->cfg.device);
     int err = DNRP_OK;

@@ -29,11 +29,24 @@ namespace dnrp::host {
 struct dbuf {
     void* p = nullptr;
     size_t n = 0;
+    hipEvent_t busy = nullptr;  // per-call argument buffers: recorded after the last kernel reading it
     dbuf() = default;
     dbuf(const dbuf&) = delete;
     dbuf& operator=(const dbuf&) = delete;
     ~dbuf() {
         if (p) (void)hipFree(p);
+        if (busy) (void)hipEventDestroy(busy);
+    }
+    // before refilling a per-call argument buffer on stream st: the kernels of an earlier call
+    // (possibly on another stream) that read it must have finished
+    hipError_t wait_idle(hipStream_t st) {
+        if (!busy) return hipEventCreateWithFlags(&busy, hipEventDisableTiming);
+        return hipStreamWaitEvent(st, busy, 0);
+    }
+    // after the launches reading it on stream st
+    hipError_t mark_busy(hipStream_t st) {
+        if (!busy && hipEventCreateWithFlags(&busy, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
+        return hipEventRecord(busy, st);
     }
     bool ensure(size_t bytes) {
         if (bytes <= n) return true;
@@ -94,7 +107,7 @@ struct tx_tables {
     dbuf code_bin;  // [N_DF+1][1024] code per FFT bin (streaming TX kernel, N_b_DFT_os = 1024)
     uint32_t pcc_syms = 0;  // bit l: symbol l carries PCC cells
     uint32_t npp = 0;  // floats in taps_pp
-    std::vector<float> wscale;  // per codebook
+    std::vector<float> wscale, wscale_opt;  // per codebook: standard / optimal_scaling_DAC
     std::vector<uint32_t> pdc_off_h;  // host copy of maps.pdc_sym_off
 };
 
@@ -176,7 +189,8 @@ struct dnrp_ctx {
     // retained RX phase-1 state: per PCC-batch slot its (u, b, N_eff_TX) tables and symbol
     // capacity; Y is laid out with the batch-wide maxima rx_nsym_cap / rx_Nf_pad
     bool rx_valid = false;
-    uint32_t rx_n = 0, rx_S_in = 0, rx_nsym_cap = 0, rx_Nf_pad = 0;
+    uint32_t rx_n = 0, rx_S_in = 0, rx_nsym_cap = 0, rx_Nf_pad = 0, rx_n_windows = 0;
+    const float* rx_iq = nullptr;  // the PCC call's windows: the PDC call must read the same ones
     std::vector<rx1_tables*> rx_slot_t;
     std::vector<uint32_t> rx_slot_cap;
     dbuf rx_sel, rx_sel2;  // [max_batch][2] launch packet -> slot / output row (PCC / PDC call), one slice per group

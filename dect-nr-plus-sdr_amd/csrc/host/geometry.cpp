@@ -253,6 +253,8 @@ std::vector<cf32> stf_values(uint32_t b, uint32_t N_eff_TX) {  // stf.cpp:171-18
     return v;
 }
 
+float drs_value(uint32_t t, uint32_t i) { return static_cast<float>(DRS_Y[(4 * i + t % 4) % 56] * (t < 4 ? 1 : -1)); }
+
 maps_t build_maps(uint32_t b, uint32_t N_TS, uint32_t N_eff_TX, uint32_t N_DF) {
     maps_t m;
     const uint32_t Nb = 64 * b, N = 56 * b, Nf = N + 1, gb = 4 * b;
@@ -275,7 +277,7 @@ maps_t build_maps(uint32_t b, uint32_t N_TS, uint32_t N_eff_TX, uint32_t N_DF) {
                     static_cast<uint32_t>(kocc(N, 4 * i + (t + 2 * par) % 4) + static_cast<int>(N / 2));
     for (uint32_t t = 0; t < 8; ++t)
         for (uint32_t i = 0; i < N / 4; ++i)
-            m.drs_v[t * (N / 4) + i] = static_cast<float>(DRS_Y[(4 * i + t % 4) % 56] * (t < 4 ? 1 : -1));
+            m.drs_v[t * (N / 4) + i] = drs_value(t, i);
     m.drs = drs_schedule(N_TS, N_DF);
     for (const auto& d : m.drs)
         for (uint32_t t = d.ts_first; t <= d.ts_last; ++t)
@@ -383,6 +385,26 @@ std::vector<cf32> W_matrix(uint32_t N_TS, uint32_t N_TX, uint32_t cb, float* sca
     }
     if (scaling) *scaling = 1.0f / std::sqrt(nz);  // beamforming_and_antenna_port_mapping.cpp:307-320
     return w;
+}
+
+float W_scaling_optimal_DAC(uint32_t N_TS, uint32_t N_TX, uint32_t cb) {
+    (void)Wtab(N_TS, N_TX).at(cb);  // throws for an undefined matrix
+    const float r2 = 1.0f / std::sqrt(2.0f), r4 = 1.0f / std::sqrt(4.0f);
+    if (N_TS == 2 && N_TX == 2) return cb == 0 ? 1.0f : r2;   // {1, 1/sqrt2, 1/sqrt2}
+    if (N_TS == 2 && N_TX == 4) return cb < 14 ? 1.0f : r2;   // 14 x 1, 8 x 1/sqrt2
+    if (N_TS == 4 && N_TX == 4) return cb == 0 ? 1.0f : cb < 3 ? r2 : r4;  // {1, r2, r2, r4, r4}
+    return 1.0f;  // SISO, N_TS = 1 (N_TX 2 / 4), N_TS = 8
+}
+
+uint32_t txdiv_modulo(uint32_t N_TS) { return N_TS <= 2 ? 1u : N_TS == 4 ? 6u : 12u; }
+
+void txdiv_pair(uint32_t N_TS, uint32_t i, uint32_t& A, uint32_t& B) {
+    static const uint8_t P4[6][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {0, 3}, {1, 2}};
+    static const uint8_t P8[12][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 4}, {1, 5},
+                                      {2, 6}, {3, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}};
+    i %= txdiv_modulo(N_TS);
+    A = N_TS <= 2 ? 0u : N_TS == 4 ? P4[i][0] : P8[i][0];
+    B = N_TS <= 2 ? 1u : N_TS == 4 ? P4[i][1] : P8[i][1];
 }
 
 // ------------------------------------------------------------ Gold sequence (TS 36.211 §7.2)

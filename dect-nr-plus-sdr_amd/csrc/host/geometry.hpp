@@ -64,6 +64,15 @@ std::vector<cf32> stf_values(uint32_t b, uint32_t N_eff_TX);
 
 std::vector<cf32> W_matrix(uint32_t N_TS, uint32_t N_TX, uint32_t codebook, float* scaling);
 uint32_t W_codebooks(uint32_t N_TS, uint32_t N_TX);
+// W_t::scaling_factor_optimal_DAC (beamforming_and_antenna_port_mapping.cpp:146-186): the scaling
+// tx_meta_t::optimal_scaling_DAC selects instead of 1/sqrt(non-zero entries) (tx.cpp:582-592)
+float W_scaling_optimal_DAC(uint32_t N_TS, uint32_t N_TX, uint32_t codebook);
+// Y_i_t::index_N_TS_x (transmit_diversity_precoding.cpp:48-75): transmit-stream pair i of the SFBC
+// cycle and the cycle length (get_modulo: 1 / 6 / 12 for N_TS = 2 / 4 / 8)
+uint32_t txdiv_modulo(uint32_t N_TS);
+void txdiv_pair(uint32_t N_TS, uint32_t i, uint32_t& A, uint32_t& B);
+// DRS value of transmit stream t at DRS cell i (drs.cpp:227-254): +-y_b_1[(4 i + t % 4) % 56]
+float drs_value(uint32_t t, uint32_t i);
 
 std::vector<uint8_t> gold_bits_packed(uint32_t c_init, uint32_t nbits);  // MSB-first bytes
 

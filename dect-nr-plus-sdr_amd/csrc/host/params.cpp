@@ -9,6 +9,7 @@
 
 #include "../params.hpp"
 #include "dnrp.h"
+#include "geometry.hpp"
 
 namespace {
 
@@ -154,6 +155,65 @@ int dnrp_get_radio_device_class(const char* name, dnrp_radio_device_class* out) 
             return DNRP_OK;
         }
     return DNRP_ECONFIG;  // the reference asserts on an unknown class string
+}
+
+int dnrp_query_table(const char* name, const uint32_t* arg, uint32_t n_arg, float* out, uint32_t cap) {
+    using namespace dnrp;
+    if (!name || (n_arg && !arg)) return DNRP_EINVAL;
+    std::vector<float> v;
+    const std::string n(name);
+    auto a = [&](uint32_t i) { return i < n_arg ? arg[i] : 0u; };
+    try {
+        if (n == "W" || n == "W_scaling" || n == "W_scaling_optimal_DAC") {  // (N_TS, N_TX, codebook)
+            if (n_arg != 3) return DNRP_EINVAL;
+            if (a(2) >= geo::W_codebooks(a(0), a(1))) return DNRP_EINVAL;
+            float sc = 1.0f;
+            const auto w = geo::W_matrix(a(0), a(1), a(2), &sc);
+            if (n == "W") {
+                for (const auto& c : w) {
+                    v.push_back(c.real());
+                    v.push_back(c.imag());
+                }
+            } else {
+                v.push_back(n == "W_scaling" ? sc : geo::W_scaling_optimal_DAC(a(0), a(1), a(2)));
+            }
+        } else if (n == "W_codebooks") {  // (N_TS, N_TX)
+            if (n_arg != 2) return DNRP_EINVAL;
+            v.push_back(static_cast<float>(geo::W_codebooks(a(0), a(1))));
+        } else if (n == "stf") {  // (b, N_eff_TX): transmit-stream vector [N_b_OCC + 1] re/im, scale 1
+            if (n_arg != 2 || !(a(0) == 1 || a(0) == 2 || a(0) == 4 || a(0) == 8 || a(0) == 12 || a(0) == 16) ||
+                !(a(1) == 1 || a(1) == 2 || a(1) == 4 || a(1) == 8))
+                return DNRP_EINVAL;
+            for (const auto& c : geo::stf_values(a(0), a(1))) {
+                v.push_back(c.real());
+                v.push_back(c.imag());
+            }
+        } else if (n == "drs_values") {  // (b, t): the N_b_OCC/4 DRS values of transmit stream t
+            if (n_arg != 2 || a(0) == 0 || a(0) > 16 || a(1) > 7) return DNRP_EINVAL;
+            const auto m = geo::build_maps(a(0), 1, 1, 1);
+            const uint32_t nd = static_cast<uint32_t>(m.drs_v.size() / 8);
+            v.assign(m.drs_v.begin() + size_t(a(1)) * nd, m.drs_v.begin() + size_t(a(1) + 1) * nd);
+        } else if (n == "txdiv_pairs") {  // (N_TS): the SFBC stream pairs of one cycle, A0 B0 A1 B1 ...
+            if (n_arg != 1 || !(a(0) == 2 || a(0) == 4 || a(0) == 8)) return DNRP_EINVAL;
+            for (uint32_t i = 0; i < geo::txdiv_modulo(a(0)); ++i) {
+                uint32_t A, B;
+                geo::txdiv_pair(a(0), i, A, B);
+                v.push_back(static_cast<float>(A));
+                v.push_back(static_cast<float>(B));
+            }
+        } else if (n == "stf_cover_sequence") {
+            v.assign(prm::STF_COVER, prm::STF_COVER + 9);
+        } else {
+            return DNRP_EINVAL;
+        }
+    } catch (...) {
+        return DNRP_EINVAL;
+    }
+    if (out) {
+        if (cap < v.size()) return DNRP_EINVAL;
+        std::memcpy(out, v.data(), v.size() * sizeof(float));
+    }
+    return static_cast<int>(v.size());
 }
 
 }  // extern "C"

@@ -27,6 +27,7 @@ int gather(dnrp_ctx* ctx, const float* ring, uint64_t ring_len, uint64_t ant_str
     auto* hs = static_cast<int64_t*>(ctx->st_ring.get(sizeof(int64_t) * n));
     if (!hs || !ctx->ring_start.ensure(sizeof(int64_t) * n)) return DNRP_ENOMEM;
     std::memcpy(hs, start, sizeof(int64_t) * n);
+    HIPCHK(ctx->ring_start.wait_idle(st));
     HIPCHK(hipMemcpyAsync(ctx->ring_start.p, hs, sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ctx->st_ring.ev, st));
     dev::ring_args a{};
@@ -37,7 +38,8 @@ int gather(dnrp_ctx* ctx, const float* ring, uint64_t ring_len, uint64_t ant_str
     a.out = reinterpret_cast<float2*>(out);
     a.n_ant = N_ant;
     a.S_win = S_win;
-    return dev::launch_ring_gather(a, n, st) == hipSuccess ? DNRP_OK : DNRP_EDEVICE;
+    if (dev::launch_ring_gather(a, n, st) != hipSuccess) return DNRP_EDEVICE;
+    return ctx->ring_start.mark_busy(st) == hipSuccess ? DNRP_OK : DNRP_EDEVICE;
 }
 
 }  // namespace

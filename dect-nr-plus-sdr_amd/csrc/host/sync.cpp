@@ -22,7 +22,7 @@ namespace {
 
 using cd = std::complex<double>;
 
-const float COVER[9] = {1, -1, 1, 1, -1, -1, -1, -1, -1};  // stf.hpp:146-151 (cover sequence active)
+const float* const COVER = prm::STF_COVER;  // stf.hpp:146-151 (cover sequence active)
 
 void fft_host(std::vector<cd>& x, int sign) {  // iterative radix-2, unnormalised
     const size_t n = x.size();

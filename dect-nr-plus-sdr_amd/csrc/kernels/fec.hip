@@ -456,14 +456,15 @@ __global__ void __launch_bounds__(64) fec_encode_kernel(FecEncArgs A) {
 }
 
 __global__ void __launch_bounds__(256) fec_pack_kernel(FecPackArgs A) {
-    const uint32_t p = blockIdx.y;
-    const uint32_t G = A.G[p], nb = (G + 7) / 8;
-    const uint8_t* e = A.ebits + A.e_off[p];
-    for (uint32_t B = blockIdx.x * blockDim.x + threadIdx.x; B < nb; B += gridDim.x * blockDim.x) {
-        uint32_t v = 0;
+    for (uint32_t p = blockIdx.y; p < A.n; p += gridDim.y) {  // packets grid-stride: any n
+        const uint32_t G = A.G[p], nb = (G + 7) / 8;
+        const uint8_t* e = A.ebits + A.e_off[p];
+        for (uint32_t B = blockIdx.x * blockDim.x + threadIdx.x; B < nb; B += gridDim.x * blockDim.x) {
+            uint32_t v = 0;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v = (v << 1) | (8 * B + t < G ? e[8 * B + t] : 0u);
-        A.d[(size_t)p * A.d_stride + B] = (uint8_t)v;
+            for (int t = 0; t < 8; ++t) v = (v << 1) | (8 * B + t < G ? e[8 * B + t] : 0u);
+            A.d[(size_t)p * A.d_stride + B] = (uint8_t)v;
+        }
     }
 }
 
@@ -474,7 +475,8 @@ int launch_fec_encode(const FecEncArgs& a, uint32_t n_waves, hipStream_t s) {
 }
 int launch_fec_pack(const FecPackArgs& a, hipStream_t s) {
     if (a.n == 0) return 0;
-    hipLaunchKernelGGL(fec_pack_kernel, dim3((a.max_bytes + 255) / 256 < 256 ? (a.max_bytes + 255) / 256 : 256, a.n), dim3(256), 0, s, a);
+    const uint32_t gx = (a.max_bytes + 255) / 256 < 256 ? (a.max_bytes + 255) / 256 : 256;
+    hipLaunchKernelGGL(fec_pack_kernel, dim3(gx > 0 ? gx : 1, a.n < 65535u ? a.n : 65535u), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

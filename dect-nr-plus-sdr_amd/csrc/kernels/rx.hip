@@ -18,7 +18,7 @@
 
 namespace dnrp::dev {
 
-__constant__ float k_cover_rx[9] = {1, -1, 1, 1, -1, -1, -1, -1, -1};  // stf.hpp:146-151
+__constant__ float k_cover_rx[9] = DNRP_STF_COVER_SEQUENCE;  // stf.hpp:146-151 (params.hpp)
 
 // resample outputs m in [m0, m0+cnt) of one antenna stream into dst and mix with
 // exp(j*(phi_m0 + (m - m0) * inc)). inbuf must hold cnt*M/L + hl + 4 samples; taps in LDS.

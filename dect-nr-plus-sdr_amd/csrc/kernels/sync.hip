@@ -954,10 +954,9 @@ size_t sync_detect_lds(const sync_args& a) {
 constexpr int SYNC_WPG = SYNC_WPG_DEF;  // waves per workgroup of the wave kernel
 
 hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
-    static const int ss_env = [] {
-        const char* e = std::getenv("DNRP_SYNC_STREAM");
-        return e ? std::atoi(e) : 1;
-    }();
+    // DNRP_SYNC_STREAM=0 selects the wave kernel below (read per call: tests switch it at run time)
+    const char* ss_e = std::getenv("DNRP_SYNC_STREAM");
+    const int ss_env = ss_e ? std::atoi(ss_e) : 1;
     if (ss_env && a.L == 9 && a.M == 10 && a.hl == 24 && a.step % 4 == 0 && a.step >= 4 &&
         64u * 9u + a.step + a.pattern + 9u <= SS_RING) {
         // segments of ~32 chunks per (window, antenna): enough waves to fill the chip, little warm-up

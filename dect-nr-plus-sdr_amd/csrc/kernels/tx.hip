@@ -22,7 +22,7 @@
 
 namespace dnrp::dev {
 
-__constant__ float k_cover[9] = {1, -1, 1, 1, -1, -1, -1, -1, -1};  // stf.hpp:146-151
+__constant__ float k_cover[9] = DNRP_STF_COVER_SEQUENCE;  // stf.hpp:146-151 (params.hpp)
 
 constexpr uint32_t TX_THREADS = 256;     // block-FFT path workgroup
 constexpr uint32_t TX_WAVE_MAX = 512;    // wave path: one wavefront per symbol slot, 64 (K + 1) threads
@@ -421,6 +421,7 @@ struct txs_wave {
     tx_pkt P;
     uint32_t pkt, ant, lane;
     float2 *buf, *wrow, *qtab;
+    float2 w0;  // unscaled W[ant][0]: the STF bins carry scale_stf alone (tx.cpp:864-871)
     const uint8_t *dpdc, *cpdc;
     uint32_t pdc_bytes;
 
@@ -493,9 +494,8 @@ struct txs_wave {
     __device__ float2 bin_stf(uint32_t c, uint32_t n) const {
         const uint32_t N = A->N_occ;
         const uint32_t k = n <= N / 2 ? N / 2 + n : n - A->off_lower;
-        const float2 v = cmul(wrow[0], A->stf[min(k, N)]);
-        const float f = P.scale_df != 0.f ? P.scale_stf / P.scale_df : 0.f;  // wrow carries scale_df
-        return (c & CODE_MASK) == CODE_STF ? cscale(v, f) : make_float2(0.f, 0.f);
+        const float2 v = cscale(cmul(w0, A->stf[min(k, N)]), P.scale_stf);
+        return (c & CODE_MASK) == CODE_STF ? v : make_float2(0.f, 0.f);
     }
 };
 
@@ -532,6 +532,7 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
         T.P = A.pk[T.pkt];
         // the W row pre-scaled by the data-field scaling (tx.cpp:582-594, 864-871)
         if (lane < A.N_TS) T.wrow[lane] = cscale(A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS + lane], T.P.scale_df);
+        T.w0 = A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS];
         if (lane < 32) pcb[lane] = lane < 25 ? static_cast<uint8_t>(A.pcc_d[size_t(T.pkt) * 25 + lane] ^ A.pcc_seq[lane]) : 0u;
     }
     __syncthreads();  // the only workgroup barrier: qtab / wrow visible

@@ -17,6 +17,10 @@ namespace dnrp::prm {
 
 // ------------------------------------------------------------------ stf_param.hpp
 constexpr bool STF_COVER_SEQUENCE_ACTIVE = true;
+// stf_t::cover_sequence (stf.hpp:146-151), the SECTIONS_PART_3_STF_COVER_SEQUENCE_ACTIVE branch:
+// +-1 per STF pattern (9 patterns for u >= 2, the first 7 for u = 1)
+#define DNRP_STF_COVER_SEQUENCE {1.0f, -1.0f, 1.0f, 1.0f, -1.0f, -1.0f, -1.0f, -1.0f, -1.0f}
+constexpr float STF_COVER[9] = DNRP_STF_COVER_SEQUENCE;
 
 // ------------------------------------------------------------------ sync_param.hpp
 constexpr uint32_t SYNC_MAX_BUFFERABLE = 10;             // RX_SYNC_PARAM_MAX_NOF_BUFFERABLE_SYNC_BEFORE_ACQUIRING_BATON

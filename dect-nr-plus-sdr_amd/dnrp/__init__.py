@@ -171,7 +171,7 @@ EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_g
            "dnrp_pcc_decode", "dnrp_pdc_encode", "dnrp_pdc_decode", "dnrp_harq_rx_create", "dnrp_harq_rx_reset",
            "dnrp_harq_rx_destroy", "dnrp_pdc_decode_batch", "dnrp_pdc_encode_batch",
            "dnrp_pcc_decode_batch", "dnrp_pdc_decode_batch_harq", "dnrp_pdc_softbuffer_size",
-           "dnrp_pcc_encode_batch"]
+           "dnrp_pcc_encode_batch", "dnrp_query_table"]
 
 _lib = None
 
@@ -192,9 +192,9 @@ def lib():
                                     C.c_uint32, P]
         L.dnrp_rx_sync_batch.argtypes = [P, C.POINTER(SyncCfg), C.c_uint32, P, C.c_uint64, C.c_uint64, C.c_uint32,
                                          P, P, P]
-        L.dnrp_rx_pcc_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, P,
+        L.dnrp_rx_pcc_batch.argtypes = [P, C.c_uint32, P, P, C.c_uint32, C.c_uint32, P,
                                         C.POINTER(PccReport), P]
-        L.dnrp_rx_pdc_batch.argtypes = [P, C.c_uint32, C.POINTER(PdcReq), P, C.c_uint32, P, C.c_uint32,
+        L.dnrp_rx_pdc_batch.argtypes = [P, C.c_uint32, C.POINTER(PdcReq), P, C.c_uint32, C.c_uint32, P, C.c_uint32,
                                         C.POINTER(PdcReport), P]
         L.dnrp_sync.argtypes = [P, P]
         L.dnrp_ring_gather.argtypes = [P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P, C.c_uint32, P, P]
@@ -214,6 +214,7 @@ def lib():
                                           C.POINTER(SyncStreamState), P, C.POINTER(C.c_uint32), P, P]
         L.dnrp_last_kernel_ms.argtypes = [P, C.c_char_p, C.POINTER(C.c_float)]
         L.dnrp_kernel_time_total.argtypes = [P, C.c_char_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.c_int]
+        L.dnrp_query_table.argtypes = [C.c_char_p, P, C.c_uint32, P, C.c_uint32]
         L.dnrp_strerror.argtypes = [C.c_int]
         L.dnrp_strerror.restype = C.c_char_p
         _lib = L
@@ -241,6 +242,20 @@ def compute_packet_sizes(ps, u_max=None, b_max=None, os_min=1, L=10, M=9):
     if rc != 0:
         raise DnrpError(rc, "dnrp_compute_packet_sizes")
     return out.as_dict()
+
+
+def query_table(name, *args):
+    """Host-only: a literal table the library builds its device tables from (dnrp_query_table) as a
+    float32 array."""
+    a = np.ascontiguousarray(np.asarray(args, dtype=np.uint32))
+    ap = C.c_void_p(a.ctypes.data) if len(a) else None
+    n = lib().dnrp_query_table(str(name).encode(), ap, len(a), None, 0)
+    if n < 0:
+        raise DnrpError(n, f"dnrp_query_table({name}, {args})")
+    out = np.zeros(max(1, n), np.float32)
+    _chk(min(0, lib().dnrp_query_table(str(name).encode(), ap, len(a), C.c_void_p(out.ctypes.data), n)),
+         "dnrp_query_table")
+    return out[:n]
 
 
 def channel_realization(cfg, window, n_tx, n_rx):
@@ -419,9 +434,8 @@ class Phy:
         if n and (wins.max() >= iq_in.shape[0] or wins.min() < 0):
             raise ValueError(f"sync report window {int(wins.max())} outside iq_in ({iq_in.shape[0]} windows)")
         rep = (PccReport * n)() if want_report else None
-        _chk(lib().dnrp_rx_pcc_batch(self._ctx, n, arr, C.c_void_p(iq_in.data_ptr()), iq_in.shape[2],
+        _chk(lib().dnrp_rx_pcc_batch(self._ctx, n, arr, C.c_void_p(iq_in.data_ptr()), iq_in.shape[0], iq_in.shape[2],
                                      C.c_void_p(pcc_llr.data_ptr()), rep, _stream_ptr(stream)), "dnrp_rx_pcc_batch")
-        self._pcc_windows = int(wins.max()) + 1 if n else 0
         return rep
 
     def rx_pdc_batch(self, reqs, iq_in, pdc_llr, want_report=False, stream=None):
@@ -430,8 +444,6 @@ class Phy:
         import torch
         m = len(reqs)
         self._check_rx_windows(iq_in)
-        if iq_in.shape[0] < getattr(self, "_pcc_windows", 0):
-            raise ValueError(f"iq_in holds {iq_in.shape[0]} windows, the PCC batch used {self._pcc_windows}")
         _check_tensor(pdc_llr, "pdc_llr", torch.int16, 2, int(self.cfg.device))
         arr = reqs if isinstance(reqs, C.Array) else (PdcReq * m)(*reqs)
         keys = {tuple(getattr(r.psdef, f) for f, _ in PsDef._fields_) for r in arr}
@@ -439,7 +451,7 @@ class Phy:
         if pdc_llr.shape[0] < m or pdc_llr.shape[1] < g_max:
             raise ValueError(f"pdc_llr shape {tuple(pdc_llr.shape)}, expected [>={m}, >={g_max}]")
         rep = (PdcReport * m)() if want_report else None
-        _chk(lib().dnrp_rx_pdc_batch(self._ctx, m, arr, C.c_void_p(iq_in.data_ptr()), iq_in.shape[2],
+        _chk(lib().dnrp_rx_pdc_batch(self._ctx, m, arr, C.c_void_p(iq_in.data_ptr()), iq_in.shape[0], iq_in.shape[2],
                                      C.c_void_p(pdc_llr.data_ptr()), pdc_llr.shape[1], rep, _stream_ptr(stream)),
              "dnrp_rx_pdc_batch")
         return rep

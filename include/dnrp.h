@@ -92,7 +92,7 @@ typedef struct {
     float DAC_scale;
     float iq_phase_rad;
     float iq_phase_increment_s2s_post_resampling_rad;
-    uint32_t optimal_scaling_DAC; /* 0: standard W scaling (tx.cpp:582-592) */
+    uint32_t optimal_scaling_DAC; /* 0: standard W scaling, 1: W_t::scaling_factor_optimal_DAC (tx.cpp:582-592) */
 } dnrp_tx_desc;
 
 /* sync_report_t fields consumed by rx_synced_t (phy/rx/sync/sync_report.hpp) */
@@ -208,32 +208,31 @@ int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32_t n, const
  * demoddecod_rx_pcc calls).
  *   sr       host [n]; packet i lies in window sr[i].window of iq_in at sr[i].fine_peak_time (may
  *            be negative: zero history before the window start)
- *   iq_in    device [windows][N_RX][S_in] cf32, N_RX = cfg.N_TX_max; every sr[i].window must
- *            index a window of it
+ *   iq_in    device [n_windows][N_RX][S_in] cf32, N_RX = cfg.N_TX_max; DNRP_EINVAL if any
+ *            sr[i].window >= n_windows (the kernels read window sr[i].window of iq_in)
  *   pcc_llr  device [n][196] int16, descrambled
  *   rep      host [n] (optional)
  * Device state for phase 2 (STF estimates, PCC-phase channel estimates) is kept in the context
  * until the next dnrp_rx_pcc_batch.
  */
 int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, const float* iq_in,
-                      uint32_t S_in, int16_t* pcc_llr, dnrp_pcc_report* rep, void* stream);
+                      uint32_t n_windows, uint32_t S_in, int16_t* pcc_llr, dnrp_pcc_report* rep, void* stream);
 
 /*
  * RX phase 2: PDC demodulation of any subset of the packets of the preceding dnrp_rx_pcc_batch,
  * each with its own PLCF-announced configuration (mixed MCS / PacketLength / network IDs are
  * grouped internally).
  *   req      host [m], m <= n of the PCC batch, distinct pcc_index values
- *   iq_in    device windows holding the same samples as the PCC call's iq_in ([n][N_RX][S_in]
- *            cf32, same S_in): the PDC symbols are read from here, so the windows must stay valid
- *            and unchanged until this call's work has completed on the stream
+ *   iq_in    the PCC call's iq_in, n_windows and S_in: the PDC symbols are read from these windows,
+ *            so they must stay valid and unchanged until this call's work has completed
  *   pdc_llr  device [m][llr_stride] int16: row r = the G descrambled LLRs of req[r]
  *   rep      host [m] (optional)
- * Returns DNRP_ESTATE without a preceding PCC batch, DNRP_EINVAL for a pcc_index out of range or
- * repeated, a psdef whose u/b/N_eff_TX differ from the slot's sync report, S_in different from
- * the PCC call, or llr_stride < G.
+ * Returns DNRP_ESTATE without a preceding PCC batch or for an iq_in / n_windows other than the
+ * PCC call's, DNRP_EINVAL for a pcc_index out of range or repeated, a psdef whose u/b/N_eff_TX
+ * differ from the slot's sync report, S_in different from the PCC call, or llr_stride < G.
  */
-int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const float* iq_in, uint32_t S_in,
-                      int16_t* pdc_llr, uint32_t llr_stride, dnrp_pdc_report* rep, void* stream);
+int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const float* iq_in, uint32_t n_windows,
+                      uint32_t S_in, int16_t* pdc_llr, uint32_t llr_stride, dnrp_pdc_report* rep, void* stream);
 
 int dnrp_sync(dnrp_ctx* ctx, void* stream);
 
@@ -353,6 +352,18 @@ int dnrp_get_radio_device_class(const char* name, dnrp_radio_device_class* out);
  * Host only: DNRP_EINVAL for an unknown name. dnrp_param_name(i) enumerates them (NULL past the end). */
 int dnrp_query_param(const char* name, double* value);
 const char* dnrp_param_name(uint32_t index);
+/* The literal tables of sections_part3 the library builds its device tables from (host only), for
+ * pinning against the reference's own text (tests/golden/ref_literals.json). Returns the number of
+ * floats (out may be NULL to ask for it; cap = floats available), DNRP_EINVAL for an unknown name or
+ * bad arguments. Names (arguments):
+ *   "W" (N_TS, N_TX, codebook)   W_t matrix [N_TX][N_TS] re/im (Tables 6.3.4-1..6)
+ *   "W_scaling" / "W_scaling_optimal_DAC" (N_TS, N_TX, codebook)   its scaling factor (tx.cpp:582-592)
+ *   "W_codebooks" (N_TS, N_TX)   number of codebook entries
+ *   "stf" (b, N_eff_TX)          stf_t transmit-stream vector [N_b_OCC + 1] re/im, scale 1 (stf.cpp:185-285)
+ *   "drs_values" (b, t)          the N_b_OCC/4 DRS values of transmit stream t (drs.cpp:227-254)
+ *   "txdiv_pairs" (N_TS)         Y_i_t::index_N_TS_x rows A0 B0 A1 B1 ... (transmit_diversity_precoding.cpp:48-75)
+ *   "stf_cover_sequence" ()      stf_t::cover_sequence (stf.hpp:146-151) */
+int dnrp_query_table(const char* name, const uint32_t* arg, uint32_t n_arg, float* out, uint32_t cap);
 
 /* Kernel timing (only when the environment has DNRP_TIMING=1 at dnrp_ctx_create): HIP events
  * recorded on the caller's stream around each launch. Names: "tx", "sync_steps", "sync_detect",

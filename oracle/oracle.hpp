@@ -90,6 +90,8 @@ void txdiv_pair(uint32_t N_TS, uint32_t i_mod, uint32_t& A, uint32_t& B);
 // Beamforming matrices (beamforming_and_antenna_port_mapping.cpp:27-320): row-major [N_TX][N_TS]
 std::vector<cd> W_matrix(uint32_t N_TS, uint32_t N_TX, uint32_t codebook);
 double W_scaling(uint32_t N_TS, uint32_t N_TX, uint32_t codebook);
+double W_scaling_optimal_DAC(uint32_t N_TS, uint32_t N_TX, uint32_t codebook);  // beamforming_...mapping.cpp:146-186
+extern const float STF_COVER_SEQ[9];  // stf.hpp:146-151 (cover sequence active)
 uint32_t W_codebook_max(uint32_t N_TS, uint32_t N_TX);
 
 // LTE Gold sequence (3GPP TS 36.211 §7.2), bits 0/1

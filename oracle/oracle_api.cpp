@@ -246,7 +246,41 @@ int oracle_chest_lut(uint32_t Nsv, uint32_t b, uint32_t b_max, uint32_t u_max, u
     }
 }
 
-// desc_u: codebook, network_id, plcf_type, GI_percentage ; desc_f: DAC_scale, phase, phase_inc
+// literal tables (pinned against tests/golden/ref_literals.json)
+int oracle_W(uint32_t N_TS, uint32_t N_TX, uint32_t codebook, double* out_re_im, double* scaling) {
+    try {
+        const auto w = W_matrix(N_TS, N_TX, codebook);
+        for (size_t i = 0; i < w.size(); ++i) {
+            out_re_im[2 * i] = w[i].real();
+            out_re_im[2 * i + 1] = w[i].imag();
+        }
+        scaling[0] = W_scaling(N_TS, N_TX, codebook);
+        scaling[1] = W_scaling_optimal_DAC(N_TS, N_TX, codebook);
+        return static_cast<int>(w.size());
+    } catch (...) {
+        return -1;
+    }
+}
+int oracle_W_codebooks(uint32_t N_TS, uint32_t N_TX) {
+    try {
+        return static_cast<int>(W_codebook_max(N_TS, N_TX)) + 1;
+    } catch (...) {
+        return -1;
+    }
+}
+int oracle_drs_values(uint32_t b, uint32_t t, double* out) {
+    const auto v = drs_y(b, t);
+    std::memcpy(out, v.data(), v.size() * sizeof(double));
+    return static_cast<int>(v.size());
+}
+int oracle_txdiv_pairs(uint32_t N_TS, uint32_t* out) {
+    const uint32_t m = txdiv_modulo(N_TS);
+    for (uint32_t i = 0; i < m; ++i) txdiv_pair(N_TS, i, out[2 * i], out[2 * i + 1]);
+    return static_cast<int>(m);
+}
+void oracle_cover_sequence(float* out9) { std::memcpy(out9, STF_COVER_SEQ, 9 * sizeof(float)); }
+
+// desc_u: codebook, network_id, plcf_type, GI_percentage, optimal_scaling_DAC ; desc_f: DAC_scale, phase, phase_inc
 int oracle_tx(const uint32_t* cfg, const uint32_t* psdef, const uint32_t* desc_u, const double* desc_f,
               const uint8_t* pcc_d, const uint8_t* pdc_d, float* out, uint32_t S_slot, int use_float) {
     try {
@@ -257,6 +291,7 @@ int oracle_tx(const uint32_t* cfg, const uint32_t* psdef, const uint32_t* desc_u
         d.network_id = desc_u[1];
         d.plcf_type = desc_u[2];
         d.GI_percentage = desc_u[3];
+        d.optimal_scaling_DAC = desc_u[4] != 0;
         d.DAC_scale = static_cast<float>(desc_f[0]);
         d.iq_phase_rad = desc_f[1];
         d.iq_phase_increment_rad = desc_f[2];

@@ -105,7 +105,7 @@ uint32_t dims_t::transmit_len(uint32_t gi_percentage) const {
     return N_no_GI_os_rs + (N_packet_os_rs - N_no_GI_os_rs) * gi_percentage / 100;
 }
 
-static const float COVER[9] = {1, -1, 1, 1, -1, -1, -1, -1, -1};  // stf.hpp:146-151
+static const float* const COVER = STF_COVER_SEQ;  // stf.hpp:146-151
 
 static std::vector<uint8_t> unpack_bits(const uint8_t* d, uint32_t nbits) {
     std::vector<uint8_t> b(nbits);
@@ -183,10 +183,10 @@ void tx_packet(const cfg_t& cfg, const packet_sizes_t& ps, const tx_desc_t& d, c
 
     // scaling (tx.cpp:579-599)
     float scale_common = d.DAC_scale;
-    if (!d.optimal_scaling_DAC)
+    if (!d.optimal_scaling_DAC)  // as described in the standard
         scale_common *= static_cast<float>(W_scaling(tm.N_TS, tm.N_TX, d.codebook_index));
-    else
-        throw std::runtime_error("optimal_scaling_DAC not supported by oracle");
+    else  // optimised for the DAC's dynamic range
+        scale_common *= static_cast<float>(W_scaling_optimal_DAC(tm.N_TS, tm.N_TX, d.codebook_index));
     const float scale_stf = 1.0f / std::sqrt(static_cast<float>(N / 4)) * scale_common;
     const float scale_df = 1.0f / std::sqrt(static_cast<float>(N)) * scale_common;
     const auto W = W_matrix(tm.N_TS, tm.N_TX, d.codebook_index);

@@ -20,7 +20,7 @@ namespace orc {
 
 namespace {
 
-const float COVER_SEQ[9] = {1, -1, 1, 1, -1, -1, -1, -1, -1};  // stf.hpp:146-151 (cover active)
+const float* const COVER_SEQ = STF_COVER_SEQ;  // stf.hpp:146-151 (cover active)
 
 // movsum.hpp:28-120
 template <typename T>

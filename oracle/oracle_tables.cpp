@@ -482,6 +482,22 @@ double W_scaling(uint32_t N_TS, uint32_t N_TX, uint32_t codebook) {
     return static_cast<double>(1.0f / std::sqrt(cnt));
 }
 
+// W_t::scaling_factor_optimal_DAC, one list per matrix family in the constructor's order
+double W_scaling_optimal_DAC(uint32_t N_TS, uint32_t N_TX, uint32_t codebook) {
+    (void)W_table(N_TS, N_TX).at(codebook);
+    const float h = 1.0f / std::sqrt(2.0f), q = 1.0f / std::sqrt(4.0f);
+    float v = 1.0f;
+    if (N_TS == 2 && N_TX == 2) v = codebook == 0 ? 1.0f : h;
+    if (N_TS == 2 && N_TX == 4) v = codebook < 14 ? 1.0f : h;
+    if (N_TS == 4 && N_TX == 4) {
+        static const float t[5] = {1.0f, h, h, q, q};
+        v = t[codebook];
+    }
+    return static_cast<double>(v);
+}
+
+const float STF_COVER_SEQ[9] = {1, -1, 1, 1, -1, -1, -1, -1, -1};
+
 // ---------------------------------------------------------------- 3GPP TS 36.211 §7.2
 std::vector<uint8_t> gold_sequence(uint32_t c_init, uint32_t len) {
     const uint32_t Nc = 1600;

@@ -59,6 +59,11 @@ def lib():
         L.oracle_sync_geometry.argtypes = [U32P, U32P, C.POINTER(C.c_float)]
         L.oracle_stf_template.argtypes = [U32P, C.c_uint32, F32P]
         L.oracle_query_param.argtypes = [C.c_char_p, C.POINTER(C.c_double)]
+        L.oracle_W.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, F64P, F64P]
+        L.oracle_W_codebooks.argtypes = [C.c_uint32, C.c_uint32]
+        L.oracle_drs_values.argtypes = [C.c_uint32, C.c_uint32, F64P]
+        L.oracle_txdiv_pairs.argtypes = [C.c_uint32, U32P]
+        L.oracle_cover_sequence.argtypes = [F32P]
         _lib = L
     return _lib
 
@@ -97,10 +102,10 @@ def gold(c_init, n):
 
 
 def tx(cf, ps, pcc_d, pdc_d, S_slot, codebook=0, network_id=100, plcf_type=1, gi=5, dac=1.0, phase=0.0,
-       phase_inc=0.0, use_float=False):
+       phase_inc=0.0, use_float=False, optimal_dac=False):
     sz = packet_sizes(ps)
     out = np.zeros((sz["N_TX"], S_slot, 2), dtype=np.float32)
-    du = np.array([codebook, network_id, plcf_type, gi], dtype=np.uint32)
+    du = np.array([codebook, network_id, plcf_type, gi, int(optimal_dac)], dtype=np.uint32)
     df = np.array([dac, phase, phase_inc], dtype=np.float64)
     n = lib().oracle_tx(cf, ps, du, df, np.ascontiguousarray(pcc_d, dtype=np.uint8),
                         np.ascontiguousarray(pdc_d, dtype=np.uint8), out, S_slot, int(use_float))
@@ -178,6 +183,41 @@ def k_b_occ(b):
     out = np.zeros(1024, np.int32)
     n = lib().oracle_k_b_occ(b, out, out.size)
     return out[:n].tolist()
+
+
+def W(N_TS, N_TX, codebook):
+    """(W [N_TX][N_TS] complex, standard scaling, optimal-DAC scaling), None if undefined."""
+    out, sc = np.zeros(2 * 64), np.zeros(2)
+    n = lib().oracle_W(N_TS, N_TX, codebook, out, sc)
+    if n < 0:
+        return None
+    return out[: 2 * n].view(np.complex128).reshape(N_TX, N_TS), float(sc[0]), float(sc[1])
+
+
+def W_codebooks(N_TS, N_TX):
+    return lib().oracle_W_codebooks(N_TS, N_TX)
+
+
+def stf(b, n_eff_tx):
+    out = np.zeros(2 * (56 * b + 1))
+    n = lib().oracle_stf(b, n_eff_tx, out)
+    return out[: 2 * n].view(np.complex128)
+
+
+def drs_values(b, t):
+    out = np.zeros(14 * b)
+    return out[: lib().oracle_drs_values(b, t, out)]
+
+
+def txdiv_pairs(N_TS):
+    out = np.zeros(24, np.uint32)
+    return out[: 2 * lib().oracle_txdiv_pairs(N_TS, out)].reshape(-1, 2).tolist()
+
+
+def cover_sequence():
+    out = np.zeros(9, np.float32)
+    lib().oracle_cover_sequence(out)
+    return out
 
 
 def special(z):

@@ -56,6 +56,14 @@ TX_ONLY_CASES = {
 }
 
 
+def case(name):
+    """(psdef tuple, cfg tuple) of a configuration name of CONFIGS, PARITY_CASES or TX_ONLY_CASES."""
+    if name in CONFIGS:
+        return CONFIGS[name]
+    c = PARITY_CASES.get(name) or TX_ONLY_CASES[name]
+    return c[0], c[1]
+
+
 def random_bits(rng, n_bits):
     return rng.integers(0, 2, n_bits, dtype=np.uint8)
 
@@ -89,7 +97,7 @@ def sync_window(rng, O, name, S_win, starts, cfo_dect_rad, snr_db=30.0, n_rx=Non
     starting at the hw-sample offsets `starts` (each with its own random N_RX x N_TX mixing), CFO
     cfo_dect_rad per DECT-rate sample (the TX mixer applies it at the hw rate), AWGN at snr_db
     relative to the packet power. Returns (window, [(pcc_d, pdc_d, network_id, plcf_type)])."""
-    psd, cfgt = CONFIGS[name]
+    psd, cfgt = case(name)
     cf = O.cfg(cfgt[0], cfgt[1], os_min=cfgt[3], L=cfgt[4], M=cfgt[5])
     ps = O.psdef(*psd)
     sz = O.packet_sizes(ps)

@@ -93,6 +93,29 @@ def test_tx_parity(name):
         _check_tx(iq[i], ref, sz, S, n_tx, (name, i))
 
 
+@pytest.mark.parametrize("name,cb", [("tm5_u2b4", 3), ("tm2_sm2", 1), ("C4", 0)])
+def test_tx_optimal_scaling_dac(name, cb):
+    """tx_meta_t::optimal_scaling_DAC (tx.cpp:582-592): W_t::scaling_factor_optimal_DAC instead of
+    1/sqrt(non-zero W entries) -- 0.5 instead of 0.25 for N_TS = N_TX = 4 codebook 3, 1/sqrt2 instead
+    of 1/2 for N_TS = N_TX = 2 codebook 1 (tests/golden/ref_literals.json)."""
+    import dnrp
+    rng = np.random.default_rng(0xDAC)
+    phy, ps, ops, ocf = _ctx(name)
+    sz = phy.packet_sizes(ps)
+    S = sz["N_samples_packet_os_rs"]
+    pcc, pdc = _tx_inputs(rng, 2, sz)
+    descs = [dnrp.TxDesc(cb, 100 + i, 1 + i, 5, 1.0, 0.0, 0.0, i) for i in range(2)]  # std, optimal
+    iq = _gpu_tx(phy, ps, descs, pcc, pdc, S)
+    for i, d in enumerate(descs):
+        ref, n_tx = O.tx(ocf, ops, pcc[i], pdc[i], S, codebook=cb, network_id=d.network_id, plcf_type=d.plcf_type,
+                         optimal_dac=bool(i))
+        _check_tx(iq[i], ref, sz, S, n_tx, (name, cb, i))
+    ratio = np.linalg.norm(iq[1]) / np.linalg.norm(iq[0])  # different payloads, same power per packet
+    want = dnrp.query_table("W_scaling_optimal_DAC", sz["N_TS"], sz["N_TX"], cb)[0] / \
+        dnrp.query_table("W_scaling", sz["N_TS"], sz["N_TX"], cb)[0]
+    assert abs(ratio / want - 1) < 0.05, (name, ratio, want)
+
+
 def _rx_windows(rng, name, phy, ps, ops, ocf, snrs, cb=0):
     """Oracle-TX packets through a random N_RX x N_TX mixing, CFO and AWGN at per-packet SNRs.
     Returns the windows, sync reports (with a small residual CFO error), network IDs, PLCF types
@@ -244,6 +267,34 @@ def test_rx_pdc_request_errors():
     with pytest.raises(dnrp.DnrpError) as e:
         phy.rx_pdc_batch([dnrp.PdcReq(ps, 0, 999, 1)], iq, pdc_llr)
     assert e.value.code == -6
+    # the PDC symbols come from the PCC call's windows: another buffer is a state error
+    other = iq.clone()
+    with pytest.raises(dnrp.DnrpError) as e:
+        phy.rx_pdc_batch([dnrp.PdcReq(ps, 0, 100, 1)], other, pdc_llr)
+    assert e.value.code == -7
+
+
+def test_rx_window_index_checked_by_c_abi():
+    """dnrp_rx_pcc_batch range-checks sync_report.window against n_windows in C (a zeroed or garbage
+    report must not make the kernels read past iq_in), bypassing the Python-side check."""
+    import ctypes as C
+    import dnrp
+    phy, ps, ops, ocf = _ctx("C2")
+    S = phy.packet_sizes(ps)["N_samples_packet_os_rs"]
+    dev = torch.device("cuda:0")
+    iq = torch.zeros((2, 1, S, 2), dtype=torch.float32, device=dev)
+    pcc_llr = torch.zeros((2, 196), dtype=torch.int16, device=dev)
+    for win in (2, 0xFFFFFFFE):
+        reps = (dnrp.SyncReport * 2)(dnrp.SyncReport(0, 0.0, 0.0, 1, 1, 1, window=0),
+                                     dnrp.SyncReport(0, 0.0, 0.0, 1, 1, 1, window=win))
+        rc = dnrp.lib().dnrp_rx_pcc_batch(phy._ctx, 2, C.cast(reps, C.c_void_p), C.c_void_p(iq.data_ptr()), 2, S,
+                                          C.c_void_p(pcc_llr.data_ptr()), None, None)
+        assert rc == -1, (win, rc)
+    reps = (dnrp.SyncReport * 2)(dnrp.SyncReport(0, 0.0, 0.0, 1, 1, 1, window=0),
+                                 dnrp.SyncReport(0, 0.0, 0.0, 1, 1, 1, window=1))
+    assert dnrp.lib().dnrp_rx_pcc_batch(phy._ctx, 2, C.cast(reps, C.c_void_p), C.c_void_p(iq.data_ptr()), 2, S,
+                                        C.c_void_p(pcc_llr.data_ptr()), None, None) == 0
+    phy.sync()
 
 
 def test_rx_tm10_unsupported():

@@ -5,7 +5,14 @@ Tolerances: found flags, report count, detection antenna and time, N_eff_TX and 
 exact; coarse peak time within 1 DECT sample (smoothed-metric plateau: float vs double sums can
 move the last maximum by one position); fractional CFO within 2e-6 rad per DECT sample; RMS and
 metrics within 1e-3 relative. Then the synchronised chain: GPU sync -> GPU PCC/PDC demodulation
-against the oracle RX started from the oracle's own sync report (int16 LLRs within 1 LSB).
+against the oracle RX started from the same (GPU) sync report (int16 LLRs within 1 LSB), after the
+oracle's own search has found the same fine peak.
+
+Geometries: the bench configurations C2/C3/C4 (L/M 10/9, hl 24 stream kernel) plus every other sync
+kernel instantiation dispatched at kernels/sync.hip SYNC_DISPATCH / launch_sync_steps: L = M = 1
+(<1,1,0>), 40/27 (<0,0,0>, generic taps), os_min 2 (<9,10,4>), two transmit streams, and eight
+antennas with the fourth STF template (N_eff_TX = 8, crosscorrelator.cpp:122-251,
+physical_resources.hpp:44); the wave-kernel fallback of the step sums (DNRP_SYNC_STREAM=0).
 """
 import numpy as np
 import pytest
@@ -20,9 +27,10 @@ pytestmark = pytest.mark.gpu
 
 def _phy(name, max_batch=8):
     import dnrp
-    ps, cf = F.CONFIGS[name]
+    ps, cf = F.case(name)
     u_max, b_max, ntx, os_min, L, M = cf
-    phy = dnrp.Phy(u_max, b_max, ntx, os_min, L, M, max_batch=max_batch)
+    lr = F.PARITY_CASES[name][2] if name in F.PARITY_CASES else 1
+    phy = dnrp.Phy(u_max, b_max, ntx, os_min, L, M, chestim_mode_lr=bool(lr), max_batch=max_batch)
     for nid in range(100, 106):
         phy.add_network_id(nid)
     return phy
@@ -61,18 +69,39 @@ def _run(phy, sc, windows, max_reports, stream_layout=False):
     return res, cnt
 
 
-@pytest.mark.parametrize("name,S_win,chunk,stream_layout", [
-    ("C4", 20480, 4096, False), ("C3", 20480, 4096, True), ("C2", 1500, 400, False)])
+SYNC_GEOMETRIES = [
+    ("C4", 20480, 4096, False), ("C3", 20480, 4096, True), ("C2", 1500, 400, False),
+    ("lm1_1_u8b16", 20480, 4096, False),        # L = M = 1: sync kernels <1, 1, 0>
+    ("lm40_27_u8b12_tm5", 20480, 4096, True),   # 40/27: generic-tap kernels <0, 0, 0>
+    ("os2_u2b2_tm1", 6000, 1200, False),        # os_min 2: 9/10 with 45 taps <9, 10, 4>
+    ("tm1_txdiv2", 12800, 2560, False),         # 2 antennas, N_eff_TX = 2 template
+    ("tm10_u8b16", 20480, 4096, False),         # 8 antennas, 4th STF template (N_eff_TX = 8)
+]
+
+
+@pytest.mark.parametrize("name,S_win,chunk,stream_layout", SYNC_GEOMETRIES)
 def test_sync_parity(name, S_win, chunk, stream_layout):
+    _sync_parity(name, S_win, chunk, stream_layout)
+
+
+@pytest.mark.parametrize("name", ["C4", "C3"])
+def test_sync_parity_wave_kernel(name, monkeypatch):
+    """The step-sum wave kernel (sync_steps_wave_kernel, used when the stream kernel's geometry does
+    not hold) against the oracle: DNRP_SYNC_STREAM=0 forces it."""
+    monkeypatch.setenv("DNRP_SYNC_STREAM", "0")
+    _sync_parity(name, 20480, 4096, False)
+
+
+def _sync_parity(name, S_win, chunk, stream_layout):
     import dnrp
     rng = np.random.default_rng(21)
-    psd, cfgt = F.CONFIGS[name]
+    psd, cfgt = F.case(name)
     n_ant = cfgt[2]
     phy = _phy(name)
     windows, truth = [], []
     for i in range(5):
         start = int(rng.integers(0.15 * S_win, 0.3 * S_win))
-        cfo = rng.uniform(-1.75, 1.75) * 2 * np.pi / (64 * psd[1])
+        cfo = rng.uniform(-1.75, 1.75) * 2 * np.pi / (64 * psd[1] * cfgt[3])  # +-1.75 subcarriers
         win, _ = F.sync_window(rng, O, name, S_win, [start], cfo)
         windows.append(win)
         truth.append((start, cfo))
@@ -80,7 +109,7 @@ def test_sync_parity(name, S_win, chunk, stream_layout):
     windows.append(noise)
     sc = dnrp.SyncCfg(psd[0], psd[1], n_ant, chunk, 2)
     res, cnt = _run(phy, sc, windows, 2, stream_layout)
-    osc = O.sync_cfg(psd[0], psd[1], L=cfgt[4], M=cfgt[5], n_ant=n_ant, chunk_len=chunk)
+    osc = O.sync_cfg(psd[0], psd[1], os_min=cfgt[3], L=cfgt[4], M=cfgt[5], n_ant=n_ant, chunk_len=chunk)
     for w, win in enumerate(windows):
         ref = O.sync(osc, win, max_reports=2)
         assert int(cnt[w]) == len(ref), (w, int(cnt[w]), len(ref))
@@ -90,6 +119,7 @@ def test_sync_parity(name, S_win, chunk, stream_layout):
             assert int(res[w, k]["found"]) == 0
         if w < len(truth):
             assert int(res[w, 0]["fine_peak_time"]) == truth[w][0]
+            assert int(res[w, 0]["N_eff_TX"]) == O.packet_sizes(O.psdef(*psd))["N_eff_TX"]
 
 
 def test_sync_two_packets_per_window():
@@ -129,28 +159,33 @@ def test_sync_two_packets_per_window():
         assert np.array_equal(np.unpackbits(meta[i][1])[:G], (r["pdc_llr"] > 0).astype(np.uint8)), i
 
 
-def test_sync_then_demodulate_c4():
-    """GPU sync -> GPU RX on the synchronised windows vs the oracle RX from the oracle sync report."""
+@pytest.mark.parametrize("name", ["C4", "lm1_1_u8b16", "lm40_27_u8b12_tm5", "os2_u2b2_tm1", "tm1_txdiv2"])
+def test_sync_then_demodulate(name):
+    """GPU sync -> GPU RX on the synchronised windows vs the oracle RX fed the same (GPU) sync report,
+    int16 LLRs within the +-1 gate; the oracle's own search must find the same fine peak and CFO."""
     import dnrp
     rng = np.random.default_rng(25)
-    name = "C4"
-    psd, cfgt = F.CONFIGS[name]
+    psd, cfgt = F.case(name)
+    lr = F.PARITY_CASES[name][2] if name in F.PARITY_CASES else 1
+    n_ant = cfgt[2]
     phy = _phy(name)
     ps = dnrp.psdef(*psd)
     sz = phy.packet_sizes(ps)
     S = sz["N_samples_packet_os_rs"]
-    pre = 2400
+    pre = sz["N_samples_STF"] * cfgt[3] * cfgt[4] // cfgt[5]  # one STF of lead-in at the hw rate
+    S_win = S + pre + 32
+    chunk = S_win * 7 // 8
     windows, metas = [], []
     for i in range(2):
-        cfo = rng.uniform(-1.75, 1.75) * 2 * np.pi / 1024
-        win, meta = F.sync_window(rng, O, name, S, [pre + int(rng.integers(0, 32))], cfo)
+        cfo = rng.uniform(-1.75, 1.75) * 2 * np.pi / sz["N_b_DFT_os"]
+        win, meta = F.sync_window(rng, O, name, S_win, [pre + int(rng.integers(0, 32))], cfo)
         windows.append(win)
         metas.append(meta[0])
-    sc = dnrp.SyncCfg(psd[0], psd[1], 4, 89280, 1)
+    sc = dnrp.SyncCfg(psd[0], psd[1], n_ant, chunk, 1)
     res, cnt = _run(phy, sc, windows, 1)
     assert list(cnt) == [1, 1]
     dev = torch.device("cuda:0")
-    iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(2, 4, S, 2)).to(dev)
+    iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(2, n_ant, S_win, 2)).to(dev)
     reps = dnrp.sync_reports(res[:, 0])
     pcc_llr = torch.zeros((2, 196), dtype=torch.int16, device=dev)
     pdc_llr = torch.zeros((2, sz["G"]), dtype=torch.int16, device=dev)
@@ -158,15 +193,15 @@ def test_sync_then_demodulate_c4():
     phy.rx_pdc_batch([dnrp.PdcReq(ps, i, m[2], m[3]) for i, m in enumerate(metas)], iq, pdc_llr)
     phy.sync()
     g_pcc, g_pdc = pcc_llr.cpu().numpy(), pdc_llr.cpu().numpy()
-    ocf = O.cfg(cfgt[0], cfgt[1], os_min=cfgt[3], L=cfgt[4], M=cfgt[5])
-    osc = O.sync_cfg(psd[0], psd[1], L=cfgt[4], M=cfgt[5], n_ant=4, chunk_len=89280)
+    ocf = O.cfg(cfgt[0], cfgt[1], os_min=cfgt[3], L=cfgt[4], M=cfgt[5], lr=lr)
+    osc = O.sync_cfg(psd[0], psd[1], os_min=cfgt[3], L=cfgt[4], M=cfgt[5], n_ant=n_ant, chunk_len=chunk)
     for i, win in enumerate(windows):
         o = O.sync(osc, win, max_reports=1)[0]
-        assert o["fine_64"] == int(res[i, 0]["fine_peak_time"])
-        r = O.rx(ocf, O.psdef(*psd), win, o["fine_64"], float(np.float32(o["cfo_frac"])), metas[i][2], metas[i][3])
+        fine, cfo_g = int(res[i, 0]["fine_peak_time"]), float(res[i, 0]["cfo_fractional_rad"])
+        assert o["fine_64"] == fine and abs(o["cfo_frac"] - cfo_g) < 2e-6, (name, i, o["fine_64"], fine)
+        r = O.rx(ocf, O.psdef(*psd), win, fine, cfo_g, metas[i][2], metas[i][3])
         d_pdc = np.abs(g_pdc[i].astype(np.int32) - r["pdc_llr"].astype(np.int32))
         d_pcc = np.abs(g_pcc[i].astype(np.int32) - r["pcc_llr"].astype(np.int32))
-        assert d_pcc.max() <= 1 and d_pdc.max() <= 2, (d_pcc.max(), d_pdc.max())
-        assert np.mean(d_pdc > 1) < 1e-4
+        assert d_pcc.max() <= 1 and d_pdc.max() <= 1, (name, i, d_pcc.max(), d_pdc.max())
         bits = np.unpackbits(metas[i][1])[: sz["G"]]
-        assert np.mean((g_pdc[i] > 0).astype(np.uint8) != bits) < 1e-3
+        assert np.mean((g_pdc[i] > 0).astype(np.uint8) != bits) < 2e-2, name
