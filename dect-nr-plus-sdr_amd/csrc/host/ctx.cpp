@@ -314,16 +314,22 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         *err = DNRP_ECONFIG;
         return nullptr;
     }
-    if (tm.N_SS > 1 || tm.N_eff_TX > 4 || t->q.N_bps > 8) {  // rx_synced.cpp:1331-1333 (AxA MIMO is \todo)
+    // rx_synced.cpp:1331-1333: spatial multiplexing (AxA MIMO) is a \todo in the reference receiver;
+    // demodulated here by MMSE only when the context opted in (DNRP_RX_MODE_SM_MMSE)
+    const bool sm = tm.N_SS > 1;
+    if ((sm && !(ctx->rx_mode & DNRP_RX_MODE_SM_MMSE)) || (sm && (tm.N_SS != tm.N_eff_TX || tm.N_SS > 4 ||
+                                                                 ctx->cfg.N_TX_max < tm.N_SS)) ||
+        tm.N_eff_TX > 4 || t->q.N_bps > 8) {
         *err = DNRP_EUNSUPPORTED;
         return nullptr;
     }
+    t->sm = sm;
     t->maps = geo::build_maps(d.b, tm.N_TS, tm.N_eff_TX, t->q.N_DF_symb);
     std::vector<geo::op_t> pcc_ops, pdc_ops;
     uint32_t pm;
     geo::build_rx_ops(t->maps, tm.N_eff_TX, t->q.N_DF_symb, ctx->cfg.chestim_mode_lr != 0,
                       std::max(1u, ctx->cfg.chestim_lr_stride), pcc_ops, pdc_ops, pm);
-    const auto plan = geo::build_rx_plan(t->maps, pdc_ops, tm.N_eff_TX);
+    const auto plan = geo::build_rx_plan(t->maps, pdc_ops, tm.N_eff_TX, !sm);
     std::vector<uint16_t> csym(t->maps.pdc_k.size());
     for (uint32_t l = 0; l <= t->q.N_DF_symb; ++l)
         for (uint32_t j = t->maps.pdc_sym_off[l]; j < t->maps.pdc_sym_off[l + 1]; ++j) csym[j] = static_cast<uint16_t>(l);
@@ -423,10 +429,12 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, con
 // back-end launches of one phase: SNR chain, then cells (rx_back.hip)
 int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t n, const uint32_t* sel, bool pdc,
                 uint32_t N_bps, const uint32_t* kk, const uint16_t* cell_sym, int16_t* llr, uint32_t llr_stride,
-                hipStream_t st) {
+                hipStream_t st, bool sm = false) {
     const char* name = pdc ? "rx_pdc" : "rx_pcc";
     if (plan.n_dops > dev::RX_MAX_DOPS || !plan.cells_ok) return DNRP_EUNSUPPORTED;
-    if (!ctx->lut_d.ensure(size_t(ctx->cfg.max_batch) * dev::RX_MAX_DOPS)) return DNRP_ENOMEM;
+    if (!ctx->lut_d.ensure(size_t(ctx->cfg.max_batch) * dev::RX_MAX_DOPS) ||
+        !ctx->nv_d.ensure(size_t(ctx->cfg.max_batch) * dev::RX_MAX_DOPS * sizeof(float)))
+        return DNRP_ENOMEM;
     dev::rx_snr_args s{};
     s.N_RX = ctx->cfg.N_TX_max;
     s.Nf_pad = ctx->rx_Nf_pad;
@@ -442,6 +450,7 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     s.Y = ctx->Y.as<float2>();
     s.st = ctx->rx_st.as<dev::rx_pkt_state>();
     s.lut_d = ctx->lut_d.as<uint8_t>();
+    s.nv_d = ctx->nv_d.as<float>();
     s.sel = sel;
     dev::rx_cells_args c{};
     c.N_occ = t->N_occ;
@@ -457,6 +466,8 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     c.wcap[1] = t->wcap[1];
     fill_pairs(t->N_eff_TX, c.pair, c.mod);
     c.is_pdc = pdc;
+    c.sm = sm ? 1u : 0u;
+    c.nv_d = s.nv_d;
     c.epochs = plan.epochs.as<dev::rx_epoch>();
     c.segs = plan.segs.as<dev::rx_seg>();
     c.dl = s.dl;
@@ -475,7 +486,8 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     c.sel = sel;
     ctx->tic(name, st);
     if (dev::launch_rx_snr(s, n, st) != hipSuccess) return DNRP_EDEVICE;
-    if (plan.n_epochs && dev::launch_rx_cells(c, n, st) != hipSuccess) return DNRP_EDEVICE;
+    if (plan.n_epochs && (sm ? dev::launch_rx_cells_sm(c, n, st) : dev::launch_rx_cells(c, n, st)) != hipSuccess)
+        return sm ? DNRP_EUNSUPPORTED : DNRP_EDEVICE;
     ctx->toc(name, st);
     return DNRP_OK;
 }
@@ -892,7 +904,7 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
             ctx->toc("rx_fft_pdc", st);
         }
         if ((err = launch_back(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps, t2->pdc_k.as<uint32_t>(),
-                               t2->pdc_sym.as<uint16_t>(), pdc_llr, llr_stride, st)) != DNRP_OK)
+                               t2->pdc_sym.as<uint16_t>(), pdc_llr, llr_stride, st, t2->sm)) != DNRP_OK)
             return err;
         if (rep) {
             // MIMO report at the packet end (rx_synced.cpp:417-436; the reference runs it after a
@@ -932,6 +944,14 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
             rep[r].tm_3_7_beamforming_reciprocal_idx = mo[3 * r + 2];
         }
     }
+    return DNRP_OK;
+}
+
+int dnrp_ctx_set_rx_mode(dnrp_ctx* ctx, uint32_t flags) {
+    if (!ctx || (flags & ~uint32_t(DNRP_RX_MODE_SM_MMSE))) return DNRP_EINVAL;
+    if (flags != ctx->rx_mode) ctx->rx2t.clear();  // PDC tables depend on the mode
+    ctx->rx_mode = flags;
+    ctx->rx_valid = false;
     return DNRP_OK;
 }
 

@@ -148,6 +148,7 @@ struct rx2_tables {  // per (psdef): PDC phase
     geo::maps_t maps;
     dbuf pdc_k, pdc_sym;
     rx_plan_dev bplan;  // PDC phase back end
+    bool sm = false;    // spatial multiplexing (N_SS > 1): MMSE cells kernel
     // MIMO report (estimator_mimo_t): wideband DRS cells, single-stream codebooks
     uint32_t N_TS = 1, ncb_tx = 0, A_tx = 0, ncb_rx = 0, A_rx = 0;
     dbuf mimo_cells, mimo_signs, Wtx, stx, Wrx, srx;
@@ -184,7 +185,8 @@ struct dnrp_ctx {
     std::map<uint32_t, std::unique_ptr<netid_seq>> netid;
     dbuf pcc_seq;
     // batch scratch
-    dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d, mimo_out;
+    dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d, nv_d, mimo_out;
+    uint32_t rx_mode = 0;  // DNRP_RX_MODE_* (dnrp_ctx_set_rx_mode)
     pinned st_tx, st_rxin, st_seq, st_rep;
     // retained RX phase-1 state: per PCC-batch slot its (u, b, N_eff_TX) tables and symbol
     // capacity; Y is laid out with the batch-wide maxima rx_nsym_cap / rx_Nf_pad

@@ -690,14 +690,15 @@ void build_rx_ops(const maps_t& m, uint32_t N_eff_TX, uint32_t N_DF, bool mode_l
     }
 }
 
-rx_plan_t build_rx_plan(const maps_t& m, const std::vector<op_t>& ops, uint32_t NT) {
+rx_plan_t build_rx_plan(const maps_t& m, const std::vector<op_t>& ops, uint32_t NT, bool pair_units) {
     rx_plan_t p;
     uint16_t src[4][2];
     for (auto& r : src) r[0] = r[1] = RX_SRC_NONE;
     uint32_t drs_off = 0, drs_cnt = 0;
     bool dirty = true;
     rx_seg_t ev{};
-    auto units = [&](const rx_seg_t& s) { return NT == 1 ? s.j1 - s.j0 : (s.j1 - s.j0) / 2; };
+    const bool pairs = NT > 1 && pair_units;
+    auto units = [&](const rx_seg_t& s) { return pairs ? (s.j1 - s.j0) / 2 : s.j1 - s.j0; };
     auto add = [&](rx_seg_t s) {
         if (s.j1 <= s.j0) return;
         if (dirty || p.epochs.empty()) {

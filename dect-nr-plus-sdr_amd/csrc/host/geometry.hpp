@@ -129,6 +129,8 @@ struct rx_plan_t {
     std::vector<rx_seg_t> segs;
     std::vector<rx_epoch_t> epochs;
 };
-rx_plan_t build_rx_plan(const maps_t& m, const std::vector<op_t>& ops, uint32_t N_eff_TX);
+// pair_units: a work unit is an SFBC pair of cells when N_eff_TX > 1 (transmit diversity); false for
+// spatial multiplexing, whose unit is one cell carrying N_SS symbols
+rx_plan_t build_rx_plan(const maps_t& m, const std::vector<op_t>& ops, uint32_t N_eff_TX, bool pair_units = true);
 
 }  // namespace dnrp::geo

@@ -24,8 +24,25 @@ using cd = std::complex<double>;
 
 const float* const COVER = prm::STF_COVER;  // stf.hpp:146-151 (cover sequence active)
 
-void fft_host(std::vector<cd>& x, int sign) {  // iterative radix-2, unnormalised
+// unnormalised DFT of any length: the STF IFFT is 64 b os points (768 / 1536 / 3072 for b = 12),
+// the template spectra are powers of two. Init-time only.
+void dft_direct(std::vector<cd>& x, int sign) {
     const size_t n = x.size();
+    std::vector<cd> y(n, cd(0, 0));
+    for (size_t k = 0; k < n; ++k) {
+        cd acc(0, 0);
+        for (size_t i = 0; i < n; ++i) {
+            const double a = sign * 2.0 * M_PI * static_cast<double>((k * i) % n) / static_cast<double>(n);
+            acc += x[i] * cd(std::cos(a), std::sin(a));
+        }
+        y[k] = acc;
+    }
+    x.swap(y);
+}
+
+void fft_host(std::vector<cd>& x, int sign) {  // iterative radix-2 for powers of two, unnormalised
+    const size_t n = x.size();
+    if (n == 0 || (n & (n - 1))) return dft_direct(x, sign);
     for (size_t i = 1, j = 0; i < n; ++i) {
         size_t bit = n >> 1;
         for (; j & bit; bit >>= 1) j ^= bit;

@@ -133,6 +133,7 @@ struct rx_snr_args {        // DRS zero-forcing SNR chain + LUT profile picks, o
     const float2* Y;
     rx_pkt_state* st;
     uint8_t* lut_d;         // [slot][RX_MAX_DOPS]: profile picked after each DRS op
+    float* nv_d;            // [slot][RX_MAX_DOPS]: noise variance per RX cell after each DRS op
     const uint32_t* sel;    // launch packet -> slot / output row
 };
 hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st);
@@ -145,6 +146,7 @@ struct rx_lut {             // one Wiener LUT: [T][4][Nf] pilot | weight << 16, 
 
 struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epoch)
     uint32_t N_occ, N_RX, NT, Nf_pad, n_sym_total, n_drs, n_dops, n_epochs, N_bps, mod, is_pdc;
+    uint32_t sm;               // 1: spatial multiplexing, NT = N_SS streams per cell, MMSE (unit = cell)
     uint32_t wcap[2];          // floats of the LDS weight-table slot of mode l / lr (largest such table)
     uint32_t pair[12];
     const rx_epoch* epochs;
@@ -158,6 +160,7 @@ struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epo
     const rx_lut* luts;        // [mode l / lr][profile] (device table: no dynamic kernel-argument indexing)
     const float2* Y;
     const uint8_t* lut_d;
+    const float* nv_d;         // [slot][RX_MAX_DOPS] noise variance after each DRS op (MMSE)
     const uint8_t* pcc_seq;
     const uint8_t* const* pdc_seq;  // per output row (PDC phase)
     int16_t* llr;                   // PCC: [n][196], PDC: [m][llr_stride] (output rows)
@@ -165,6 +168,8 @@ struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epo
     const uint32_t* sel;            // launch packet -> slot / output row
 };
 hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st);
+// spatial multiplexing (a.sm): N_RX x N_SS in {2, 4, 8} x {2, 4} with N_RX >= N_SS
+hipError_t launch_rx_cells_sm(const rx_cells_args& a, uint32_t n, hipStream_t st);
 
 // rx_cells_kernel's per-workgroup LDS staging (rx_back.hip, rx_eq.hpp).
 // The epoch's pilot buffer zfi: one row per (rx, ts) of 2 nd interlaced pilots plus ZFI_PAD zeros.

@@ -115,6 +115,8 @@ __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
             }
         }
         A.lut_d[size_t(pkt) * MAX_DOPS + d] = static_cast<uint8_t>(pick);
+        // noise variance per RX cell behind the pick (MMSE regularisation of spatial multiplexing)
+        A.nv_d[size_t(pkt) * MAX_DOPS + d] = nn > 0.0 ? static_cast<float>(nn / nn_cnt) : 0.f;
     }
     if (A.is_pdc)
         st->snr_pdc = snr_db();
@@ -137,7 +139,7 @@ hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st) {
 // ===================================================================== cells
 constexpr uint32_t CELL_THREADS = 512;
 
-template <int NRX, int NT>
+template <int NRX, int NT, bool SM = false>
 __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     const uint32_t zst = zfi_stride(A.n_drs);
@@ -182,6 +184,25 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
     if (tid >= units) return;
     const uint8_t* __restrict__ seq = A.is_pdc ? A.pdc_seq[row] : A.pcc_seq;
     int16_t* __restrict__ llr = A.llr + size_t(row) * A.llr_stride;
+    if constexpr (SM) {  // spatial multiplexing: unit = one cell carrying NT symbols, MMSE (rx_eq.hpp)
+        const float nv = dc ? A.nv_d[size_t(pkt) * RX_MAX_DOPS + dc - 1] : 0.f;
+        uint32_t si = 0;
+        unit_a na;
+        unit_sm<NRX, NT> cur;
+        uint32_t u = tid;
+        unit_stage_a(A, sg, nseg, si, u, 1u, na);
+        unit_stage_b_sm<NRX, NT>(A, sg, Yp, seq, na, cur);
+        if (u + CELL_THREADS < units) unit_stage_a(A, sg, nseg, si, u + CELL_THREADS, 1u, na);
+        for (; u < units; u += CELL_THREADS) {
+            unit_sm<NRX, NT> nb;
+            const bool m1 = u + CELL_THREADS < units, m2 = u + 2 * CELL_THREADS < units;
+            if (m1) unit_stage_b_sm<NRX, NT>(A, sg, Yp, seq, na, nb);
+            if (m2) unit_stage_a(A, sg, nseg, si, u + 2 * CELL_THREADS, 1u, na);
+            eq_mmse<NRX, NT>(A, sg, zfi, wtab, zst, nv, cur, llr);
+            if (m1) cur = nb;
+        }
+        return;
+    }
     constexpr uint32_t per_unit = NT == 1 ? 1u : 2u;
     // stage A two units ahead, stage B one unit ahead of eq_compute (rx_eq.hpp)
     uint32_t si = 0;
@@ -220,6 +241,24 @@ hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st) {
     DNRP_CELLS(4, 4)
     DNRP_CELLS(8, 4)
 #undef DNRP_CELLS
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_rx_cells_sm(const rx_cells_args& a, uint32_t n, hipStream_t st) {
+    const size_t lds = cell_lds_bytes(a.N_RX, a.NT, a.n_drs, a.wcap[0], a.wcap[1]);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const dim3 g(n * a.n_epochs), b(CELL_THREADS);
+#define DNRP_CELLS_SM(R, T)                                                              \
+    if (a.N_RX == R && a.NT == T) {                                                      \
+        hipLaunchKernelGGL((rx_cells_kernel<R, T, true>), g, b, lds, st, a);             \
+        return hipGetLastError();                                                        \
+    }
+    DNRP_CELLS_SM(2, 2)
+    DNRP_CELLS_SM(4, 2)
+    DNRP_CELLS_SM(8, 2)
+    DNRP_CELLS_SM(4, 4)
+    DNRP_CELLS_SM(8, 4)
+#undef DNRP_CELLS_SM
     return hipErrorInvalidValue;
 }
 

@@ -244,6 +244,159 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
     }
 }
 
+// ===================================================================== spatial multiplexing (MMSE)
+// N_SS = NT > 1 spatial streams on the NT transmit streams (tx.cpp:1051-1067: symbol s of cell j is
+// spatial-stream symbol j NT + s). Not in the reference receiver (run_pdc_mode_AxA_MIMO,
+// rx_synced.cpp:1331-1333, \todo): opt-in (dnrp_ctx_set_rx_mode). Per cell the Wiener-interpolated
+// channel H[rx][ss] of every stream, linear MMSE x = (H^H H + nv I)^-1 H^H y with nv the SNR
+// estimator's noise variance at the epoch's LUT pick, unbiased per stream by
+// beta_s = 1 - nv [(H^H H + nv I)^-1]_ss, then the same demapper and descrambling as MRC / SFBC.
+// The NT x NT Hermitian solve runs per lane in registers (Cholesky, L^-1): per cell it is ~NRX NT^2
+// complex MACs for the Gram matrix and ~NT^3 for the solve -- a lane-per-subcarrier batch of tiny
+// independent systems, which the lane layout keeps off the matrix cores.
+template <int NRX, int NT>
+struct unit_sm {
+    uint32_t si, jj;
+    uint32_t pw[NT];  // LUT pilot | weight words of every stream at the cell's subcarrier
+    uint32_t sb[5];   // scrambling bytes from bit (jj NT N_bps) & ~7: NT N_bps <= 32 bits
+    float2 r0[NRX];
+};
+
+template <int NRX, int NT>
+__device__ __forceinline__ void unit_stage_b_sm(const rx_cells_args& A, const cell_seg* sg,
+                                                const float2* __restrict__ Yp, const uint8_t* __restrict__ seq,
+                                                const unit_a& a, unit_sm<NRX, NT>& b) {
+    const uint32_t Nf = A.N_occ + 1;
+    const cell_seg& S = sg[a.si];
+    const uint32_t swap = (S.info >> 1) & 3u;
+    b.si = a.si;
+    b.jj = a.jj;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b.pw[t] = S.pw[((static_cast<uint32_t>(t) & 3u) ^ swap) * Nf + a.k0];
+    const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
+    const uint32_t yoff = a.l * A.Nf_pad;
+#pragma unroll
+    for (int r = 0; r < NRX; ++r) b.r0[r] = Yp[r * ast + yoff + a.k0];
+    const uint32_t b0 = (a.jj * NT * A.N_bps) >> 3, bl = ((a.jj + 1) * NT * A.N_bps - 1) >> 3;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) b.sb[i] = seq[min(b0 + i, bl)];
+}
+
+// demap + descramble + int16 of one symbol: LLRs base .. base + N_bps - 1; bits: 5 scrambling bytes
+// (byte k at bits 8k) from bit b_first & ~7 of the unit's first LLR
+__device__ __forceinline__ void emit_sym64(float2 x, uint32_t base, uint32_t b_first, uint32_t N_bps, uint64_t bits,
+                                           int16_t* __restrict__ llr) {
+    float L[8];
+    demap(x, N_bps, L);
+    const uint32_t r0 = base - (b_first & ~7u);
+    auto sbit = [&](uint32_t i) {
+        const uint32_t r = r0 + i;
+        return static_cast<uint32_t>(bits >> (8 * (r >> 3) + 7 - (r & 7u))) & 1u;
+    };
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k)
+        if (k < N_bps) llr[base + k] = q16(sbit(k) ? -L[k] : L[k]);
+}
+
+template <int NRX, int NT>
+__device__ __forceinline__ void eq_mmse(const rx_cells_args& A, const cell_seg* sg, const float2* zfi, const float* wtab,
+                                        uint32_t zst, float nv, const unit_sm<NRX, NT>& b, int16_t* __restrict__ llr) {
+    const uint32_t info = sg[b.si].info, wbase = sg[b.si].wbase;
+    const uint32_t mode = info & 1u, off = (info >> 4) & 0xFFu, nI = info >> 12;
+    const uint32_t step = mode ? 1u : 2u;
+    // Wiener interpolation of every (rx, stream) at the cell (rx_synced.cpp:932-946)
+    float2 h[NRX][NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        uint32_t p = b.pw[t] & 0xFFFFu;
+        if (!mode) p = 2 * p + ((off >> t) & 1u);
+        const uint32_t pos = p + t * zst, wo = wbase + (b.pw[t] >> 16) * nI;
+#pragma unroll
+        for (int a = 0; a < NRX; ++a) h[a][t] = make_float2(0.f, 0.f);
+        for (uint32_t i = 0; i < nI; ++i) {
+            const float wv = wtab[wo + i];
+            const uint32_t q = pos + i * step;
+#pragma unroll
+            for (int a = 0; a < NRX; ++a) {
+                const float2 z = zfi[a * NT * zst + q];
+                h[a][t].x = fmaf(z.x, wv, h[a][t].x);
+                h[a][t].y = fmaf(z.y, wv, h[a][t].y);
+            }
+        }
+    }
+    // G = H^H H + nv I (diagonal gd, strictly lower go[i][j] = sum_a conj(h_ai) h_aj), z = H^H y
+    float gd[NT];
+    float2 go[NT][NT], zz[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        gd[i] = nv;
+        zz[i] = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int a = 0; a < NRX; ++a) {
+            gd[i] += cnorm(h[a][i]);
+            zz[i] = cadd(zz[i], cmulc(b.r0[a], h[a][i]));
+        }
+#pragma unroll
+        for (int j = 0; j < i; ++j) {
+            go[i][j] = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int a = 0; a < NRX; ++a) go[i][j] = cadd(go[i][j], cmulc(h[a][j], h[a][i]));
+        }
+    }
+    // Cholesky G = L L^H (real diagonal ld, reciprocal il), then Mi = L^-1
+    float il[NT];
+    float2 Lm[NT][NT], Mi[NT][NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        float d = gd[j];
+#pragma unroll
+        for (int m = 0; m < j; ++m) d -= cnorm(Lm[j][m]);
+        il[j] = rsqrtf(fmaxf(d, 1e-30f));
+#pragma unroll
+        for (int i = j + 1; i < NT; ++i) {
+            float2 v = go[i][j];
+#pragma unroll
+            for (int m = 0; m < j; ++m) v = csub(v, cmulc(Lm[i][m], Lm[j][m]));
+            Lm[i][j] = cscale(v, il[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        Mi[j][j] = make_float2(il[j], 0.f);
+#pragma unroll
+        for (int i = j + 1; i < NT; ++i) {
+            float2 v = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int m = j; m < i; ++m) v = cadd(v, cmul(Lm[i][m], Mi[m][j]));
+            Mi[i][j] = cscale(v, -il[i]);
+        }
+    }
+    // w = L^-1 z; x = L^-H w; [G^-1]_ss = sum_m |Mi[m][s]|^2
+    float2 w[NT];
+#pragma unroll
+    for (int m = 0; m < NT; ++m) {
+        w[m] = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q <= m; ++q) w[m] = cadd(w[m], cmul(Mi[m][q], zz[q]));
+    }
+    const uint32_t b_first = b.jj * NT * A.N_bps;
+    uint64_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) bits |= static_cast<uint64_t>(b.sb[i] & 0xFFu) << (8 * i);
+#pragma unroll
+    for (int s = 0; s < NT; ++s) {
+        float2 x = make_float2(0.f, 0.f);
+        float ginv = 0.f;
+#pragma unroll
+        for (int m = s; m < NT; ++m) {
+            x = cadd(x, cmulc(w[m], Mi[m][s]));
+            ginv += cnorm(Mi[m][s]);
+        }
+        const float beta = 1.f - nv * ginv;
+        emit_sym64(cscale(x, 1.0f / beta), b_first + s * A.N_bps, b_first, A.N_bps, bits, llr);
+    }
+}
+
 // The epoch's pilot buffer: zero-forced DRS cells of every (rx, ts) at their interlace slots
 // (channel_antenna.hpp:38-63), read from the DRS symbols in Y. Whole workgroup, no barrier. The
 // source DRS op of every (ts, interlace slot), its parity and symbol are workgroup-uniform (scalar

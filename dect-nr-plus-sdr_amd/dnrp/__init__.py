@@ -171,7 +171,7 @@ EXPORTS = ["dnrp_ctx_create", "dnrp_ctx_destroy", "dnrp_add_network_id", "dnrp_g
            "dnrp_pcc_decode", "dnrp_pdc_encode", "dnrp_pdc_decode", "dnrp_harq_rx_create", "dnrp_harq_rx_reset",
            "dnrp_harq_rx_destroy", "dnrp_pdc_decode_batch", "dnrp_pdc_encode_batch",
            "dnrp_pcc_decode_batch", "dnrp_pdc_decode_batch_harq", "dnrp_pdc_softbuffer_size",
-           "dnrp_pcc_encode_batch", "dnrp_query_table"]
+           "dnrp_pcc_encode_batch", "dnrp_query_table", "dnrp_ctx_set_rx_mode"]
 
 _lib = None
 
@@ -197,6 +197,7 @@ def lib():
         L.dnrp_rx_pdc_batch.argtypes = [P, C.c_uint32, C.POINTER(PdcReq), P, C.c_uint32, C.c_uint32, P, C.c_uint32,
                                         C.POINTER(PdcReport), P]
         L.dnrp_sync.argtypes = [P, P]
+        L.dnrp_ctx_set_rx_mode.argtypes = [P, C.c_uint32]
         L.dnrp_ring_gather.argtypes = [P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P, C.c_uint32, P, P]
         L.dnrp_channel_batch.argtypes = [P, C.POINTER(ChannelCfg), C.c_uint32, C.c_uint32, P, C.c_uint32, C.c_uint32, P, P,
                                          P, C.c_uint32, P]
@@ -353,6 +354,12 @@ class Phy:
             self.close()
         except Exception:
             pass
+
+    RX_MODE_SM_MMSE = 1
+
+    def set_rx_mode(self, flags):
+        """dnrp_ctx_set_rx_mode: RX_MODE_SM_MMSE enables the MMSE receiver for spatial multiplexing."""
+        _chk(lib().dnrp_ctx_set_rx_mode(self._ctx, int(flags)), "dnrp_ctx_set_rx_mode")
 
     def add_network_id(self, nid):
         _chk(lib().dnrp_add_network_id(self._ctx, nid), "dnrp_add_network_id")

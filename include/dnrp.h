@@ -237,6 +237,19 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
 int dnrp_sync(dnrp_ctx* ctx, void* stream);
 
 /*
+ * Receiver options beyond the reference (default 0: exactly the reference's receiver).
+ *   DNRP_RX_MODE_SM_MMSE  dnrp_rx_pdc_batch demodulates spatial multiplexing (N_SS = N_eff_TX in
+ *                         {2, 4}: TM 2/4/6/8/9, N_RX >= N_SS) by linear MMSE per cell, x = (H^H H +
+ *                         nv I)^-1 H^H y with the Wiener-interpolated channel of every transmit stream
+ *                         and the SNR estimator's noise variance nv, unbiased per stream, then the same
+ *                         soft demapper. The reference leaves run_pdc_mode_AxA_MIMO empty
+ *                         (rx_synced.cpp:1331-1333) and returns DNRP_EUNSUPPORTED without this flag.
+ * Takes effect for the next dnrp_rx_pcc_batch (a preceding PCC batch's state is dropped).
+ */
+#define DNRP_RX_MODE_SM_MMSE 1u
+int dnrp_ctx_set_rx_mode(dnrp_ctx* ctx, uint32_t flags);
+
+/*
  * Ring-buffer window gather <- rx_pacer_t's wrap copy (rx_pacer.cpp:106-143) over the per-antenna
  * ring of radio::buffer_rx_t (radio/buffer_rx.hpp:46-141; sample of global time t at index
  * t % ring_len). Copies window w = global samples [start[w], start[w] + S_win) of antennas

@@ -325,11 +325,12 @@ int oracle_tx(const uint32_t* cfg, const uint32_t* psdef, const uint32_t* desc_u
 //           12 mimo N_TS_other, 13 tm_3_7_beamforming_idx, 14 tm_3_7_beamforming_reciprocal_idx
 int oracle_rx(const uint32_t* cfg, const uint32_t* psdef, uint32_t N_RX, const float* iq, uint32_t S_in,
               int64_t fine_peak, double cfo_rad, uint32_t network_id, uint32_t plcf_type, int16_t* pcc_llr,
-              int16_t* pdc_llr, float* pcc_llr_f, float* pdc_llr_f, float* meta, int use_float, const float* sync_rms) {
+              int16_t* pdc_llr, float* pcc_llr_f, float* pdc_llr_f, float* meta, int use_float, const float* sync_rms,
+              int sm_mmse) {
     try {
         packet_sizes_t q;
         if (!get_packet_sizes(to_psdef(psdef), q)) return -1;
-        rx_in_t in{iq, N_RX, S_in, fine_peak, cfo_rad, network_id, plcf_type, sync_rms};
+        rx_in_t in{iq, N_RX, S_in, fine_peak, cfo_rad, network_id, plcf_type, sync_rms, sm_mmse != 0};
         rx_out_t o;
         if (use_float)
             rx_packet<float>(to_cfg(cfg), q, in, o);

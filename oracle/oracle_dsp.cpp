@@ -385,6 +385,7 @@ struct rx_state_t {
     std::vector<chest_stats_t> prof;
     std::vector<chest_lut_t> lut0, lut_lr;
     int lut_eff = -1;
+    double nv_eff = 0.0;  // noise variance per RX cell at the latest LUT pick (MMSE regularisation)
     uint32_t ps_idx = 0, rel = 0, l_abs = 1, ts_first = 0, ts_last = 0;
     bool mode_lr = false;
     std::vector<drs_sym_t> drs;
@@ -593,6 +594,7 @@ struct rx_state_t {
             }
         }
         lut_eff = idx;
+        nv_eff = snr_N > 0 ? snr_N / static_cast<double>(snr_N_cnt) : 0.0;
     }
 
     // estimator_mimo_t::process_drs at the packet end (rx_synced.cpp:417-436,
@@ -710,10 +712,67 @@ struct rx_state_t {
         ++pcc_sym;
     }
 
+    // Spatial multiplexing (N_SS > 1, TM 2/4/6/8/9/11) -- absent from the reference RX
+    // (run_pdc_mode_AxA_MIMO, rx_synced.cpp:1331-1333 \todo), parity unpinned. Per PDC cell k the
+    // interpolated channel H[rx][ss] of every transmit stream (= spatial stream, tx.cpp:1051-1067),
+    // linear MMSE x = (H^H H + nv I)^-1 H^H y with nv the noise variance of the SNR estimator at the
+    // latest LUT pick (estimator_snr.cpp:104-146), unbiased per stream by
+    // beta_s = [(H^H H + nv I)^-1 H^H H]_ss = 1 - nv [(H^H H + nv I)^-1]_ss. Symbol s of cell j is
+    // spatial-stream symbol j N_SS + s. Double precision, Cholesky.
+    std::vector<cd> mmse(const std::vector<uint32_t>& kk) {
+        const uint32_t S = ps.tm.N_SS;
+        const auto& Y = stage[rel];
+        std::vector<cd> out(kk.size() * S);
+        for (size_t c = 0; c < kk.size(); ++c) {
+            const uint32_t k = kk[c];
+            cd G[8][8], z[8], Lm[8][8], Mi[8][8];
+            for (uint32_t s1 = 0; s1 < S; ++s1) {
+                z[s1] = 0;
+                for (uint32_t s2 = 0; s2 < S; ++s2) {
+                    cd g = 0;
+                    for (uint32_t a = 0; a < N_RX; ++a) g += std::conj(chest[a][s1][k]) * chest[a][s2][k];
+                    G[s1][s2] = g + (s1 == s2 ? cd(nv_eff, 0) : cd(0, 0));
+                }
+                for (uint32_t a = 0; a < N_RX; ++a) z[s1] += std::conj(chest[a][s1][k]) * Y[a][k];
+            }
+            for (uint32_t j = 0; j < S; ++j) {  // G = L L^H
+                double d = G[j][j].real();
+                for (uint32_t m = 0; m < j; ++m) d -= std::norm(Lm[j][m]);
+                Lm[j][j] = std::sqrt(std::max(d, 1e-300));
+                for (uint32_t i = j + 1; i < S; ++i) {
+                    cd v = G[i][j];
+                    for (uint32_t m = 0; m < j; ++m) v -= Lm[i][m] * std::conj(Lm[j][m]);
+                    Lm[i][j] = v / Lm[j][j].real();
+                }
+            }
+            for (uint32_t j = 0; j < S; ++j) {  // Mi = L^-1 (lower triangular)
+                Mi[j][j] = 1.0 / Lm[j][j].real();
+                for (uint32_t i = j + 1; i < S; ++i) {
+                    cd v = 0;
+                    for (uint32_t m = j; m < i; ++m) v += Lm[i][m] * Mi[m][j];
+                    Mi[i][j] = -v / Lm[i][i].real();
+                }
+            }
+            for (uint32_t s1 = 0; s1 < S; ++s1) {
+                // x = G^-1 z = Mi^H Mi z ; [G^-1]_ss = sum_m |Mi[m][s]|^2
+                cd x = 0;
+                double ginv = 0;
+                for (uint32_t m = s1; m < S; ++m) {
+                    cd w = 0;
+                    for (uint32_t q = 0; q <= m; ++q) w += Mi[m][q] * z[q];
+                    x += std::conj(Mi[m][s1]) * w;
+                    ginv += std::norm(Mi[m][s1]);
+                }
+                out[c * S + s1] = x / (1.0 - nv_eff * ginv);
+            }
+        }
+        return out;
+    }
+
     void pdc_collect(uint32_t l) {
         const auto& kk = pdc_k[l];
         if (kk.empty()) return;
-        const auto eq = combine(kk, pdc_idx);
+        const auto eq = ps.tm.N_SS > 1 ? mmse(kk) : combine(kk, pdc_idx);
         for (const auto& v : eq) emit_llr(v, ps.mcs.N_bps, out.pdc_llr, out.pdc_llr_f, bits_idx);
         pdc_idx += static_cast<uint32_t>(kk.size());
     }
@@ -725,7 +784,8 @@ struct rx_state_t {
         N_RX = in.N_RX;
         N_eff_TX = ps.tm.N_eff_TX;
         if (N_eff_TX > 4) throw std::runtime_error("oracle RX supports N_eff_TX <= 4");
-        if (ps.tm.N_SS > 1) throw std::runtime_error("spatial multiplexing not demodulated (rx_synced.cpp:1331)");
+        if (ps.tm.N_SS > 1 && !in.sm_mmse)
+            throw std::runtime_error("spatial multiplexing not demodulated (rx_synced.cpp:1331)");
         N_step = N_eff_TX <= 2 ? 5 : 10;
         ps_len = N_eff_TX <= 2 ? 6 : 11;
         Nf = dm.N_b_OCC + 1;

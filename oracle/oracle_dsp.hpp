@@ -29,6 +29,7 @@ struct rx_in_t {  // sync_report_t subset + HARQ scrambling parameters
     double cfo_rad;     // cfo_fractional_rad + cfo_integer_rad
     uint32_t network_id, plcf_type;
     const float* sync_rms = nullptr;  // sync_report_t::rms_array[8] (nullable)
+    bool sm_mmse = false;             // demodulate N_SS > 1 by MMSE (not in the reference, rx_synced.cpp:1331)
 };
 
 struct rx_out_t {

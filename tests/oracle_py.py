@@ -44,7 +44,7 @@ def lib():
         L.oracle_chest_lut.argtypes = [C.c_uint32] * 5 + [U32P, U32P, F32P, C.c_uint32]
         L.oracle_tx.argtypes = [U32P, U32P, U32P, F64P, U8P, U8P, F32P, C.c_uint32, C.c_int]
         L.oracle_rx.argtypes = [U32P, U32P, C.c_uint32, F32P, C.c_uint32, C.c_int64, C.c_double, C.c_uint32,
-                                C.c_uint32, I16P, I16P, C.c_void_p, C.c_void_p, F32P, C.c_int, C.c_void_p]
+                                C.c_uint32, I16P, I16P, C.c_void_p, C.c_void_p, F32P, C.c_int, C.c_void_p, C.c_int]
         L.oracle_loopback_timed.argtypes = [U32P, U32P, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
         L.oracle_loopback_timed.restype = C.c_double
         L.oracle_numerology.argtypes = [C.c_uint32, C.c_uint32, U32P, C.POINTER(C.c_double)]
@@ -113,9 +113,11 @@ def tx(cf, ps, pcc_d, pdc_d, S_slot, codebook=0, network_id=100, plcf_type=1, gi
     return out.view(np.complex64)[..., 0], n
 
 
-def rx(cf, ps, iq, fine_peak=0, cfo_rad=0.0, network_id=100, plcf_type=1, use_float=False, sync_rms=None):
-    """iq: complex64 [N_RX, S_in]; sync_rms: the sync report's rms_array (8 floats, optional).
-    Returns dict with int16/float LLRs and meta."""
+def rx(cf, ps, iq, fine_peak=0, cfo_rad=0.0, network_id=100, plcf_type=1, use_float=False, sync_rms=None,
+       sm_mmse=False):
+    """iq: complex64 [N_RX, S_in]; sync_rms: the sync report's rms_array (8 floats, optional);
+    sm_mmse: demodulate spatial multiplexing (N_SS > 1) by MMSE. Returns dict with int16/float LLRs
+    and meta."""
     sz = packet_sizes(ps)
     iq = np.ascontiguousarray(iq, dtype=np.complex64)
     n_rx, s_in = iq.shape
@@ -127,7 +129,7 @@ def rx(cf, ps, iq, fine_peak=0, cfo_rad=0.0, network_id=100, plcf_type=1, use_fl
     srms = None if sync_rms is None else np.ascontiguousarray(np.resize(np.asarray(sync_rms, np.float32), 8))
     r = lib().oracle_rx(cf, ps, n_rx, iq.view(np.float32).reshape(-1), s_in, int(fine_peak), float(cfo_rad),
                         network_id, plcf_type, pcc, pdc, pccf.ctypes.data, pdcf.ctypes.data, meta,
-                        int(use_float), srms.ctypes.data if srms is not None else None)
+                        int(use_float), srms.ctypes.data if srms is not None else None, int(sm_mmse))
     assert r == 0, r
     return dict(pcc_llr=pcc, pdc_llr=pdc, pcc_llr_f=pccf, pdc_llr_f=pdcf, rms=meta[:8].copy(),
                 cfo_fine=float(meta[8]), sto=float(meta[9]), snr_pcc=float(meta[10]), snr_pdc=float(meta[11]),

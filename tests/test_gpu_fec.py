@@ -26,7 +26,12 @@ LOOPS = {
     "1.1.1.A_mcs4": ((1, 1, 1, 2, 0, 4), (1, 1, 1, 1, 10, 9)),
     "u2b4_tm5_mcs6": ((2, 4, 1, 1, 5, 6), (2, 4, 4, 1, 10, 9)),
     "u2b4_mrc2_mcs3": ((2, 4, 1, 2, 0, 3), (2, 4, 2, 1, 10, 9)),
+    # spatial multiplexing, MMSE receiver (opt-in, DNRP_RX_MODE_SM_MMSE; not in the reference RX)
+    "u2b4_tm6_sm4_mcs4": ((2, 4, 1, 2, 6, 4), (2, 4, 4, 1, 10, 9)),
+    "u8b16_tm6_sm4_mcs4": ((8, 16, 1, 1, 6, 4), (8, 16, 4, 1, 10, 9)),
+    "u2b2_tm2_sm2_mcs6": ((2, 2, 1, 2, 2, 6), (2, 2, 2, 1, 10, 9)),
 }
+SM_TM = (2, 4, 6, 8, 9)  # transmission modes with N_SS > 1
 
 
 def _loop(name, snr_db, n=4, seed=1):
@@ -37,6 +42,9 @@ def _loop(name, snr_db, n=4, seed=1):
     phy = dnrp.Phy(u_max, b_max, ntx, os_min, L, M, max_batch=n)
     for nid in range(100, 106):
         phy.add_network_id(nid)
+    sm = ps_t[4] in SM_TM
+    if sm:
+        phy.set_rx_mode(phy.RX_MODE_SM_MMSE)
     ps = dnrp.psdef(*ps_t)
     sz = phy.packet_sizes(ps)
     S = sz["N_samples_packet_os_rs"]
@@ -46,6 +54,7 @@ def _loop(name, snr_db, n=4, seed=1):
     masks = [(i % 2, (i // 2) % 2) for i in range(n)]
     tbs = [rng.integers(0, 256, sz["N_TB_bits"] // 8, dtype=np.uint8) for _ in range(n)]
     fcfg = FE.fec_cfg(sz["N_TB_bits"], sz["N_bps"], sz["G"], Z=6144)
+    assert sz["N_TB_bits"] % 8 == 0
     pcc = np.stack([FE.pcc_encode(plcfs[i], plcf_types[i], *masks[i]) for i in range(n)])
     pdc = np.stack([FE.pdc_encode(fcfg, tbs[i]) for i in range(n)])
     dev = torch.device("cuda:0")
@@ -62,7 +71,11 @@ def _loop(name, snr_db, n=4, seed=1):
     for i in range(n):
         off = int(rng.integers(0, 32))
         cfo = rng.uniform(-1.5, 1.5) * 2 * np.pi / sz["N_b_DFT_os"]
-        windows.append(PF.channel(rng, iq_tx[i], ntx, S, off, cfo * M / L, snr_db))
+        H = None
+        if sm:  # spatial multiplexing: a random channel of condition number 2.5 (U diag V^H)
+            q = lambda: np.linalg.qr(rng.standard_normal((ntx, ntx)) + 1j * rng.standard_normal((ntx, ntx)))[0]
+            H = (q() @ np.diag(np.linspace(1.0, 0.4, ntx)) @ q().conj().T).astype(np.complex64)
+        windows.append(PF.channel(rng, iq_tx[i], ntx, S, off, cfo * M / L, snr_db, H=H))
         reports.append(dnrp.SyncReport(off, float(-cfo), 0.0, ps_t[0], ps_t[1], sz["N_eff_TX"]))
     iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(n, ntx, S, 2)).to(dev)
     pcc_llr = torch.zeros((n, 196), dtype=torch.int16, device=dev)
@@ -83,7 +96,7 @@ def _loop(name, snr_db, n=4, seed=1):
     res = []
     for i in range(n):
         r = O.rx(ocf, ops, windows[i], reports[i].fine_peak_time, float(np.float32(reports[i].cfo_fractional_rad)),
-                 100 + i, plcf_types[i])
+                 100 + i, plcf_types[i], sm_mmse=sm)
         for src, lp, ld in (("gpu", g_pcc[i], g_pdc[i]), ("oracle", r["pcc_llr"], r["pdc_llr"])):
             ok_c, got_plcf, cl, bf, _ = FE.pcc_decode(lp, plcf_types[i])
             ok_d, got_tb, _ = FE.pdc_decode(fcfg, ld)

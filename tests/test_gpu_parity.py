@@ -297,6 +297,60 @@ def test_rx_window_index_checked_by_c_abi():
     phy.sync()
 
 
+# Spatial multiplexing with the MMSE receiver (opt-in DNRP_RX_MODE_SM_MMSE; the reference RX has no
+# AxA MIMO, rx_synced.cpp:1331-1333, so the oracle's MMSE restatement is parity-unpinned):
+# name: psdef, ctx cfg, SNRs
+SM_CASES = {
+    "tm6_u2b4_16qam": ((2, 4, 1, 2, 6, 4), (2, 4, 4, 1, 10, 9), (20.0, 30.0)),
+    "tm6_u8b16_64qam": ((8, 16, 1, 1, 6, 6), (8, 16, 4, 1, 10, 9), (30.0,)),
+    "tm6_u8b16_256qam": ((8, 16, 1, 1, 6, 8), (8, 16, 4, 1, 10, 9), (40.0,)),
+    "tm2_sm2_u2b2": ((2, 2, 1, 2, 2, 6), (2, 2, 2, 1, 10, 9), (15.0, 30.0)),
+    "tm4_cl_sm2_u1b4": ((1, 4, 1, 2, 4, 3), (1, 4, 2, 1, 10, 9), (25.0,)),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SM_CASES))
+def test_rx_sm_mmse_parity(name):
+    """GPU MMSE (rx_cells_kernel<., ., true>) vs the oracle's double-precision MMSE on the same windows:
+    int16 LLRs within 1 LSB, SNR report within 0.05 dB; without the opt-in the PDC request is
+    DNRP_EUNSUPPORTED, as the reference's receiver declines N_SS > 1."""
+    import dnrp
+    rng = np.random.default_rng(17)
+    ps_t, cf, snrs = SM_CASES[name]
+    u_max, b_max, ntx, os_min, L, M = cf
+    phy = dnrp.Phy(u_max, b_max, ntx, os_min, L, M, max_batch=4)
+    for nid in range(100, 106):
+        phy.add_network_id(nid)
+    ps, ops, ocf = dnrp.psdef(*ps_t), O.psdef(*ps_t), O.cfg(u_max, b_max, os_min, L, M)
+    sz = phy.packet_sizes(ps)
+    assert sz["N_SS"] > 1
+    S = sz["N_samples_packet_os_rs"]
+    windows, reports, nids, types, _, pdc = _rx_windows(rng, name, phy, ps, ops, ocf, snrs)
+    n = len(windows)
+    dev = torch.device("cuda:0")
+    iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(n, ntx, S, 2)).to(dev)
+    pcc_llr = torch.zeros((n, 196), dtype=torch.int16, device=dev)
+    pdc_llr = torch.zeros((n, sz["G"]), dtype=torch.int16, device=dev)
+    reqs = [dnrp.PdcReq(ps, i, nids[i], types[i]) for i in range(n)]
+    phy.rx_pcc_batch(reports, iq, pcc_llr)
+    with pytest.raises(dnrp.DnrpError) as e:  # the reference receiver's behaviour by default
+        phy.rx_pdc_batch(reqs, iq, pdc_llr)
+    assert e.value.code == -3
+    phy.set_rx_mode(phy.RX_MODE_SM_MMSE)
+    rep1 = phy.rx_pcc_batch(reports, iq, pcc_llr, want_report=True)
+    rep2 = phy.rx_pdc_batch(reqs, iq, pdc_llr, want_report=True)
+    phy.sync()
+    g_pcc, g_pdc = pcc_llr.cpu().numpy(), pdc_llr.cpu().numpy()
+    for i in range(n):
+        r = O.rx(ocf, ops, windows[i], reports[i].fine_peak_time, float(np.float32(reports[i].cfo_fractional_rad)),
+                 nids[i], types[i], sm_mmse=True)
+        _check_rx((name, i), g_pcc[i], g_pdc[i], rep1[i], None, r)
+        assert abs(rep2[i].snr_dB - r["snr_pdc"]) < 0.05, (name, i)
+        if snrs[i] >= 30.0 and sz["N_bps"] <= 4:  # uncoded decisions; random flat H can be ill-conditioned
+            bits = np.unpackbits(pdc[i])[: sz["G"]]
+            assert np.mean(bits != (g_pdc[i] > 0)) < 5e-2, (name, i, np.mean(bits != (g_pdc[i] > 0)))
+
+
 def test_rx_tm10_unsupported():
     """N_eff_TX = 8 (device class 8.16.8.A): the reference receiver aborts on its l-mode LUT at the
     TS 4-7 DRS symbol; the boundary returns DNRP_EUNSUPPORTED instead of output."""
