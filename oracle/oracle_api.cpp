@@ -359,8 +359,8 @@ int oracle_rx(const uint32_t* cfg, const uint32_t* psdef, uint32_t N_RX, const f
 // (worker_tx_rx_t model). With sync_chunk > 0 each RX window holds the packet after sync_pre
 // hw samples and is synchronised first (sync_chunk_t::search, float path), RX starting at the
 // found fine peak. Returns wall seconds, or negative on error.
-double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_t n_packets, uint32_t n_threads,
-                             uint64_t seed, uint32_t sync_pre, uint32_t sync_chunk) {
+double oracle_loopback_timed2(const uint32_t* cfg, const uint32_t* psdef, uint32_t n_packets, uint32_t n_threads,
+                              uint64_t seed, uint32_t sync_pre, uint32_t sync_chunk, double* phase_s) {
     try {
         packet_sizes_t q;
         if (!get_packet_sizes(to_psdef(psdef), q)) return -1.0;
@@ -370,7 +370,9 @@ double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_
         const uint32_t S = dm.N_packet_os_rs;
         std::atomic<uint32_t> next{0};
         std::atomic<int> err{0};
+        std::vector<double> t_tx(n_threads, 0.0), t_rx(n_threads, 0.0);  // thread seconds per phase
         auto worker = [&](uint32_t tid) {
+            using clk = std::chrono::steady_clock;
             std::mt19937_64 rng(seed + tid);
             std::vector<uint8_t> pcc(25), pdc((q.G + 7) / 8);
             std::vector<float> iq(2ull * q.tm.N_TX * S);
@@ -383,7 +385,10 @@ double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_
                 d.network_id = 100 + i % 6;
                 d.plcf_type = 1 + i % 2;
                 std::vector<std::vector<std::complex<float>>> v;
+                const auto c0 = clk::now();
                 tx_packet<float>(c, q, d, pcc.data(), pdc.data(), v, S);
+                const auto c1 = clk::now();
+                t_tx[tid] += std::chrono::duration<double>(c1 - c0).count();
                 int64_t fine = 0;
                 if (sync_chunk) {
                     std::fill(iq.begin(), iq.end(), 0.0f);
@@ -410,6 +415,7 @@ double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_
                 rx_in_t in{iq.data(), q.tm.N_TX, S, fine, 0.0, d.network_id, d.plcf_type};
                 rx_out_t o;
                 rx_packet<float>(c, q, in, o);
+                t_rx[tid] += std::chrono::duration<double>(clk::now() - c1).count();  // sync + RX
                 if (o.pdc_llr.size() != q.G) err = 1;
             }
         };
@@ -419,10 +425,22 @@ double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_
         for (auto& t : th) t.join();
         const auto t1 = std::chrono::steady_clock::now();
         if (err) return -3.0 - err;
+        if (phase_s) {
+            phase_s[0] = phase_s[1] = 0.0;
+            for (uint32_t t = 0; t < n_threads; ++t) {
+                phase_s[0] += t_tx[t];
+                phase_s[1] += t_rx[t];
+            }
+        }
         return std::chrono::duration<double>(t1 - t0).count();
     } catch (...) {
         return -2.0;
     }
+}
+
+double oracle_loopback_timed(const uint32_t* cfg, const uint32_t* psdef, uint32_t n_packets, uint32_t n_threads,
+                             uint64_t seed, uint32_t sync_pre, uint32_t sync_chunk) {
+    return oracle_loopback_timed2(cfg, psdef, n_packets, n_threads, seed, sync_pre, sync_chunk, nullptr);
 }
 
 // Synchronisation of one window (= one chunk starting at iq[0]); reports in search order.

@@ -10,7 +10,8 @@ import subprocess
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+# ORACLE_LIB: another build of the same sources (bench.py's cpu_baseline builds one -march=native)
+LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(ROOT, "oracle", "liboracle.so")
 
 _lib = None
 
@@ -47,6 +48,9 @@ def lib():
                                 C.c_uint32, I16P, I16P, C.c_void_p, C.c_void_p, F32P, C.c_int, C.c_void_p, C.c_int]
         L.oracle_loopback_timed.argtypes = [U32P, U32P, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
         L.oracle_loopback_timed.restype = C.c_double
+        L.oracle_loopback_timed2.argtypes = [U32P, U32P, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                                             F64P]
+        L.oracle_loopback_timed2.restype = C.c_double
         L.oracle_numerology.argtypes = [C.c_uint32, C.c_uint32, U32P, C.POINTER(C.c_double)]
         L.oracle_tm_mode.argtypes = [C.c_uint32, U32P]
         L.oracle_mcs.argtypes = [C.c_uint32, U32P]
@@ -136,8 +140,14 @@ def rx(cf, ps, iq, fine_peak=0, cfo_rad=0.0, network_id=100, plcf_type=1, use_fl
                 mimo_N_TS_other=int(meta[12]), mimo_idx=int(meta[13]), mimo_idx_reciprocal=int(meta[14]))
 
 
-def loopback_timed(cf, ps, n_packets, n_threads, seed=0xDEC7, sync_pre=0, sync_chunk=0):
-    return lib().oracle_loopback_timed(cf, ps, n_packets, n_threads, seed, sync_pre, sync_chunk)
+def loopback_timed(cf, ps, n_packets, n_threads, seed=0xDEC7, sync_pre=0, sync_chunk=0, phases=False):
+    """wall seconds of n_packets TX + (sync +) RX slot-pairs on n_threads; phases=True also returns
+    the thread-seconds spent in TX and in sync + RX"""
+    if not phases:
+        return lib().oracle_loopback_timed(cf, ps, n_packets, n_threads, seed, sync_pre, sync_chunk)
+    ph = np.zeros(2)
+    t = lib().oracle_loopback_timed2(cf, ps, n_packets, n_threads, seed, sync_pre, sync_chunk, ph)
+    return t, float(ph[0]), float(ph[1])
 
 
 def pack_bits(bits):

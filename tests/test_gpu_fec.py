@@ -172,6 +172,59 @@ def test_gpu_turbo_decoder_matches_host():
     assert ok[0] and ok[1] and ok[2] and 1 <= n_fail <= m - 3
 
 
+def test_gpu_decoders_match_numpy_oracle():
+    """dnrp_pdc_decode_batch and dnrp_pcc_decode_batch against oracle/fec_np.py's numpy max-log-MAP
+    decoder (independent of the library's code; tests/test_fec_decoder_oracle.py holds the host
+    decoder to the same oracle): CRC verdict, iterations and bits, clean / marginal / failing inputs."""
+    import dnrp
+    import dnrp.fec as FE
+    import fec_np as ON
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import test_fec_decoder_oracle as TD
+    phy = dnrp.Phy(1, 1, 1, max_batch=8)
+    dev = torch.device("cuda:0")
+    cfgs, llrs, want = [], [], []
+    for tbs, Qm, G, rv, snr in TD.PDC_CASES:
+        while not TD._tbs_valid(tbs):
+            tbs += 8
+        rng = np.random.default_rng(tbs + G)
+        tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+        cfg = FE.fec_cfg(tbs, Qm, G, rv=rv)
+        llr = TD.noisy(np.unpackbits(FE.pdc_encode(cfg, tb))[:G], snr, rng)
+        cfgs.append(cfg)
+        llrs.append(llr)
+        want.append(ON.pdc_decode(llr, tbs, 6144, Qm, G, rv, TD.qpp_of))
+    m = len(cfgs)
+    buf = np.zeros((m, max(c.G for c in cfgs)), np.int16)
+    for i in range(m):
+        buf[i, : cfgs[i].G] = llrs[i]
+    tb_dev = torch.zeros((m, max(c.N_TB_bits for c in cfgs) // 8 + 3), dtype=torch.uint8, device=dev)
+    ok, it = FE.pdc_decode_batch(phy, cfgs, torch.from_numpy(buf).to(dev), tb_dev)
+    g_tb = tb_dev.cpu().numpy()
+    for i, (ok_o, bits_o, it_o) in enumerate(want):
+        assert (bool(ok[i]), int(it[i])) == (bool(ok_o), it_o), (TD.PDC_CASES[i], ok[i], it[i], ok_o, it_o)
+        assert np.array_equal(np.unpackbits(g_tb[i, : cfgs[i].N_TB_bits // 8]), bits_o), TD.PDC_CASES[i]
+    # PLCF: both types, the four CRC masks, clean / marginal / failing
+    rng = np.random.default_rng(77)
+    types, llr_p, want_p = [], [], []
+    for trial in range(8):
+        t = 1 + trial % 2
+        plcf = rng.integers(0, 256, 5 * t, dtype=np.uint8)
+        d = np.unpackbits(FE.pcc_encode(plcf, t, trial % 2, (trial // 2) % 2))[:196]
+        l = TD.noisy(d, (8.0, 0.0, -6.0)[trial % 3], rng)
+        types.append(t)
+        llr_p.append(l)
+        want_p.append(ON.pcc_decode(l, t, TD.qpp_of))
+    plcf_dev = torch.zeros((8, 10), dtype=torch.uint8, device=dev)
+    res, it = FE.pcc_decode_batch(phy, types, torch.from_numpy(np.stack(llr_p)).to(dev), plcf_dev)
+    got = plcf_dev.cpu().numpy()
+    for i, (ok_o, bits_o, m_o, it_o) in enumerate(want_p):
+        assert (bool(res[i] > 0), int(it[i])) == (bool(ok_o), it_o), (i, res[i], it[i], ok_o, it_o)
+        if ok_o:
+            assert res[i] == 1 + m_o[0] + 2 * m_o[1]
+            assert np.array_equal(np.unpackbits(got[i, : 5 * types[i]]), bits_o)
+
+
 def test_gpu_encoder_matches_host():
     """dnrp_pdc_encode_batch against dnrp_pdc_encode (itself bit-exact against the numpy oracle):
     mixed sizes, Z, modulation orders and redundancy versions in one call."""

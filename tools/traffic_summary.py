@@ -38,6 +38,14 @@ def main():
     os.makedirs(dst, exist_ok=True)
     with open(os.path.join(dst, "traffic.json"), "w") as fh:
         json.dump(res, fh, indent=1)
+    # SQ_INSTS_VALU per launch (summed over the launch's waves) -> valu.json (bench.py roofline_valu)
+    vpath = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
+    if os.path.exists(vpath):
+        valu = {k: [v / 1024.0 for v in vals] for k, vals in load(vpath, "SQ_INSTS_VALU").items()}
+        vres = {f"{k[0]}@grid{k[1]}": {"kernel": k[0], "grid": k[1], "valu_insts": sum(v) / len(v), "launches": len(v)}
+                for k, v in sorted(valu.items())}
+        with open(os.path.join(dst, "valu.json"), "w") as fh:
+            json.dump(vres, fh, indent=1)
     for k, v in res.items():
         print(f"{k:60s} fetch {v['fetch'] / 1e9:8.3f} GB  write {v['write'] / 1e9:8.3f} GB")
 
