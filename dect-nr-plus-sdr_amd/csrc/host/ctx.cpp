@@ -645,7 +645,6 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     const uint32_t K_max = wave ? 7u : 3u;  // wave path: one wavefront per symbol slot, <= 8 slots
     const uint32_t K = (K_env >= 1 && static_cast<uint32_t>(K_env) <= K_max) ? static_cast<uint32_t>(K_env) : (wave ? 6u : 3u);
     a.K = K;
-    a.dbg = std::getenv("DNRP_TX_DBG") ? static_cast<uint32_t>(std::atoi(std::getenv("DNRP_TX_DBG"))) : 0u;
     a.n_runs = (t->q.N_DF_symb + 1 + K - 1) / K;
     a.m_star = 0;
     while ((t->rs.delay + a.m_star * t->rs.M) % t->rs.L) ++a.m_star;
@@ -704,6 +703,10 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
         const int64_t mfirst0 = int64_t(a.m_star) + 10 * qlo0;
         if (fits) {
             a.stream = 1;
+            // polyphase blocks on the matrix cores (tx.hip, polyphase.hpp mf_blocks): opt-in A/B,
+            // DNRP_TX_MFMA=1 (read per call); the VALU blocks measured faster
+            const char* mf_env = std::getenv("DNRP_TX_MFMA");
+            a.mfma = (mf_env && std::atoi(mf_env)) ? 1u : 0u;
             a.code_bin = t->code_bin.as<uint32_t>();
             a.pcc_syms = t->pcc_syms;
             a.n_pieces = static_cast<uint32_t>((int64_t(a.n_keep) - mfirst0 + 1279) / 1280);

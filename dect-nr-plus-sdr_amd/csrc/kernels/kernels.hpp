@@ -40,7 +40,7 @@ struct tx_args {
     // before them (resampler history) into a linear cyclic-prefixed buffer of lin_len samples
     uint32_t K, n_runs, HP, lin_len, bufB_len;
     uint32_t stage_bytes;  // PDC source bytes of one run staged in LDS (0: read HBM directly)
-    uint32_t dbg;          // TEMP: section-skip mask for profiling
+    uint32_t mfma;         // streaming kernel: polyphase blocks on the matrix cores (split fp16)
     uint32_t pair[12];     // transmit diversity TS pairs, A | B << 4
     const uint32_t* code;
     const uint32_t* pdc_off;  // [N_DF+2] first PDC cell of each symbol

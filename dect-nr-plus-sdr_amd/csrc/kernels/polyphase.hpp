@@ -161,3 +161,65 @@ struct pp_const {
 };
 
 }  // namespace dnrp::dev
+
+namespace dnrp::dev {
+
+// ---- polyphase blocks on the matrix cores (split fp16, three passes)
+// 16 polyphase blocks of L outputs as one v_mfma_f32_16x16x32_f16 per pass and component:
+//   C[q][c] = sum_i X[q][i] G[i][c],  X[q][i] = window input i of block q (16 x 32), G = the block
+//   taps (32 x 16: G[i][c] = h[ph_c + (HL + o_c - i) L] inside output c's FIR span, else 0).
+// Every f32 operand is split into fp16 hi + lo (x = hi + lo to ~2^-20 relative, hi rounded toward
+// zero); the product keeps hi*hi + hi*lo + lo*hi (the dropped lo*lo is ~2^-20 of it), accumulated in
+// f32 -- about 1e-6 relative against the f32 FMA chain of pp_direct. The window samples are stored as
+// split words in the block's LDS buffer: slot s = {HI = (re_hi, im_hi), LO = (re_lo, im_lo)} in the
+// 8 bytes a float2 takes, so the buffer keeps its layout.
+// Lane l: A rows (blocks) l & 15, k = 8 (l >> 4) + j (j = 0..7); B rows k, column (output) l & 15;
+// C column l & 15, rows 4 (l >> 4) + r (MI355X guide, 16x16x32 operand / accumulator maps).
+typedef _Float16 mf_h8 __attribute__((ext_vector_type(8)));
+typedef __fp16 mf_h2 __attribute__((ext_vector_type(2)));  // v_cvt_pkrtz_f16_f32 result
+typedef float mf_f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t mf_u2 __attribute__((ext_vector_type(2)));
+typedef uint32_t mf_u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint2 mf_split(float2 v) {  // -> {HI, LO} words of one complex sample
+    const mf_h2 hi = __builtin_amdgcn_cvt_pkrtz(v.x, v.y);
+    const mf_h2 lo = __builtin_amdgcn_cvt_pkrtz(v.x - static_cast<float>(hi.x), v.y - static_cast<float>(hi.y));
+    return make_uint2(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo));
+}
+
+// A operands of one lane: 8 consecutive split slots s[0..7] -> (re_hi, im_hi, re_lo, im_lo) half8 each
+__device__ __forceinline__ void mf_operands(const uint2 (&s)[8], mf_h8& rh, mf_h8& ih, mf_h8& rl, mf_h8& il) {
+    uint4 a, b, c, d;
+    uint32_t* pa = &a.x;
+    uint32_t* pb = &b.x;
+    uint32_t* pc = &c.x;
+    uint32_t* pd = &d.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint2 s0 = s[2 * j], s1 = s[2 * j + 1];
+        pa[j] = __builtin_amdgcn_perm(s1.x, s0.x, 0x05040100u);  // re_hi of samples 2j, 2j+1
+        pb[j] = __builtin_amdgcn_perm(s1.x, s0.x, 0x07060302u);  // im_hi
+        pc[j] = __builtin_amdgcn_perm(s1.y, s0.y, 0x05040100u);  // re_lo
+        pd[j] = __builtin_amdgcn_perm(s1.y, s0.y, 0x07060302u);  // im_lo
+    }
+    rh = __builtin_bit_cast(mf_h8, a);
+    ih = __builtin_bit_cast(mf_h8, b);
+    rl = __builtin_bit_cast(mf_h8, c);
+    il = __builtin_bit_cast(mf_h8, d);
+}
+
+// 16 blocks: w = the lane's 8 window slots (block l & 15, window inputs 8 (l >> 4) ..), gh / gl =
+// the lane's taps (hi / lo). Returns the real and imaginary accumulators (C rows 4 (l >> 4) + r).
+__device__ __forceinline__ void mf_blocks(const uint2 (&w)[8], const mf_h8& gh, const mf_h8& gl, mf_f4& cr, mf_f4& ci) {
+    mf_h8 rh, ih, rl, il;
+    mf_operands(w, rh, ih, rl, il);
+    const mf_f4 z = {0.f, 0.f, 0.f, 0.f};
+    cr = __builtin_amdgcn_mfma_f32_16x16x32_f16(rh, gh, z, 0, 0, 0);
+    ci = __builtin_amdgcn_mfma_f32_16x16x32_f16(ih, gh, z, 0, 0, 0);
+    cr = __builtin_amdgcn_mfma_f32_16x16x32_f16(rh, gl, cr, 0, 0, 0);
+    ci = __builtin_amdgcn_mfma_f32_16x16x32_f16(ih, gl, ci, 0, 0, 0);
+    cr = __builtin_amdgcn_mfma_f32_16x16x32_f16(rl, gh, cr, 0, 0, 0);
+    ci = __builtin_amdgcn_mfma_f32_16x16x32_f16(il, gh, ci, 0, 0, 0);
+}
+
+}  // namespace dnrp::dev

@@ -23,6 +23,21 @@
 namespace dnrp::dev {
 
 __constant__ float k_cover[9] = DNRP_STF_COVER_SEQUENCE;  // stf.hpp:146-151 (params.hpp)
+// the same sequence as a sign mask (bit q: entry q is -1), for the streaming kernel: no vector load
+constexpr uint32_t cover_neg_mask() {
+    constexpr float cv[9] = DNRP_STF_COVER_SEQUENCE;
+    uint32_t mk = 0;
+    for (int q = 0; q < 9; ++q) mk |= (cv[q] < 0.f ? 1u : 0u) << q;
+    return mk;
+}
+constexpr bool cover_is_sign() {
+    constexpr float cv[9] = DNRP_STF_COVER_SEQUENCE;
+    for (int q = 0; q < 9; ++q)
+        if (cv[q] != 1.f && cv[q] != -1.f) return false;
+    return true;
+}
+static_assert(cover_is_sign(), "cover sequence entries are +-1");
+__device__ __forceinline__ float cover_sign(uint32_t q) { return ((cover_neg_mask() >> q) & 1u) ? -1.f : 1.f; }
 
 constexpr uint32_t TX_THREADS = 256;     // block-FFT path workgroup
 constexpr uint32_t TX_WAVE_MAX = 512;    // wave path: one wavefront per symbol slot, 64 (K + 1) threads
@@ -377,20 +392,15 @@ __global__ void __launch_bounds__(TX_WAVE_MAX) tx_kernel_wave(tx_args A) {
     __syncthreads();
     if (b < w.nsl) {
         float2 v[16];
-        if (A.dbg & 1) {
 #pragma unroll
-            for (int m = 0; m < 16; ++m) v[m] = make_float2(__uint_as_float(rc[m]), 0.f);
-        } else {
-#pragma unroll
-            for (int m = 0; m < 16; ++m) v[m] = w.bin(rc[m], lane + 64 * m, l);
-        }
+        for (int m = 0; m < 16; ++m) v[m] = w.bin(rc[m], lane + 64 * m, l);
         float2* xb = w.slot(l);  // the symbol's own slot (>= 1152 samples) is the exchange buffer
-        if (!(A.dbg & 2)) wave_fft1024<+1>(v, xb, w.twl, lane);
+        wave_fft1024<+1>(v, xb, w.twl, lane);
         __builtin_amdgcn_wave_barrier();
         w.put_symbol(l, v, lane);
     }
     __syncthreads();
-    if (!(A.dbg & 4)) tx_resample<LR, MR, HLR>(w);
+    tx_resample<LR, MR, HLR>(w);
 }
 
 // ---- streaming TX: N_b_DFT_os = 1024, L/M = 10/9 (os_min 1), CP 128, STF CP 1280.
@@ -405,15 +415,23 @@ __global__ void __launch_bounds__(TX_WAVE_MAX) tx_kernel_wave(tx_args A) {
 constexpr uint32_t TXS_WPG = 4;
 constexpr uint32_t TXS_PIECE = 1152;                  // input samples per piece = 128 blocks of 9
 constexpr uint32_t TXS_CARRY = 30;                    // inputs before the piece its first window reads
-constexpr uint32_t TXS_BUF = TXS_CARRY + TXS_PIECE;   // float2 per wave
+// float2 per wave: carry + piece + 2 pad slots (zero; the matrix-core blocks read 32 window inputs,
+// the last block one slot past the piece, with a zero tap)
+constexpr uint32_t TXS_BUF = TXS_CARRY + TXS_PIECE + 2;
 constexpr uint32_t TXS_XB = 32;                       // FFT exchange / PDC byte staging offset
 constexpr uint32_t TXS_WROW = 12;                     // beamforming row (8) + descrambled PCC bytes (32 B)
-static_assert(TXS_XB + WFFT_XB <= TXS_BUF, "FFT exchange buffer must fit behind the carry");
+static_assert(TXS_XB + WFFT_XB <= TXS_CARRY + TXS_PIECE, "FFT exchange buffer must fit behind the carry");
 
 enum { TXS_SISO = 0, TXS_TXDIV = 1, TXS_SM = 2 };
 
 __device__ __forceinline__ uint32_t txs_sym(uint32_t r, uint32_t N_DF) {  // symbol of piece r (N_DF+1: none)
     return r <= 1 ? 0u : (r - 1 <= N_DF ? r - 1 : N_DF + 1);
+}
+
+template <bool MF>
+__device__ __forceinline__ float2 txs_slot(float2 v) {  // buffer slot of a piece sample (MF: split fp16 words)
+    if constexpr (MF) return __builtin_bit_cast(float2, mf_split(v));
+    else return v;
 }
 
 struct txs_wave {
@@ -427,22 +445,28 @@ struct txs_wave {
 
     // first staged byte of symbol l (16-B aligned), PDC cells from pdc_off[l] & ~1 (SFBC partners)
     __device__ uint32_t stage_base(uint32_t l) const {
-        const uint32_t j0 = A->pdc_off[l] & ~1u;
+        // l is wave-uniform: a scalar load (constant address space), no vector-memory wait
+        const uint32_t j0 = reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(reinterpret_cast<uintptr_t>(A->pdc_off))[l] & ~1u;
         return ((j0 * A->N_SS * A->N_bps) >> 3) & ~15u;
     }
-    // raw 16-B chunk of the descrambled PDC bytes at byte g (zero beyond the packet)
-    __device__ uint4 chunk(uint32_t g) const {
+    // 16-B chunk of the descrambled PDC bytes at byte g (zero beyond the packet) as the d-bit and
+    // Gold-sequence words, XORed where they are used: the loads are a prefetch, not waited for here
+    __device__ void chunk(uint32_t g, uint4& d, uint4& c) const {
         if (g + 16 <= pdc_bytes) {
             // the d-bit rows need not be 16-B aligned (byte stride): one unaligned dwordx4 load
-            uint4 d;
             __builtin_memcpy(&d, dpdc + g, 16);
-            const uint4 c = *reinterpret_cast<const uint4*>(cpdc + g);
-            return make_uint4(d.x ^ c.x, d.y ^ c.y, d.z ^ c.z, d.w ^ c.w);
+            // the Gold row is 16-B aligned device memory: a global (not flat) load, so it retires in the
+            // vector-memory counter alone
+            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+            const u4v cv = *reinterpret_cast<const __attribute__((address_space(1))) u4v*>(reinterpret_cast<uintptr_t>(cpdc + g));
+            c = make_uint4(cv.x, cv.y, cv.z, cv.w);
+            return;
         }
         uint32_t w[4] = {0u, 0u, 0u, 0u};
         for (uint32_t i = 0; i < 16; ++i)
             if (g + i < pdc_bytes) w[i >> 2] |= uint32_t(dpdc[g + i] ^ cpdc[g + i]) << (8 * (i & 3));
-        return make_uint4(w[0], w[1], w[2], w[3]);
+        d = make_uint4(w[0], w[1], w[2], w[3]);
+        c = make_uint4(0u, 0u, 0u, 0u);
     }
     // branch-free cell values: every source is read unconditionally at an in-bounds (masked)
     // index and the code type selects the result, so 16 bins per lane cost no divergent control
@@ -499,7 +523,44 @@ struct txs_wave {
     }
 };
 
-template <int LR, int MR, int HLR, int MODE, bool Q8>
+// Outputs m0 .. m0 + N - 1, staged in buf[0, N), to the wave's output row as contiguous 16-B lane
+// stores of the output pairs (m, m + 1), m even (so no pair straddles 0 or S, both even); with an
+// odd m0 the first and last output go alone. Branch-free: lanes out of [0, S) store past the
+// descriptor's range (dropped by the hardware) and outputs >= n_keep are zero, so every call issues
+// the same stores -- the next piece's input waits stay counted (vmcnt(n)), not a drain of them.
+// inner (uniform): [m0, m0 + N) inside [0, n_keep), no per-element range work.
+template <int N>
+__device__ __forceinline__ void txs_emit(const float2* buf, __amdgpu_buffer_rsrc_t orsrc, uint32_t head, uint32_t lid,
+                                         int m0, int S, int n_keep) {
+    constexpr int K = (N / 2 + 63) / 64;
+    const bool inner = m0 >= 0 && m0 + N <= n_keep;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t e = head + 2 * (lid + 64 * k);  // local output pair (e, e + 1)
+        const uint32_t ec = min(e, static_cast<uint32_t>(N - 2));
+        const float2 a = buf[ec], b = buf[ec + 1];
+        const int m = m0 + static_cast<int>(e);
+        mf_u4 v = {__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(b.x), __float_as_uint(b.y)};
+        uint32_t off = static_cast<uint32_t>(m) * 8u;
+        if ((k + 1) * 128 >= N || !inner) {  // the last store (partly filled with an odd m0), or a packet edge
+            const bool ok = e <= static_cast<uint32_t>(N - 2) && m >= 0 && m < S;
+            const bool ka = m < n_keep, kb = m + 1 < n_keep;
+            v = mf_u4{ka ? v.x : 0u, ka ? v.y : 0u, kb ? v.z : 0u, kb ? v.w : 0u};
+            off = ok ? off : 0x80000000u;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off, 0, 0);
+    }
+    {  // odd m0: the first and last output alone (lanes 0, 1)
+        const uint32_t e = lid == 0 ? 0u : static_cast<uint32_t>(N - 1);
+        const float2 a = buf[e];
+        const int m = m0 + static_cast<int>(e);
+        const bool ok = head && lid < 2 && m >= 0 && m < S;
+        const float2 ov = m < n_keep ? a : make_float2(0.f, 0.f);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mf_u2, ov), orsrc, ok ? static_cast<uint32_t>(m) * 8u : 0x80000000u, 0, 0);
+    }
+}
+
+template <int LR, int MR, int HLR, int MODE, bool Q8, bool MF>
 #ifndef DNRP_TX_WPE
 #define DNRP_TX_WPE 4  // waves per SIMD (5: 96 VGPRs + 120 B/lane of spills)
 #endif
@@ -552,14 +613,62 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
     const float2 step1 = T.P.do_mix ? phasor(T.P.inc) : make_float2(1.f, 0.f);
     // the FFT's two lane twiddles, loaded once (wave_fft1024_rt)
     const float2 tw1 = wfft_tw<+1>(A.tw, 4 * (lane & 15u)), twl = wfft_tw<+1>(A.tw, lane);
+    // MF: the lane's block taps for the matrix cores (polyphase.hpp mf_blocks), split fp16 hi / lo:
+    // B[i = 8 (lane >> 4) + j][c = lane & 15] = h[ph_c + (HL + o_c - i) L] inside output c's span
+    mf_h8 gh, gl;
+    float2 step10 = make_float2(1.f, 0.f), step160 = step10;
+    if constexpr (MF) {
+        const uint32_t c = lane & 15u, hq = lane >> 4;
+        const int o = static_cast<int>(MR * c) / LR, ph = static_cast<int>(MR * c) % LR;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int d = HLR + o - static_cast<int>(8 * hq) - j;
+            const float t = (c < LR && d >= 0 && d <= HLR) ? A.taps[ph + d * LR] : 0.f;
+            const mf_h2 hv = __builtin_amdgcn_cvt_pkrtz(t, 0.f);
+            gh[j] = hv.x;
+            gl[j] = __builtin_amdgcn_cvt_pkrtz(t - static_cast<float>(hv.x), 0.f).x;
+        }
+        if (T.P.do_mix) {
+            step10 = phasor(10.0 * T.P.inc);
+            step160 = phasor(160.0 * T.P.inc);
+        }
+        if (lane < 2) buf[TXS_CARRY + TXS_PIECE + lane] = make_float2(0.f, 0.f);
+    }
     if (seg == 0)  // outputs before piece 0's first block see only zero input
         for (int m = lane; m < mfirst0; m += 64) out[m] = make_float2(0.f, 0.f);
     const uint32_t r_start = r_a > 0 ? r_a - 1 : 0;
+    // the wave's output row as a buffer: out-of-range offsets are dropped by the range check
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, static_cast<int>(A.S * 8u), 0x00020000);
     if (r_a == 0 && lane < TXS_CARRY) buf[lane] = make_float2(0.f, 0.f);
     // PDC bytes of the first symbol
     const uint32_t l_cur = txs_sym(r_start, A.N_DF);
-    uint4 pre = make_uint4(0u, 0u, 0u, 0u);
-    if (l_cur >= 1 && l_cur <= A.N_DF) pre = T.chunk(T.stage_base(l_cur) + 16 * lane);
+    uint4 pre = make_uint4(0u, 0u, 0u, 0u), prc = pre;
+    if (l_cur >= 1 && l_cur <= A.N_DF) T.chunk(T.stage_base(l_cur) + 16 * lane, pre, prc);
+    // cell codes of the piece's 16 bins per lane, loaded one piece ahead: issued before the piece's
+    // output stores, so waiting for them never waits for those stores (vmcnt retires in order)
+    uint32_t cd[16];
+    auto load_codes = [&](uint32_t rr, uint32_t ln) {
+        const uint32_t ls = txs_sym(rr, A.N_DF);
+        const uint32_t* crow = A.code_bin + size_t(min(ls, A.N_DF)) * 1024;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) cd[m] = crow[ln + 64 * m];
+    };
+    load_codes(r_start, lane);
+    // the next piece's inputs (cell codes, PDC bytes of its symbol), issued once the FFT is done:
+    // pre / prc / cd are redefined on every path here, so none of them is live across the FFT
+    auto prefetch_next = [&](uint32_t r, uint32_t lid) {
+        load_codes(r + 1, lid);
+        const uint32_t l = txs_sym(r, A.N_DF), ln = txs_sym(r + 1, A.N_DF);
+        if (r + 1 < r_b && ln != l && ln >= 1 && ln <= A.N_DF) {
+            T.chunk(T.stage_base(ln) + 16 * lid, pre, prc);
+        } else {
+            pre = make_uint4(0u, 0u, 0u, 0u);
+            prc = pre;
+        }
+    };
+    // drain the prologue's loads: the loop header then sees only the back edge's pending loads and
+    // stores, and the code-row wait stays counted (the in-loop loads precede the piece's stores)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     for (uint32_t r = r_start; r < r_b; ++r) {
         // lid index opaque per piece: lid-dependent addresses are recomputed in the loop instead of
         // being hoisted out of it as dozens of 64-bit VGPR pairs (loop-invariant code motion)
@@ -571,13 +680,7 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
         if (real) {
             // stage this symbol's bytes, prefetch the next symbol's
             const uint32_t ab = (l >= 1) ? T.stage_base(l) : 0u;
-            if (l >= 1) reinterpret_cast<uint4*>(sb)[lid] = pre;
-            const uint32_t ln = txs_sym(r + 1, A.N_DF);
-            if (r + 1 < r_b && ln != l && ln >= 1 && ln <= A.N_DF) pre = T.chunk(T.stage_base(ln) + 16 * lid);
-            uint32_t cd[16];
-            const uint32_t* crow = A.code_bin + size_t(l) * 1024;
-#pragma unroll
-            for (int m = 0; m < 16; ++m) cd[m] = crow[lid + 64 * m];
+            if (l >= 1) reinterpret_cast<uint4*>(sb)[lid] = make_uint4(pre.x ^ prc.x, pre.y ^ prc.y, pre.z ^ prc.z, pre.w ^ prc.w);
             __builtin_amdgcn_wave_barrier();
             if (l == 0) {
 #pragma unroll
@@ -602,8 +705,9 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
             if (l >= 1) {  // DF symbol (CP 128): sample nn + 128, CP copies of the last 128 (m >= 14)
 #pragma unroll
                 for (int m = 0; m < 16; ++m) {
-                    buf[TXS_CARRY + 128 + lid + 64 * m] = v[m];
-                    if (m >= 14) buf[TXS_CARRY + lid + 64 * (m - 14)] = v[m];
+                    const float2 sv = txs_slot<MF>(v[m]);
+                    buf[TXS_CARRY + 128 + lid + 64 * m] = sv;
+                    if (m >= 14) buf[TXS_CARRY + lid + 64 * (m - 14)] = sv;
                 }
             } else {  // STF (CP 1280, covered): piece r holds samples [1152 r, 1152 r + 1152)
                 const uint32_t cp = A.STF_CP, len = cp + 1024, i0 = r == 1 ? TXS_PIECE : 0u;
@@ -611,7 +715,7 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
                 for (int m = 0; m < 16; ++m) {
                     const uint32_t nn = lid + 64 * m;
                     for (uint32_t i = (nn + cp) & 1023u; i < len; i += 1024)
-                        if (i - i0 < TXS_PIECE) buf[TXS_CARRY + i - i0] = cscale(v[m], k_cover[min(i / A.pattern_len, 8u)]);
+                        if (i - i0 < TXS_PIECE) buf[TXS_CARRY + i - i0] = txs_slot<MF>(cscale(v[m], cover_sign(min(i / A.pattern_len, 8u))));
                 }
             }
         } else {
@@ -619,7 +723,61 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
         }
         __builtin_amdgcn_wave_barrier();
         float2 creg = make_float2(0.f, 0.f);
-        if (r >= r_a) {
+        if (MF && r >= r_a) {
+            // 8 groups of 16 blocks on the matrix cores (lane: output phase c = lid & 15 of blocks
+            // 16 g + 4 (lid >> 4) + q, phases >= 10 idle), each group's 160 outputs transposed through
+            // LDS slots [0, 160) -- dead once the windows of group 1 are read (they start at slot
+            // base0 + 144) -- into contiguous 16-B lane stores: group 0 is staged after group 1 is computed
+            const uint32_t c = lid & 15u, hq = lid >> 4;
+            const uint2* slots = reinterpret_cast<const uint2*>(buf) + base0 + MR * c + 8 * hq;
+            const int mrow = mfirst0 + static_cast<int>(1280 * r);
+            const int mb = mrow + static_cast<int>(40 * hq + c);
+            const uint32_t head = static_cast<uint32_t>(mfirst0) & 1u;  // pairs start at even outputs
+            float2 rot = make_float2(1.f, 0.f);
+            if (T.P.do_mix) rot = phasor(T.P.ph0 + static_cast<double>(mb) * T.P.inc);
+            prefetch_next(r, lid);
+            auto group = [&](int g, float2 (&y)[4]) {
+                uint2 w[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) w[j] = slots[MR * 16 * g + j];
+                mf_f4 cr, ci;
+                mf_blocks(w, gh, gl, cr, ci);
+                float2 rr = rot;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    y[q] = make_float2(cr[q], ci[q]);
+                    if (T.P.do_mix) {
+                        y[q] = cmul(y[q], rr);
+                        rr = cmul(rr, step10);
+                    }
+                }
+                if (T.P.do_mix) rot = cmul(rot, step160);
+            };
+            // branch-free stores: out-of-range lanes get an offset past the descriptor's range, which
+            // the hardware drops -- a fixed store count per piece, so the next piece's input waits are
+            // counted ones (vmcnt(n)), not a drain of this piece's stores
+            auto stage = [&](int g, const float2 (&y)[4]) {
+                if (c < LR) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) buf[10 * (4 * hq + q) + c] = y[q];
+                }
+                __builtin_amdgcn_wave_barrier();
+                txs_emit<160>(buf, orsrc, head, lid, mrow + 160 * g, static_cast<int>(A.S), static_cast<int>(A.n_keep));
+                __builtin_amdgcn_wave_barrier();
+            };
+            // one group ahead: group g + 1's matrix work is in flight while group g is staged (and
+            // group 0 waits for group 1's windows to be read before its slots are reused)
+            float2 y0[4], y1[4];
+            group(0, y0);
+#pragma unroll
+            for (int g = 0; g < 8; g += 2) {
+                group(g + 1, y1);
+                stage(g, y0);
+                if (g + 2 < 8) group(g + 2, y0);
+                stage(g + 1, y1);
+            }
+            if (lid < TXS_CARRY) creg = buf[TXS_PIECE + lid];
+        } else if (r >= r_a) {
             float2 y[2][LR];
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
@@ -637,6 +795,7 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
                     }
                 }
             }
+            prefetch_next(r, lid);
             __builtin_amdgcn_wave_barrier();
             if (lid < TXS_CARRY) creg = buf[TXS_PIECE + lid];
             __builtin_amdgcn_wave_barrier();
@@ -645,32 +804,15 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
 #pragma unroll
                 for (int k = 0; k < LR; ++k) buf[LR * lid + k] = y[b][k];
                 __builtin_amdgcn_wave_barrier();
-                const int m0 = mfirst0 + static_cast<int>(1280 * r) + 640 * b;
-                if (m0 >= 0 && m0 + 640 <= static_cast<int>(A.n_keep)) {
-                    // contiguous 16-B lid stores (the row base is 16-B aligned, host-checked)
-                    const uint32_t head = static_cast<uint32_t>(m0) & 1u;
-                    if (lid == 0 && head) out[m0] = buf[0];
-                    float4* o4 = reinterpret_cast<float4*>(out + m0 + head);
-#pragma unroll
-                    for (int i = 0; i < 5; ++i) {
-                        const uint32_t e = lid + 64 * i;
-                        if (e < (640 - head) / 2) {
-                            const float2 p0 = buf[head + 2 * e], p1 = buf[head + 2 * e + 1];
-                            o4[e] = make_float4(p0.x, p0.y, p1.x, p1.y);
-                        }
-                    }
-                    if (lid == 0 && head) out[m0 + 639] = buf[639];
-                } else {
-                    for (int i = lid; i < 640; i += 64) {
-                        const int m = m0 + i;
-                        if (m >= 0 && m < static_cast<int>(A.S))
-                            out[m] = m < static_cast<int>(A.n_keep) ? buf[i] : make_float2(0.f, 0.f);
-                    }
-                }
+                txs_emit<640>(buf, orsrc, static_cast<uint32_t>(mfirst0) & 1u, lid, mfirst0 + static_cast<int>(1280 * r) + 640 * b,
+                              static_cast<int>(A.S), static_cast<int>(A.n_keep));
                 __builtin_amdgcn_wave_barrier();
             }
-        } else if (lid < TXS_CARRY) {
-            creg = buf[TXS_PIECE + lid];
+        } else {  // the history piece ahead of the segment: nothing to store
+            prefetch_next(r, lid);
+            // drained here so the loop header's merge keeps the storing path's counted wait
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            if (lid < TXS_CARRY) creg = buf[TXS_PIECE + lid];
         }
         __builtin_amdgcn_wave_barrier();
         if (lid < TXS_CARRY) buf[lid] = creg;
@@ -738,7 +880,11 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
         const uint64_t waves = uint64_t(n) * a.N_TX * a.n_seg;
         const dim3 g(static_cast<uint32_t>((waves + TXS_WPG - 1) / TXS_WPG)), b(64 * TXS_WPG);
         const int mode = a.N_TS == 1 ? TXS_SISO : a.txdiv ? TXS_TXDIV : TXS_SM;
-#define DNRP_TXS(MODE, Q8) hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8>), g, b, tx_stream_lds(), st, a, n)
+#define DNRP_TXS(MODE, Q8)                                                                                       \
+    do {                                                                                                         \
+        if (a.mfma) hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8, true>), g, b, tx_stream_lds(), st, a, n);   \
+        else hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8, false>), g, b, tx_stream_lds(), st, a, n); \
+    } while (0)
         if (a.N_bps == 8) {
             if (mode == TXS_SISO) DNRP_TXS(TXS_SISO, true);
             else if (mode == TXS_TXDIV) DNRP_TXS(TXS_TXDIV, true);

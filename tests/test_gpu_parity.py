@@ -93,6 +93,15 @@ def test_tx_parity(name):
         _check_tx(iq[i], ref, sz, S, n_tx, (name, i))
 
 
+@pytest.mark.parametrize("name", sorted(TX_CASES))
+def test_tx_parity_matrix_blocks(name, monkeypatch):
+    """The streaming TX kernel's opt-in matrix-core polyphase blocks (DNRP_TX_MFMA=1: split-fp16
+    v_mfma_f32_16x16x32_f16, polyphase.hpp mf_blocks) against the same oracle and tolerance;
+    configurations outside the streaming kernel's geometry ignore the switch."""
+    monkeypatch.setenv("DNRP_TX_MFMA", "1")
+    test_tx_parity(name)
+
+
 @pytest.mark.parametrize("name,cb", [("tm5_u2b4", 3), ("tm2_sm2", 1), ("C4", 0)])
 def test_tx_optimal_scaling_dac(name, cb):
     """tx_meta_t::optimal_scaling_DAC (tx.cpp:582-592): W_t::scaling_factor_optimal_DAC instead of
