@@ -274,6 +274,7 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
     std::vector<float2> stfv(t->maps.Nf);
     for (uint32_t k = 0; k < t->maps.Nf; ++k) stfv[k] = make_float2(t->maps.stf[k].real(), t->maps.stf[k].imag());
     const auto plan = geo::build_rx_plan(t->maps, pcc_ops, N_eff_TX);
+    t->drs_arith = geo::drs_tables_arithmetic(t->maps);
     bool ok = t->stf.upload(stfv) && t->tw.upload(twiddles(t->Nd)) && t->taps.upload(t->rs.h) && t->taps_pp.upload(taps_polyphase(t->rs, &t->npp)) &&
               t->drs_k.upload(t->maps.drs_k) && t->drs_v.upload(t->maps.drs_v) && t->pcc_k.upload(t->maps.pcc_k) &&
               t->pcc_sym.upload(pcc_cell_symbols(t->maps)) &&
@@ -383,7 +384,12 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
     return r;
 }
 
-dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, const uint32_t* sel) {
+// the DRS SNR sums of a phase come from the front end (rx_fft_wave_kernel) where it runs; both phases
+// of a packet use the same PCC-phase geometry t, so the PCC and PDC launches agree
+bool snr_from_front(dnrp_ctx* ctx, rx1_tables* t);
+
+dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, const uint32_t* sel,
+                              const rx_plan_dev* plan = nullptr) {
     dev::rx_front_args a{};
     a.plan = t->plan;
     a.N_occ = t->N_occ;
@@ -423,7 +429,22 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, con
         return e ? std::atoi(e) : 1;
     }();
     a.stream = (ct_env && dev::rx_stream_taps_match(t->rs.h.data(), t->rs.h.size())) ? 1u : 0u;
+    if (plan && dev::rx_fft_wave_path(a)) {
+        a.snr_part = ctx->snr_part.as<double2>();
+        a.dl = plan->dl.as<uint32_t>();
+        a.dmeta = plan->dmeta.as<uint32_t>();
+        a.n_dops = plan->n_dops;
+        a.n_drs = t->N_occ / 4;
+        a.drs_neg = geo::drs_neg_mask();
+        a.sym_op = plan->sym_op.as<uint16_t>();
+        a.n_sym_op = plan->n_sym_op;
+    }
     return a;
+}
+
+bool snr_from_front(dnrp_ctx* ctx, rx1_tables* t) {
+    const char* e = std::getenv("DNRP_RX_SNR_FRONT");  // A/B: 0 -> rx_snr gathers the DRS cells from Y
+    return (!e || std::atoi(e)) && t->drs_arith && dev::rx_fft_wave_path(front_args(ctx, t, nullptr, nullptr));
 }
 
 // back-end launches of one phase: SNR chain, then cells (rx_back.hip)
@@ -452,6 +473,7 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     s.lut_d = ctx->lut_d.as<uint8_t>();
     s.nv_d = ctx->nv_d.as<float>();
     s.sel = sel;
+    s.snr_part = snr_from_front(ctx, t) ? ctx->snr_part.as<double2>() : nullptr;
     dev::rx_cells_args c{};
     c.N_occ = t->N_occ;
     c.N_RX = ctx->cfg.N_TX_max;
@@ -771,7 +793,8 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
     ctx->rx_iq = iq_in;
     ctx->rx_n_windows = n_windows;
     const size_t ybytes = size_t(n) * ctx->cfg.N_TX_max * (ctx->rx_nsym_cap + 1) * ctx->rx_Nf_pad * sizeof(float2);
-    if (!ctx->Y.ensure(ybytes) || !ctx->rx_in.ensure(sizeof(dev::rx_pkt_in) * ctx->cfg.max_batch) ||
+    const size_t pbytes = size_t(n) * (ctx->rx_nsym_cap + 1) * ctx->cfg.N_TX_max * 8 * sizeof(double2);
+    if (!ctx->Y.ensure(ybytes) || !ctx->snr_part.ensure(pbytes) || !ctx->rx_in.ensure(sizeof(dev::rx_pkt_in) * ctx->cfg.max_batch) ||
         !ctx->rx_st.ensure(sizeof(dev::rx_pkt_state) * ctx->cfg.max_batch) ||
         !ctx->rx_sel.ensure(2 * sizeof(uint32_t) * ctx->cfg.max_batch))
         return DNRP_ENOMEM;
@@ -803,7 +826,7 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         const uint32_t ng = static_cast<uint32_t>(g.second->size());
         const uint32_t* gsel = ctx->rx_sel.as<uint32_t>() + 2 * off;
         off += ng;
-        auto fa = front_args(ctx, t, iq_in, gsel);
+        auto fa = front_args(ctx, t, iq_in, gsel, snr_from_front(ctx, t) ? &t->bplan : nullptr);
         ctx->tic("rx_stf", st);
         if (dev::launch_rx_stf(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
         ctx->toc("rx_stf", st);
@@ -898,7 +921,7 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
         const uint32_t ng = static_cast<uint32_t>(g.second.size());
         const uint32_t* gsel = ctx->rx_sel2.as<uint32_t>() + 2 * off;
         off += ng;
-        auto fa = front_args(ctx, t, iq_in, gsel);
+        auto fa = front_args(ctx, t, iq_in, gsel, snr_from_front(ctx, t) ? &t2->bplan : nullptr);
         fa.sym_first = t->pcc_max + 1;
         if (t2->q.N_DF_symb > t->pcc_max) {
             fa.sym_count = t2->q.N_DF_symb - t->pcc_max;

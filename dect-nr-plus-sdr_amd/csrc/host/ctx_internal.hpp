@@ -116,6 +116,8 @@ struct rx_plan_dev {
     uint32_t n_dops = 0, n_epochs = 0;
     bool cells_ok = true;  // every epoch fits rx_cells_kernel: <= CELL_MAX_SEGS segments, one DRS count
     dbuf dl, dmeta, segs, epochs;
+    dbuf sym_op;  // [n_sym] first DRS op at symbol l, 0xFFFF: none (the front end's DRS test)
+    uint32_t n_sym_op = 0;
     bool upload(const geo::rx_plan_t& p) {
         static_assert(sizeof(geo::rx_seg_t) == sizeof(dev::rx_seg), "rx_seg layout");
         static_assert(sizeof(geo::rx_epoch_t) == sizeof(dev::rx_epoch), "rx_epoch layout");
@@ -125,7 +127,12 @@ struct rx_plan_dev {
             cells_ok = cells_ok && e.seg1 - e.seg0 <= dev::CELL_MAX_SEGS;
             for (uint32_t i = e.seg0; i < e.seg1; ++i) cells_ok = cells_ok && p.segs[i].drs_cnt == p.segs[e.seg0].drs_cnt;
         }
-        return dl.upload(p.dl) && dmeta.upload(p.dmeta) && segs.upload(p.segs) && epochs.upload(p.epochs);
+        uint32_t lmax = 0;
+        for (uint32_t l : p.dl) lmax = std::max(lmax, l);
+        std::vector<uint16_t> so((lmax + 2) & ~1u, 0xFFFFu);  // whole dwords (scalar loads)
+        for (uint32_t d = n_dops; d-- > 0;) so[p.dl[d]] = static_cast<uint16_t>(d);
+        n_sym_op = lmax + 1;
+        return dl.upload(p.dl) && dmeta.upload(p.dmeta) && segs.upload(p.segs) && epochs.upload(p.epochs) && sym_op.upload(so);
     }
 };
 
@@ -135,6 +142,7 @@ struct rx1_tables {  // per (u, b, N_eff_TX): STF/PCC phase
     geo::resampler_t rs;
     geo::maps_t maps;
     uint32_t pcc_max = 0;
+    bool drs_arith = false;  // DRS tables match rx_drs_partials' arithmetic (front-end SNR sums)
     dbuf stf, tw, taps, taps_pp, drs_k, drs_v, pcc_k, pcc_sym;
     uint32_t npp = 0;  // floats in taps_pp
     rx_plan_dev bplan;  // PCC phase back end
@@ -186,6 +194,7 @@ struct dnrp_ctx {
     dbuf pcc_seq;
     // batch scratch
     dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d, nv_d, mimo_out;
+    dbuf snr_part;  // [slot][n_sym_total][N_RX][8] double2: front-end DRS SNR partial sums
     uint32_t rx_mode = 0;  // DNRP_RX_MODE_* (dnrp_ctx_set_rx_mode)
     pinned st_tx, st_rxin, st_seq, st_rep;
     // retained RX phase-1 state: per PCC-batch slot its (u, b, N_eff_TX) tables and symbol

@@ -255,6 +255,26 @@ std::vector<cf32> stf_values(uint32_t b, uint32_t N_eff_TX) {  // stf.cpp:171-18
 
 float drs_value(uint32_t t, uint32_t i) { return static_cast<float>(DRS_Y[(4 * i + t % 4) % 56] * (t < 4 ? 1 : -1)); }
 
+uint64_t drs_neg_mask() {
+    uint64_t m = 0;
+    for (uint32_t j = 0; j < 56; ++j) m |= uint64_t(DRS_Y[j] < 0) << j;
+    return m;
+}
+
+// the front end's arithmetic DRS cells (rx_front.hpp rx_drs_partials) against the tables
+bool drs_tables_arithmetic(const maps_t& m) {
+    const uint32_t N = m.Nf - 1, nd = N / 4;
+    const uint64_t neg = drs_neg_mask();
+    for (uint32_t p = 0; p < 2; ++p)
+        for (uint32_t t = 0; t < 8; ++t)
+            for (uint32_t i = 0; i < nd; ++i) {
+                const uint32_t x = 4 * i + ((t + 2 * p) & 3u), k = x + (x >= N / 2 ? 1u : 0u);
+                const float s = (((neg >> ((4 * i + (t & 3u)) % 56)) & 1ull) ? -1.f : 1.f) * (t < 4 ? 1.f : -1.f);
+                if (m.drs_k[(p * 4 + t % 4) * nd + i] != k || m.drs_v[t * nd + i] != s) return false;
+            }
+    return true;
+}
+
 maps_t build_maps(uint32_t b, uint32_t N_TS, uint32_t N_eff_TX, uint32_t N_DF) {
     maps_t m;
     const uint32_t Nb = 64 * b, N = 56 * b, Nf = N + 1, gb = 4 * b;

@@ -73,6 +73,8 @@ uint32_t txdiv_modulo(uint32_t N_TS);
 void txdiv_pair(uint32_t N_TS, uint32_t i, uint32_t& A, uint32_t& B);
 // DRS value of transmit stream t at DRS cell i (drs.cpp:227-254): +-y_b_1[(4 i + t % 4) % 56]
 float drs_value(uint32_t t, uint32_t i);
+uint64_t drs_neg_mask();                     // bit j: DRS y_b_1[j] = -1 (drs.hpp)
+bool drs_tables_arithmetic(const maps_t& m);  // drs_k / drs_v == the front end's arithmetic DRS cells
 
 std::vector<uint8_t> gold_bits_packed(uint32_t c_init, uint32_t nbits);  // MSB-first bytes
 

@@ -102,7 +102,20 @@ struct rx_front_args {
     float2* Y;                 // [n][N_RX][n_sym_total][Nf_pad]
     uint32_t stream;           // compile-time-tap front end allowed (host: compiled-in taps match)
     const uint32_t* sel;       // [launch packets][2]: PCC-batch slot, output row (rx_slot_of / rx_row_of)
+    // DRS SNR partial sums taken while a DRS symbol's bins are in the wave (rx_fft_wave_kernel):
+    // snr_part[((slot n_sym_total + l) N_RX + rx) 8 + ts_first] = (sum |w y|^2, sum |w y_i - w y_i+1|^2)
+    // over the DRS cells of every stream of the op at symbol l (estimator_snr.cpp:104-146 terms);
+    // null: rx_snr gathers them from Y. The DRS cells are computed, not loaded: stream t, parity p,
+    // cell i at occupied index 4 i + (t + 2 p) % 4 (DC skipped), value -+1 from drs_neg bit
+    // (4 i + t % 4) % 56, negated for t >= 4 (drs.cpp:196-254; host-checked against drs_k / drs_v)
+    double2* snr_part;
+    const uint32_t* dl;        // the phase plan's DRS ops (rx_snr_args)
+    const uint32_t* dmeta;
+    uint64_t drs_neg;          // bit j: y_b_1[j] = -1 (drs.hpp)
+    const uint16_t* sym_op;    // [n_sym_op]: first DRS op of symbol l, 0xFFFF: none
+    uint32_t n_dops, n_drs, n_sym_op;
 };
+bool rx_fft_wave_path(const rx_front_args& a);  // launch_rx_fft takes rx_fft_wave_kernel (snr_part supported)
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);
 bool rx_stream_taps_match(const float* h, size_t n);  // compiled-in 9/10 taps == run-time taps
 hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st);
@@ -135,6 +148,7 @@ struct rx_snr_args {        // DRS zero-forcing SNR chain + LUT profile picks, o
     uint8_t* lut_d;         // [slot][RX_MAX_DOPS]: profile picked after each DRS op
     float* nv_d;            // [slot][RX_MAX_DOPS]: noise variance per RX cell after each DRS op
     const uint32_t* sel;    // launch packet -> slot / output row
+    const double2* snr_part;  // front-end partial sums (rx_front_args::snr_part) or null: gather from Y
 };
 hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st);
 

@@ -340,6 +340,13 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
     // valid input window relative to the fine peak: history is zero before it (rx_synced.cpp:711-740)
     const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
     const float2* src = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in + in.fine_peak;
+    // a DRS symbol's bins also stay in R for the SNR partial sums: its op-table entry by a scalar load
+    // issued ahead of the staging (a vector load here would add a memory round trip to every wave)
+    uint32_t so = 0xFFFFu;
+    if (A.snr_part && l < A.n_sym_op) {
+        const auto* sop = reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(reinterpret_cast<uintptr_t>(A.sym_op));
+        so = (sop[l >> 1] >> (16 * (l & 1u))) & 0xFFFFu;
+    }
     if (active) stage_span_lo<20>(R, src, sp.in0, sp.n_in, q_lo, q_hi, lane, 64);
     if constexpr (CT)
         __builtin_amdgcn_wave_barrier();  // only the wave's own staging
@@ -347,9 +354,18 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
         __syncthreads();  // twiddles / taps (and this wave's own staging)
     if (!active) return;
     float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
+    const bool drs = so != 0xFFFFu;
     if constexpr (CT) {
         rx_resample_ct<LR, MR, HLR>(A, in, S, sp, R, lane);
-        rx_fft_bins(A, S, R, lane, [&](uint32_t k, float2 v) { Yrow[k] = v; });
+        // one instantiation of the (large, unrolled) FFT for both kinds of symbol: instruction cache
+        rx_fft_bins(A, S, R, lane, [&](uint32_t k, float2 v) {
+            Yrow[k] = v;
+            if (drs) R[k] = v;
+        });
+        if (drs) {
+            __builtin_amdgcn_wave_barrier();
+            rx_drs_partials(A, pkt, a, l, R, lane);
+        }
         return;
     } else {
         constexpr int BR = (Nd + 2 * LR) / LR / 64 + 1;  // block rounds per lane
@@ -382,7 +398,14 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
         // table path: twiddles from LDS (rx_fft_bins reads them through A.tw)
         rx_front_args B = A;
         B.tw = twl;
-        rx_fft_bins(B, S, R, lane, [&](uint32_t k, float2 v) { Yrow[k] = v; });
+        rx_fft_bins(B, S, R, lane, [&](uint32_t k, float2 v) {
+            Yrow[k] = v;
+            if (drs) R[k] = v;
+        });
+        if (drs) {
+            __builtin_amdgcn_wave_barrier();
+            rx_drs_partials(A, pkt, a, l, R, lane);
+        }
     }
 }
 
@@ -391,6 +414,10 @@ bool rx_stream_taps_match(const float* h, size_t n) {  // run-time RX taps == co
     for (size_t i = 0; i < n; ++i)
         if (__builtin_bit_cast(uint32_t, h[i]) != __builtin_bit_cast(uint32_t, taps_rx_9_10::h[i])) return false;
     return true;
+}
+
+bool rx_fft_wave_path(const rx_front_args& a) {
+    return a.plan.N == 1024 && a.L == 9 && a.M == 10 && a.hl == 24 && a.sym_per_block == RXW_SYMS;
 }
 
 hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
@@ -402,7 +429,7 @@ hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
         const size_t lds = base + rx_in_cap(Nd, a.CP, a.L, a.M, W) * sizeof(float2) + a.npp * sizeof(float);
         hipLaunchKernelGGL(kern, g, b, lds, st, a);
     };
-    if (Nd == 1024 && a.L == 9 && a.M == 10 && a.hl == 24 && a.sym_per_block == RXW_SYMS) {  // os_min 1
+    if (rx_fft_wave_path(a)) {  // os_min 1
         const uint32_t W = pp_block<9, 10, 24>::W;
         if (a.stream) {  // host: run-time taps == compiled-in taps bit for bit
             // one wave per workgroup by default: each wave's LDS region is freed when it retires

@@ -30,7 +30,28 @@ __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u, nw = SNR_THREADS / 64;
     const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
     const float2* Yp = A.Y + size_t(pkt) * NRX * ast;
-    for (uint32_t d = wave; d < A.n_dops; d += nw) {
+    if (A.snr_part) {  // the front end's partial sums of every RX antenna (one lane each)
+        for (uint32_t d = wave; d < A.n_dops; d += nw) {
+            const uint32_t meta = __builtin_amdgcn_readfirstlane(A.dmeta[d]);
+            const uint32_t l = __builtin_amdgcn_readfirstlane(A.dl[d]);
+            const uint32_t tf = meta & 0xFFu;
+            double s1 = 0.0, s2 = 0.0;
+            if (lane < NRX) {
+                const double2 p = A.snr_part[((size_t(pkt) * A.n_sym_total + l) * NRX + lane) * 8 + tf];
+                s1 = p.x;
+                s2 = p.y;
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                s1 += __shfl_xor(s1, o);
+                s2 += __shfl_xor(s2, o);
+            }
+            if (lane == 0) {
+                s1s[d] = s1;
+                s2s[d] = s2;
+            }
+        }
+    }
+    for (uint32_t d = A.snr_part ? A.n_dops : wave; d < A.n_dops; d += nw) {
         const uint32_t meta = __builtin_amdgcn_readfirstlane(A.dmeta[d]);
         const uint32_t l = __builtin_amdgcn_readfirstlane(A.dl[d]);
         const uint32_t tf = meta & 0xFFu, tl = (meta >> 8) & 0xFFu, par = (meta >> 16) & 0xFFu;
@@ -125,7 +146,7 @@ __global__ void __launch_bounds__(SNR_THREADS) rx_snr_kernel(rx_snr_args A) {
 }
 
 hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st) {
-    if (a.n_dops > MAX_DOPS || a.n_drs > 64 * SNR_ROUNDS) return hipErrorInvalidValue;
+    if (a.n_dops > MAX_DOPS || a.n_drs > 64 * SNR_ROUNDS || (a.snr_part && a.N_RX > 64)) return hipErrorInvalidValue;
     switch (a.N_RX) {
         case 1: hipLaunchKernelGGL(rx_snr_kernel<1>, dim3(n), dim3(SNR_THREADS), 0, st, a); break;
         case 2: hipLaunchKernelGGL(rx_snr_kernel<2>, dim3(n), dim3(SNR_THREADS), 0, st, a); break;

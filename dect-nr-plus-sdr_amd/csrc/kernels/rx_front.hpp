@@ -106,4 +106,38 @@ __device__ __forceinline__ void rx_fft_bins(const rx_front_args& A, const rx_pkt
     }
 }
 
+// DRS SNR terms of one (antenna, DRS symbol) while its bins sit in the wave's region R (R[k] = bin
+// of subcarrier k): for every DRS op of symbol l and each of its transmit streams t, the sums over
+// the stream's DRS cells i of |w_i y_i|^2 and |w_i y_i - w_i+1 y_i+1|^2 (rx_snr_kernel's terms, the
+// same float products accumulated in double) -> A.snr_part. The op list is uniform (scalar loads).
+__device__ __forceinline__ void rx_drs_partials(const rx_front_args& A, uint32_t slot, uint32_t a, uint32_t l,
+                                                const float2* R, uint32_t lane) {
+    const uint32_t nd = A.n_drs, half = 2 * nd;  // N_b_OCC / 2
+    // subcarrier index and value of DRS cell i of stream t with parity p
+    auto cell = [&](uint32_t t, uint32_t p, uint32_t i) {
+        const uint32_t x = 4 * i + ((t + 2 * p) & 3u);
+        const float s = (((A.drs_neg >> ((4 * i + (t & 3u)) % 56)) & 1ull) ? -1.f : 1.f) * (t < 4 ? 1.f : -1.f);
+        return cscale(R[x + (x >= half ? 1u : 0u)], s);
+    };
+    for (uint32_t d = A.sym_op[l]; d < A.n_dops; ++d) {  // the ops of one symbol are consecutive
+        if (__builtin_amdgcn_readfirstlane(A.dl[d]) != l) break;
+        const uint32_t meta = __builtin_amdgcn_readfirstlane(A.dmeta[d]);
+        const uint32_t tf = meta & 0xFFu, tl = (meta >> 8) & 0xFFu, par = (meta >> 16) & 0xFFu;
+        // per lane at most 4 (nd <= 256) terms per stream: float sums, double across the lanes
+        float f1 = 0.f, f2 = 0.f;
+        for (uint32_t t = tf; t <= tl; ++t)
+            for (uint32_t i = lane; i < nd; i += 64) {
+                const float2 v = cell(t, par, i);
+                f1 += cnorm(v);
+                if (i + 1 < nd) f2 += cnorm(csub(v, cell(t, par, i + 1)));
+            }
+        double s1 = f1, s2 = f2;
+        for (int o = 32; o > 0; o >>= 1) {
+            s1 += __shfl_xor(s1, o);
+            s2 += __shfl_xor(s2, o);
+        }
+        if (lane == 0) A.snr_part[((size_t(slot) * A.n_sym_total + l) * A.N_RX + a) * 8 + tf] = make_double2(s1, s2);
+    }
+}
+
 }  // namespace dnrp::dev

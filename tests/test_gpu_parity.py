@@ -206,6 +206,14 @@ def test_rx_parity(name):
             assert np.mean(bits != (g_pdc[i] > 0)) < 2e-2, (name, i)
 
 
+@pytest.mark.parametrize("name", ["C4", "C3", "C2"])
+def test_rx_parity_snr_from_y(name, monkeypatch):
+    """DNRP_RX_SNR_FRONT=0: the DRS SNR sums gathered by rx_snr_kernel from Y instead of the front end's
+    partial sums (rx_front.hpp rx_drs_partials) -- the same oracle and gates on both paths."""
+    monkeypatch.setenv("DNRP_RX_SNR_FRONT", "0")
+    test_rx_parity(name)
+
+
 def test_rx_pdc_per_packet_requests():
     """One PCC batch of 8 packets with mixed transmission modes (N_eff_TX 1 / 2 / 4 in one call),
     then a PDC batch in which the MAC dropped 2 packets (continue_with_pdc = false) and the rest
