@@ -483,6 +483,7 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     c.n_drs = t->N_occ / 4;
     c.n_dops = plan.n_dops;
     c.n_epochs = plan.n_epochs;
+    c.n_pkt = n;
     c.N_bps = N_bps;
     c.wcap[0] = t->wcap[0];
     c.wcap[1] = t->wcap[1];

@@ -160,6 +160,7 @@ struct rx_lut {             // one Wiener LUT: [T][4][Nf] pilot | weight << 16, 
 
 struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epoch)
     uint32_t N_occ, N_RX, NT, Nf_pad, n_sym_total, n_drs, n_dops, n_epochs, N_bps, mod, is_pdc;
+    uint32_t n_pkt;  // launch packets (the grid is padded to whole XCD rounds, rx_cells_kernel)
     uint32_t sm;               // 1: spatial multiplexing, NT = N_SS streams per cell, MMSE (unit = cell)
     uint32_t wcap[2];          // floats of the LDS weight-table slot of mode l / lr (largest such table)
     uint32_t pair[12];

@@ -168,7 +168,12 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
     float* wtab = reinterpret_cast<float*>(zfi + NRX * NT * zst);            // slots: mode l, mode lr
     cell_seg* sg = reinterpret_cast<cell_seg*>(wtab + A.wcap[0] + A.wcap[1]);  // CELL_MAX_SEGS
     uint32_t* pairs = reinterpret_cast<uint32_t*>(sg + CELL_MAX_SEGS);       // 12
-    const uint32_t pl = blockIdx.x / A.n_epochs, ep = blockIdx.x % A.n_epochs;
+    // XCD-aware: workgroups are dealt round-robin over the 8 XCDs, so workgroup b runs on XCD b % 8;
+    // the epochs of one packet are consecutive on one XCD (b / 8 = packet-of-XCD * n_epochs + epoch)
+    // and re-read the packet's DRS cells from that XCD's L2 instead of HBM
+    const uint32_t xs = blockIdx.x >> 3;
+    const uint32_t pl = (xs / A.n_epochs) * 8 + (blockIdx.x & 7u), ep = xs % A.n_epochs;
+    if (pl >= A.n_pkt) return;
     const uint32_t pkt = rx_slot_of(A.sel, pl), row = rx_row_of(A.sel, pl);
     const rx_epoch* E = A.epochs + ep;
     const uint32_t units = E->units, seg0 = E->seg0, nseg = E->seg1 - E->seg0;
@@ -245,8 +250,8 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
 
 hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st) {
     const size_t lds = cell_lds_bytes(a.N_RX, a.NT, a.n_drs, a.wcap[0], a.wcap[1]);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const dim3 g(n * a.n_epochs), b(CELL_THREADS);
+    if (lds > 160 * 1024 || a.n_pkt != n) return hipErrorInvalidValue;
+    const dim3 g((n + 7) / 8 * 8 * a.n_epochs), b(CELL_THREADS);
 #define DNRP_CELLS(R, T)                                                                 \
     if (a.N_RX == R && a.NT == T) {                                                      \
         hipLaunchKernelGGL((rx_cells_kernel<R, T>), g, b, lds, st, a);                   \
@@ -267,8 +272,8 @@ hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st) {
 
 hipError_t launch_rx_cells_sm(const rx_cells_args& a, uint32_t n, hipStream_t st) {
     const size_t lds = cell_lds_bytes(a.N_RX, a.NT, a.n_drs, a.wcap[0], a.wcap[1]);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const dim3 g(n * a.n_epochs), b(CELL_THREADS);
+    if (lds > 160 * 1024 || a.n_pkt != n) return hipErrorInvalidValue;
+    const dim3 g((n + 7) / 8 * 8 * a.n_epochs), b(CELL_THREADS);
 #define DNRP_CELLS_SM(R, T)                                                              \
     if (a.N_RX == R && a.NT == T) {                                                      \
         hipLaunchKernelGGL((rx_cells_kernel<R, T, true>), g, b, lds, st, a);             \
