@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
         });
         if (drs) {
             __builtin_amdgcn_wave_barrier();
-            rx_drs_partials(A, pkt, a, l, R, lane);
+            rx_drs_partials(A, pkt, a, l, so, R, lane);
         }
         return;
     } else {
@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
         });
         if (drs) {
             __builtin_amdgcn_wave_barrier();
-            rx_drs_partials(A, pkt, a, l, R, lane);
+            rx_drs_partials(A, pkt, a, l, so, R, lane);
         }
     }
 }

@@ -111,7 +111,7 @@ __device__ __forceinline__ void rx_fft_bins(const rx_front_args& A, const rx_pkt
 // the stream's DRS cells i of |w_i y_i|^2 and |w_i y_i - w_i+1 y_i+1|^2 (rx_snr_kernel's terms, the
 // same float products accumulated in double) -> A.snr_part. The op list is uniform (scalar loads).
 __device__ __forceinline__ void rx_drs_partials(const rx_front_args& A, uint32_t slot, uint32_t a, uint32_t l,
-                                                const float2* R, uint32_t lane) {
+                                                uint32_t d0, const float2* R, uint32_t lane) {
     const uint32_t nd = A.n_drs, half = 2 * nd;  // N_b_OCC / 2
     // subcarrier index and value of DRS cell i of stream t with parity p
     auto cell = [&](uint32_t t, uint32_t p, uint32_t i) {
@@ -119,17 +119,27 @@ __device__ __forceinline__ void rx_drs_partials(const rx_front_args& A, uint32_t
         const float s = (((A.drs_neg >> ((4 * i + (t & 3u)) % 56)) & 1ull) ? -1.f : 1.f) * (t < 4 ? 1.f : -1.f);
         return cscale(R[x + (x >= half ? 1u : 0u)], s);
     };
-    for (uint32_t d = A.sym_op[l]; d < A.n_dops; ++d) {  // the ops of one symbol are consecutive
-        if (__builtin_amdgcn_readfirstlane(A.dl[d]) != l) break;
-        const uint32_t meta = __builtin_amdgcn_readfirstlane(A.dmeta[d]);
+    // the op table by scalar loads (uniform symbol and op index): a vector load here would wait
+    // (vmcnt retires in order) for the symbol's Y stores just issued. d0: the symbol's first op.
+    typedef const __attribute__((address_space(4))) uint32_t* cu32;
+    const cu32 dl = reinterpret_cast<cu32>(reinterpret_cast<uintptr_t>(A.dl));
+    const cu32 dm = reinterpret_cast<cu32>(reinterpret_cast<uintptr_t>(A.dmeta));
+    l = __builtin_amdgcn_readfirstlane(l);
+    for (uint32_t d = __builtin_amdgcn_readfirstlane(d0); d < A.n_dops; ++d) {  // ops of a symbol: consecutive
+        if (dl[d] != l) break;
+        const uint32_t meta = dm[d];
         const uint32_t tf = meta & 0xFFu, tl = (meta >> 8) & 0xFFu, par = (meta >> 16) & 0xFFu;
-        // per lane at most 4 (nd <= 256) terms per stream: float sums, double across the lanes
+        // per lane at most 4 (nd <= 256) terms per stream: float sums, double across the lanes; the
+        // right neighbour of cell i comes from the next lane (lane 63: the next round's first cell)
         float f1 = 0.f, f2 = 0.f;
         for (uint32_t t = tf; t <= tl; ++t)
-            for (uint32_t i = lane; i < nd; i += 64) {
-                const float2 v = cell(t, par, i);
-                f1 += cnorm(v);
-                if (i + 1 < nd) f2 += cnorm(csub(v, cell(t, par, i + 1)));
+            for (uint32_t i0 = 0; i0 < nd; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const float2 v = cell(t, par, min(i, nd - 1));
+                float2 vn = make_float2(__shfl_down(v.x, 1), __shfl_down(v.y, 1));
+                if (lane == 63) vn = cell(t, par, min(i + 1, nd - 1));
+                if (i < nd) f1 += cnorm(v);
+                if (i + 1 < nd) f2 += cnorm(csub(v, vn));
             }
         double s1 = f1, s2 = f2;
         for (int o = 32; o > 0; o >>= 1) {
