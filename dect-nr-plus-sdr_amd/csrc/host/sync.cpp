@@ -220,9 +220,11 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     const size_t nsa = size_t(n) * a.n_ant * a.n_steps;
     if (!ctx->sy_P.ensure(nsa * sizeof(float)) || !ctx->sy_C.ensure(nsa * sizeof(float2)) ||
         !ctx->sy_res.ensure(size_t(n) * a.max_reports * sizeof(dev::sync_res)) || !ctx->sy_cnt.ensure(size_t(n) * 4) ||
-        !ctx->sy_spec.ensure(size_t(n) * a.max_reports * (size_t(1) << a.log2_fft) * sizeof(float2)))
+        !ctx->sy_spec.ensure(size_t(n) * a.max_reports * (size_t(1) << a.log2_fft) * sizeof(float2)) ||
+        !ctx->sy_post.ensure(size_t(n) * a.max_reports * 8 * sizeof(float)))
         return DNRP_ENOMEM;
     a.spec = ctx->sy_spec.as<float2>();
+    a.post = ctx->sy_post.as<float>();
     a.P = ctx->sy_P.as<float>();
     a.Cs = ctx->sy_C.as<float2>();
     a.res = ctx->sy_res.as<dev::sync_res>();
@@ -274,6 +276,9 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
                      cnt ? q[0] / cnt : 0.0, cnt ? q[1] / cnt : 0.0, cnt ? q[2] / cnt : 0.0, cnt ? q[3] / cnt : 0.0);
     }
 #endif
+    ctx->tic("sync_post", st);
+    if (dev::launch_sync_post(a, n, st) != hipSuccess) return DNRP_EDEVICE;
+    ctx->toc("sync_post", st);
     ctx->tic("sync_fine", st);
     if (dev::launch_sync_fine(a, n, st) != hipSuccess) return DNRP_EDEVICE;
     ctx->toc("sync_fine", st);

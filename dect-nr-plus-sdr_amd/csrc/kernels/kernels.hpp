@@ -299,10 +299,12 @@ struct sync_args {
     const float2* tmpl_f;                      // [n_templates][n_fft] conj(DFT(template)) / n_fft
     const float2* tw_fft;                      // forward twiddles of n_fft
     float2* spec;                              // sync_fine scratch: forward spectrum per report [n * max_reports][n_fft]
+    float* post;                               // [n * max_reports][8]: per antenna m_a atan2(c_a) / P (sync_post_kernel)
     uint32_t u, b;
 };
 hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st);
 hipError_t launch_sync_detect(const sync_args& a, uint32_t n, hipStream_t st);
+hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st);
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st);
 uint32_t sync_detect_stage(const sync_args& a);
 size_t sync_detect_lds(const sync_args& a);

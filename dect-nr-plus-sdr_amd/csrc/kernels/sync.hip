@@ -765,30 +765,9 @@ __global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_ker
         const uint32_t wpk = static_cast<uint32_t>(roundf(wsum / msum));
         if (wpk < A.stf_len - 1) continue;  // STF would start before the chunk (asserted in the reference)
         const uint32_t cpl = wpk - (A.stf_len - 1);
-        // post_processing_at_coarse_peak (:366-394): RMS and fractional CFO over the STF at the peak
-        float cfo_w = 0.f, msum2 = 0.f, rms[8];
-        for (uint32_t a = 0; a < A.n_ant; ++a) {
-            rms[a] = 0.f;
-            if (!(cm[a] > 0.f)) continue;
-            const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
-            sync_resample<LR, MR, HLR>(A, x, cpl, A.stf_len, stage, lbuf, taps, A.det_stage);
-            double cr = 0.0, ci = 0.0, pw = 0.0;
-            const uint32_t Lw = A.pattern * A.n_uw;
-            for (uint32_t i = threadIdx.x; i < A.stf_len; i += blockDim.x) {
-                pw += cnorm(lbuf[i]);
-                if (i < Lw) {
-                    const float2 c = cmulc(lbuf[i], lbuf[i + A.pattern]);
-                    const float u = A.uw[i / A.pattern];
-                    cr += u * static_cast<double>(c.x);
-                    ci += u * static_cast<double>(c.y);
-                }
-            }
-            block_sum3(pw, cr, ci, red);
-            const float m = s_pk_metric[a];
-            msum2 += m;
-            rms[a] = sqrtf(static_cast<float>(pw) / static_cast<float>(A.stf_len));
-            cfo_w += m * atan2f(static_cast<float>(ci), static_cast<float>(cr)) / static_cast<float>(A.pattern);
-        }
+        // post_processing_at_coarse_peak (:366-394, RMS and fractional CFO over the STF at the peak)
+        // runs per (report, antenna) in sync_post_kernel, the CFO's antenna sum in sync_fine_kernel:
+        // nothing in the detection loop depends on them
         SYNC_STAMP(10);
         if (threadIdx.x == 0) {
             sync_res r{};
@@ -805,9 +784,9 @@ __global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_ker
             r.coarse_64 = static_cast<int64_t>(static_cast<uint32_t>(round(g)));
             for (uint32_t a = 0; a < 8; ++a) {
                 r.coarse_metric[a] = a < A.n_ant ? cm[a] : 0.f;
-                r.rms[a] = a < A.n_ant ? rms[a] : 0.f;
+                r.rms[a] = 0.f;  // sync_post_kernel
             }
-            r.cfo_frac = cfo_w / msum2;
+            r.cfo_frac = 0.f;  // sync_fine_kernel (antenna sum of sync_post_kernel's terms)
             r.cfo_int = 0.f;  // coarse_peak_f_domain.cpp:195-199
             r.u = A.u;
             r.b = A.b;  // coarse_peak_f_domain.cpp:75-120: b of the radio device class
@@ -824,6 +803,46 @@ __global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_ker
     }
 }
 
+// ===================================================================== coarse-peak post-processing
+// autocorrelator_peak.cpp:366-394 for one (report, antenna): the STF at the coarse peak resampled
+// again, its power and cover-weighted pattern correlation (the same loops and block reduction the
+// detection kernel ran, so the same doubles) -> rms[a] into the report and the antenna's CFO term
+// m_a atan2(c_a) / P into A.post; sync_fine_kernel sums the terms in antenna order. One workgroup
+// per (report, antenna) instead of four serial passes inside the detection workgroup.
+template <int LR, int MR, int HLR>
+__global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    double* red = reinterpret_cast<double*>(smem);  // [24]
+    float* taps = reinterpret_cast<float*>(smem + 12);
+    const uint32_t tap_f2 = (A.npp + 3) / 4 * 2;
+    float2* lbuf = smem + 12 + tap_f2;
+    float2* stage = lbuf + (A.stf_len + 1) / 2 * 2;
+    const uint32_t rep = blockIdx.x / A.n_ant, a = blockIdx.x % A.n_ant, w = rep / A.max_reports;
+    sync_res* rp = A.res + rep;
+    const float m = rp->coarse_metric[a];
+    if (!rp->found || !(m > 0.f)) return;  // uniform: the whole workgroup leaves
+    if (LR > 1) stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, blockDim.x);
+    __syncthreads();
+    const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
+    sync_resample<LR, MR, HLR>(A, x, rp->coarse_local, A.stf_len, stage, lbuf, taps, A.det_stage);
+    double cr = 0.0, ci = 0.0, pw = 0.0;
+    const uint32_t Lw = A.pattern * A.n_uw;
+    for (uint32_t i = threadIdx.x; i < A.stf_len; i += blockDim.x) {
+        pw += cnorm(lbuf[i]);
+        if (i < Lw) {
+            const float2 c = cmulc(lbuf[i], lbuf[i + A.pattern]);
+            const float u = A.uw[i / A.pattern];
+            cr += u * static_cast<double>(c.x);
+            ci += u * static_cast<double>(c.y);
+        }
+    }
+    block_sum3(pw, cr, ci, red);
+    if (threadIdx.x == 0) {
+        rp->rms[a] = sqrtf(static_cast<float>(pw) / static_cast<float>(A.stf_len));
+        A.post[size_t(rep) * 8 + a] = m * atan2f(static_cast<float>(ci), static_cast<float>(cr)) / static_cast<float>(A.pattern);
+    }
+}
+
 // ===================================================================== fine peak
 __global__ void __launch_bounds__(SYNC_THREADS) sync_fine_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -832,6 +851,18 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_fine_kernel(sync_args A) {
     sync_res* rp = A.res + blockIdx.x;
     if (!rp->found) return;
     const uint32_t w = blockIdx.x / A.max_reports;
+    {  // fractional CFO: metric-weighted antenna mean of sync_post_kernel's terms, in antenna order
+        float cfo_w = 0.f, msum = 0.f;
+        for (uint32_t a = 0; a < A.n_ant; ++a) {
+            const float m = rp->coarse_metric[a];
+            if (!(m > 0.f)) continue;
+            msum += m;
+            cfo_w += A.post[size_t(blockIdx.x) * 8 + a];
+        }
+        __syncthreads();  // every thread has read the report before thread 0 updates it
+        if (threadIdx.x == 0) rp->cfo_frac = cfo_w / msum;
+        __syncthreads();
+    }
     const uint32_t nf = 1u << A.log2_fft;
     float2* xb = smem + 4;
     float2* yb = xb + nf;
@@ -1000,6 +1031,16 @@ hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
 hipError_t launch_sync_detect(const sync_args& a, uint32_t n, hipStream_t st) {
     const dim3 g(n);
     SYNC_DISPATCH(sync_detect_kernel, g, sync_detect_lds(a));
+    return hipGetLastError();
+}
+
+size_t sync_post_lds(const sync_args& a) {
+    return (12 + (a.npp + 3) / 4 * 2 + (a.stf_len + 1) / 2 * 2) * sizeof(float2) + size_t(a.det_stage) * sizeof(float2);
+}
+
+hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st) {
+    const dim3 g(n * a.max_reports * a.n_ant);
+    SYNC_DISPATCH(sync_post_kernel, g, sync_post_lds(a));
     return hipGetLastError();
 }
 

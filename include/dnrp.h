@@ -380,7 +380,7 @@ int dnrp_query_table(const char* name, const uint32_t* arg, uint32_t n_arg, floa
 
 /* Kernel timing (only when the environment has DNRP_TIMING=1 at dnrp_ctx_create): HIP events
  * recorded on the caller's stream around each launch. Names: "tx", "sync_steps", "sync_detect",
- * "sync_fine", "rx_stf", "rx_fft_pcc", "rx_pcc", "rx_fft_pdc", "rx_pdc". */
+ * "sync_post", "sync_fine", "rx_stf", "rx_fft_pcc", "rx_pcc", "rx_fft_pdc", "rx_pdc". */
 int dnrp_last_kernel_ms(const dnrp_ctx* ctx, const char* name, float* ms);
 int dnrp_kernel_time_total(dnrp_ctx* ctx, const char* name, float* total_ms, uint32_t* count, int reset);
 
