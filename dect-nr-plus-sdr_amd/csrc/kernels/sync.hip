@@ -386,6 +386,138 @@ __global__ void __launch_bounds__(64 * SS_WPG) sync_steps_stream_kernel(sync_arg
     }
 }
 
+// ---- the streaming path for 64-sample steps with two chunks of loads in flight per wave
+// (sync_steps_stream_kernel<.., 16, 1> restated): the window is read through a range-checked buffer
+// descriptor (samples outside [0, S_win) read as zeros, no branches), the P / C step values are
+// stored the same way, and a chunk completes at most 10 steps (576 outputs), so every chunk issues
+// a fixed number of memory instructions. The waits for a chunk's loads are then counted vmcnt(n)
+// with the next chunk's loads still in flight, instead of draining the queue.
+template <int LR, int MR, int HLR>
+__device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, float2* ring, float2 (&pre)[MR],
+                                              __amdgpu_buffer_rsrc_t xr, __amdgpu_buffer_rsrc_t pr,
+                                              __amdgpu_buffer_rsrc_t cr, int64_t ib0, int64_t qa, uint32_t c,
+                                              uint32_t s_b, uint32_t& s_next, uint32_t lane) {
+    using PD = pp_direct<LR, MR, HLR>;
+    constexpr int W = PD::W, CARRY = W - MR, NEW = 64 * MR;
+    const int64_t step = A.step, ms = A.m_star;
+#pragma unroll
+    for (int j = 0; j < MR; ++j) inb[CARRY + j * 64 + lane] = pre[j];
+    {  // the chunk after next (past the segment: harmless reads, range-checked)
+        const int64_t ibn = ib0 + static_cast<int64_t>(c + 2) * NEW + CARRY + lane;
+#pragma unroll
+        for (int j = 0; j < MR; ++j) {
+            typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+            const u2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, static_cast<uint32_t>((ibn + j * 64) * 8), 0, 0);
+            pre[j] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    float2 xv[W];
+    if constexpr ((MR & 1) == 0) PD::template load<true>(inb + MR * lane, xv);
+    else PD::template load<false>(inb + MR * lane, xv);
+    float2 y[LR];
+    {
+        const float* tp = A.taps;
+        asm volatile("" : "+s"(tp));
+        PD::run(xv, (ctap_ptr)(tp), y);
+    }
+    const int64_t mb = ms + LR * (qa + 64 * static_cast<int64_t>(c) + lane);
+#pragma unroll
+    for (int k = 0; k < LR; ++k) ring[static_cast<uint32_t>(mb + k) & (SS_RING - 1)] = y[k];
+    if (lane < CARRY) inb[lane] = inb[NEW + lane];
+    __builtin_amdgcn_wave_barrier();
+    const int64_t m_end = ms + LR * (qa + 64 * static_cast<int64_t>(c) + 64);
+    const uint32_t s_end = static_cast<uint32_t>(min<int64_t>(s_b, m_end >= 0 ? m_end / step : 0));
+    // one pass of 16 steps covers the chunk's (<= 10) completed steps: 4 lanes per step, a quarter each
+    const uint32_t s = s_next + (lane >> 2), part = lane & 3u;
+    const uint32_t rot = (2u * ((lane >> 2) & 7u) + ((part >> 1) & 1u) + (lane >> 5)) % 16u;
+    const bool live = s < s_end;
+    const uint32_t n0 = (live ? s : s_next) * 64u + part * 16u;
+    const bool corr = live && static_cast<int64_t>(s) * step >= A.pattern;
+    const float2* rv = ring + (n0 & (SS_RING - 1));
+    const float2* ru = ring + ((n0 - A.pattern) & (SS_RING - 1));
+    float pw = 0.f;
+    float2 cc = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // two halves of 8 samples: 32 VGPRs of reads in flight, not 64
+        float2 v[8], u[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t jj = (8 * h + j + rot) & 15u;
+            v[j] = rv[jj];
+            u[j] = ru[jj];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (!corr) u[j] = make_float2(0.f, 0.f);
+            pw = fmaf(v[j].x, v[j].x, fmaf(v[j].y, v[j].y, pw));
+            cc.x = fmaf(u[j].x, v[j].x, fmaf(u[j].y, v[j].y, cc.x));
+            cc.y = fmaf(u[j].y, v[j].x, fmaf(-u[j].x, v[j].y, cc.y));
+        }
+    }
+    if (!live) {
+        pw = 0.f;
+        cc = make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+        pw += __shfl_xor(pw, o);
+        cc.x += __shfl_xor(cc.x, o);
+        cc.y += __shfl_xor(cc.y, o);
+    }
+    const bool st = live && part == 0;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pw), pr, st ? s * 4u : 0x80000000u, 0, 0);
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    const u2 cv = {__float_as_uint(cc.x), __float_as_uint(cc.y)};
+    __builtin_amdgcn_raw_buffer_store_b64(cv, cr, st ? s * 8u : 0x80000000u, 0, 0);
+    s_next = max(s_next, s_end);
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int LR, int MR, int HLR>
+__global__ void __launch_bounds__(64) sync_steps_pipe_kernel(sync_args A, uint32_t seg_steps, uint32_t n_seg) {
+    using PD = pp_direct<LR, MR, HLR>;
+    constexpr int W = PD::W, CARRY = W - MR, NEW = 64 * MR;
+    constexpr uint32_t INB = ss_inbuf<LR, MR, HLR>();
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const uint32_t lane = threadIdx.x & 63u;
+    float2* inb = smem;
+    float2* ring = inb + INB;
+    const uint32_t gw = blockIdx.x;
+    const uint32_t seg = gw % n_seg, a = (gw / n_seg) % A.n_ant, w = gw / (n_seg * A.n_ant);
+    if (w >= A.n_win) return;
+    const uint32_t s_a = seg * seg_steps, s_b = min(s_a + seg_steps, A.n_steps);
+    if (s_a >= s_b) return;
+    const int64_t step = A.step, P = A.pattern;
+    const int64_t m_lo = max<int64_t>(0, s_a * step - P), m_hi = s_b * step;
+    const int64_t ms = A.m_star;
+    const int64_t qa = floordiv(m_lo - ms, LR), qb = floordiv(m_hi - 1 - ms, LR);
+    const uint32_t nch = static_cast<uint32_t>((qb - qa + 64) / 64);
+    // range-checked rows: the window row (zeros outside [0, S_win)) and the step-value rows
+    const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
+    const size_t orow = (static_cast<size_t>(w) * A.n_ant + a) * A.n_steps;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(x), 0, static_cast<int>(A.S_win * 8u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(A.P + orow, 0, static_cast<int>(A.n_steps * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(A.Cs + orow, 0, static_cast<int>(A.n_steps * 8u), 0x00020000);
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    auto ldb = [&](int64_t q) {
+        const u2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, static_cast<uint32_t>(q * 8), 0, 0);
+        return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+    };
+    const int64_t ib0 = static_cast<int64_t>(A.p_star) + MR * qa - HLR;
+    float2 pa[MR], pb[MR];
+#pragma unroll
+    for (int j = 0; j < MR; ++j) pa[j] = ldb(ib0 + CARRY + j * 64 + lane);
+#pragma unroll
+    for (int j = 0; j < MR; ++j) pb[j] = ldb(ib0 + NEW + CARRY + j * 64 + lane);
+    if (lane < CARRY) inb[lane] = ldb(ib0 + lane);
+    uint32_t s_next = s_a;
+    for (uint32_t c = 0; c < nch; c += 2) {  // chunk c + 1 >= nch: harmless work, no stores
+        ss_pipe_chunk<LR, MR, HLR>(A, inb, ring, pa, xr, pr, cr, ib0, qa, c, s_b, s_next, lane);
+        ss_pipe_chunk<LR, MR, HLR>(A, inb, ring, pb, xr, pr, cr, ib0, qa, c + 1, s_b, s_next, lane);
+    }
+}
+
 // ===================================================================== detection + coarse peak
 struct det_eval {
     float rms, metric;
@@ -1002,7 +1134,13 @@ hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
             const char* e = std::getenv("DNRP_SYNC_WPG");
             return e ? std::atoi(e) : 1;
         }();
-        if (a.step == 64 && wpg == 1)
+        // DNRP_SYNC_PIPE=0: the single-chunk-prefetch form (read per call)
+        const char* pp_e = std::getenv("DNRP_SYNC_PIPE");
+        const bool pipe = !pp_e || std::atoi(pp_e);
+        if (a.step == 64 && wpg == 1 && pipe && a.pattern % 16 == 0)
+            hipLaunchKernelGGL((sync_steps_pipe_kernel<9, 10, 24>), dim3(static_cast<uint32_t>(waves)), dim3(64),
+                               lds / SS_WPG, st, a, seg_steps, n_seg);
+        else if (a.step == 64 && wpg == 1)
             hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 16, 1>), dim3(static_cast<uint32_t>(waves)), dim3(64),
                                lds / SS_WPG, st, a, seg_steps, n_seg);
         else if (a.step == 64)
