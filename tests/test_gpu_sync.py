@@ -92,6 +92,14 @@ def test_sync_parity_wave_kernel(name, monkeypatch):
     _sync_parity(name, 20480, 4096, False)
 
 
+@pytest.mark.parametrize("name,stream_layout", [("C4", False), ("C3", True)])
+def test_sync_parity_single_prefetch(name, stream_layout, monkeypatch):
+    """The one-chunk-prefetch stream kernel (sync_steps_stream_kernel<.., 16, 1>) that the pipelined
+    kernel (sync_steps_pipe_kernel, default for 64-sample steps) replaced: DNRP_SYNC_PIPE=0."""
+    monkeypatch.setenv("DNRP_SYNC_PIPE", "0")
+    _sync_parity(name, 20480, 4096, stream_layout)
+
+
 def _sync_parity(name, S_win, chunk, stream_layout):
     import dnrp
     rng = np.random.default_rng(21)
