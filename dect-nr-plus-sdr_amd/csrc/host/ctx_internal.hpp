@@ -208,7 +208,7 @@ struct dnrp_ctx {
     pinned st_sel, st_sel2;
     // synchronisation: per (u, b) tables, step sums and reports
     std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<dnrp::host::sync_tables>> synct;
-    dbuf sy_P, sy_C, sy_res, sy_cnt, sy_spec, sy_post;
+    dbuf sy_P, sy_C, sy_res, sy_cnt, sy_spec, sy_post, sy_state, sy_pk;
     // ring-buffer gather / continuous-stream synchronisation (stream.cpp)
     dbuf ring_start, ring_win;
     pinned st_ring, st_stream;

@@ -188,6 +188,7 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     a.M = t->rs.M;
     a.delay = t->rs.delay;
     a.hl = t->rs.hl;
+    a.ct_taps = dev::sync_taps_match(t->rs.h.data(), t->rs.h.size()) ? 1u : 0u;
     a.m_star = t->m_star;
     a.p_star = t->p_star;
     a.npp = t->npp;
@@ -221,8 +222,11 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     if (!ctx->sy_P.ensure(nsa * sizeof(float)) || !ctx->sy_C.ensure(nsa * sizeof(float2)) ||
         !ctx->sy_res.ensure(size_t(n) * a.max_reports * sizeof(dev::sync_res)) || !ctx->sy_cnt.ensure(size_t(n) * 4) ||
         !ctx->sy_spec.ensure(size_t(n) * a.max_reports * (size_t(1) << a.log2_fft) * sizeof(float2)) ||
-        !ctx->sy_post.ensure(size_t(n) * a.max_reports * 8 * sizeof(float)))
+        !ctx->sy_post.ensure(size_t(n) * a.max_reports * 8 * sizeof(float)) ||
+        !ctx->sy_state.ensure(size_t(n) * sizeof(dev::sync_state)) || !ctx->sy_pk.ensure(size_t(n) * 8 * sizeof(float2)))
         return DNRP_ENOMEM;
+    a.state = ctx->sy_state.as<dev::sync_state>();
+    a.pk = ctx->sy_pk.as<float2>();
     a.spec = ctx->sy_spec.as<float2>();
     a.post = ctx->sy_post.as<float>();
     a.P = ctx->sy_P.as<float>();
@@ -236,22 +240,38 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
 #ifdef DNRP_SYNC_PROFILE
     // phase clocks of sync_detect per window (tools/sync_profile.py): averages to stderr
     static dbuf prof;
-    const bool do_prof = std::getenv("DNRP_SYNC_PROFILE") && prof.ensure(size_t(n) * 16 * 8);
+    const bool do_prof = std::getenv("DNRP_SYNC_PROFILE") && prof.ensure(size_t(n) * 32 * 8);
     a.prof = do_prof ? prof.as<unsigned long long>() : nullptr;
-    if (do_prof) HIPCHK(hipMemsetAsync(prof.p, 0, size_t(n) * 16 * 8, st));
+    if (do_prof) HIPCHK(hipMemsetAsync(prof.p, 0, size_t(n) * 32 * 8, st));
 #endif
+    // detection + coarse peak: `rounds` split rounds (detection-only workgroups, then one coarse-peak
+    // workgroup per (window, antenna) of every pending detection), then the inline form finishes what
+    // is left (windows with more detections than rounds); DNRP_SYNC_ROUNDS=0: the inline form alone.
+    // Read per call (tests switch it at run time).
+    const char* rd_e = std::getenv("DNRP_SYNC_ROUNDS");
+    const int rounds = !dev::sync_peak_ok(a) ? 0 : rd_e ? std::max(0, std::atoi(rd_e)) : 2;
+    a.first = 1;
+    for (int r = 0; r < rounds; ++r) {
+        ctx->tic("sync_detect", st);
+        if (dev::launch_sync_detect_split(a, n, st) != hipSuccess) return DNRP_EDEVICE;
+        ctx->toc("sync_detect", st);
+        a.first = 0;
+        ctx->tic("sync_peak", st);
+        if (dev::launch_sync_peak(a, n, st) != hipSuccess) return DNRP_EDEVICE;
+        ctx->toc("sync_peak", st);
+    }
     ctx->tic("sync_detect", st);
     if (dev::launch_sync_detect(a, n, st) != hipSuccess) return DNRP_EDEVICE;
     ctx->toc("sync_detect", st);
 #ifdef DNRP_SYNC_PROFILE
     if (do_prof) {
-        std::vector<unsigned long long> h(size_t(n) * 16);
+        std::vector<unsigned long long> h(size_t(n) * 32);
         HIPCHK(hipMemcpyAsync(h.data(), prof.p, h.size() * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         double acc[16] = {};
         uint32_t cnt = 0;
         for (uint32_t i = 0; i < n; ++i) {
-            const unsigned long long* r = &h[size_t(i) * 16];
+            const unsigned long long* r = &h[size_t(i) * 32];
             if (!r[0] || !r[11]) continue;
             ++cnt;
             unsigned long long prev = r[0];
@@ -265,7 +285,7 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
         for (int k = 1; k < 12; ++k) std::fprintf(stderr, " p%d=%.0f", k, cnt ? acc[k] / cnt : 0.0);
         double q[4] = {};
         for (uint32_t i = 0; i < n; ++i) {
-            const unsigned long long* r = &h[size_t(i) * 16];
+            const unsigned long long* r = &h[size_t(i) * 32];
             if (!r[8] || !r[12] || !r[13] || !r[14]) continue;
             q[0] += double(r[12] - r[8]);
             q[1] += double(r[13] - r[12]);
@@ -274,6 +294,17 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
         }
         std::fprintf(stderr, " | last peak search: sums %.0f scans %.0f metric %.0f smooth+argmax %.0f\n",
                      cnt ? q[0] / cnt : 0.0, cnt ? q[1] / cnt : 0.0, cnt ? q[2] / cnt : 0.0, cnt ? q[3] / cnt : 0.0);
+        double pq[6] = {};
+        uint32_t pc = 0;
+        for (uint32_t i = 0; i < n; ++i) {  // sync_peak_kernel of antenna 0 (split rounds)
+            const unsigned long long* r = &h[size_t(i) * 32 + 16];
+            if (!r[0] || !r[6]) continue;
+            ++pc;
+            for (int k = 0; k < 6; ++k) pq[k] += double(r[k + 1] - r[k]);
+        }
+        std::fprintf(stderr, "sync_peak phases (%u windows): resample %.0f sums %.0f scans %.0f metric %.0f met %.0f smooth+argmax %.0f\n",
+                     pc, pc ? pq[0] / pc : 0.0, pc ? pq[1] / pc : 0.0, pc ? pq[2] / pc : 0.0, pc ? pq[3] / pc : 0.0,
+                     pc ? pq[4] / pc : 0.0, pc ? pq[5] / pc : 0.0);
     }
 #endif
     ctx->tic("sync_post", st);

@@ -301,9 +301,25 @@ struct sync_args {
     float2* spec;                              // sync_fine scratch: forward spectrum per report [n * max_reports][n_fft]
     float* post;                               // [n * max_reports][8]: per antenna m_a atan2(c_a) / P (sync_post_kernel)
     uint32_t u, b;
+    // split detection (sync_detect_split / sync_peak_kernel rounds): per window the detection state
+    // machine's registers between launches, and the per-antenna coarse-peak results of the pending
+    // detection
+    struct sync_state* state;                  // [n]
+    float2* pk;                                // [n][8]: (metric, index bits) per antenna
+    uint32_t first;                            // 1: the launch starts every window from the initial state
+    uint32_t ct_taps;                          // host: the sync taps equal taps_sync_9_10 (compile-time-tap kernels)
+};
+struct sync_state {  // sync_detect_kernel's loop registers (autocorrelator_detection / _peak state)
+    uint32_t s_cur, ignore, nrep, pend;  // pend: 0 searching, 1 coarse peak pending, 2 finished
+    uint32_t sd, s_ant;
+    float s_rms, s_metric;
 };
 hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st);
 hipError_t launch_sync_detect(const sync_args& a, uint32_t n, hipStream_t st);
+hipError_t launch_sync_detect_split(const sync_args& a, uint32_t n, hipStream_t st);
+hipError_t launch_sync_peak(const sync_args& a, uint32_t n, hipStream_t st);
+bool sync_peak_ok(const sync_args& a);
+bool sync_taps_match(const float* h, size_t n);  // compiled-in 9/10 sync taps == run-time taps
 hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st);
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st);
 uint32_t sync_detect_stage(const sync_args& a);

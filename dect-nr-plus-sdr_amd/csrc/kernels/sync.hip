@@ -21,10 +21,12 @@
 //                      FFT per template, argmax over the search range, N_eff_TX, fine peak.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
+#include "taps_gen.hpp"
 
 namespace dnrp::dev {
 
@@ -593,7 +595,7 @@ __device__ void wave_scan_d2(double2* v, uint32_t n, uint32_t lane) {
 
 #ifdef DNRP_SYNC_PROFILE
 #define SYNC_STAMP(i) \
-    if (threadIdx.x == 0 && A.prof) A.prof[size_t(w) * 16 + (i)] = wall_clock64()
+    if (threadIdx.x == 0 && A.prof) A.prof[size_t(w) * 32 + (i)] = wall_clock64()
 #else
 #define SYNC_STAMP(i)
 #endif
@@ -783,7 +785,19 @@ struct sync_shared {  // block scalars, at the start of the dynamic LDS (no stat
 };
 constexpr uint32_t SYNC_SHARED_F2 = (sizeof(sync_shared) + 15) / 16 * 2;  // float2 slots, 16-B multiple
 
-template <int LR, int MR, int HLR>
+// The detection / coarse-peak state machine of one window. Two forms of the same loop:
+//  SPLIT = false  (sync_detect_kernel): the whole loop in the workgroup, the per-antenna coarse-peak
+//                 search inline (resampled STF region in LDS, 3 workgroups per CU);
+//  SPLIT = true   (the split rounds): the workgroup runs the detection conditions only and leaves at
+//                 the first detection with its state saved (pend = 1); sync_peak_kernel then runs the
+//                 coarse-peak search of that detection with one workgroup per (window, antenna), and
+//                 the next split launch resumes from the saved state with the peak results. Small
+//                 LDS (detection staging only), so many workgroups per CU; the inline form finishes
+//                 whatever the split rounds left (several detections or false alarms in one window).
+// The split form's coarse-peak search (sync_peak_kernel) evaluates the same metric expression with its
+// double sums grouped differently (prefixes on an 8-sample grid): the coarse peaks of the two forms
+// agree to double rounding; both are held to the oracle by the same GPU tests (DNRP_SYNC_ROUNDS).
+template <int LR, int MR, int HLR, bool SPLIT>
 __global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     sync_shared& sh = *reinterpret_cast<sync_shared*>(smem);
@@ -796,16 +810,19 @@ __global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_ker
     uint32_t* s_pk_idx = sh.s_pk_idx;
     const uint32_t w = blockIdx.x;
     float* taps = reinterpret_cast<float*>(smem + SYNC_SHARED_F2);
-    const uint32_t tap_f2 = (A.npp + 3) / 4 * 2;
+    const uint32_t tap_f2 = SPLIT ? 0u : (A.npp + 3) / 4 * 2;
     const uint32_t region = A.stf_len + A.D + SYNC_PAD_PEAK;
     float2* lbuf = smem + SYNC_SHARED_F2 + tap_f2;
-    float2* stage = lbuf + (region + 1) / 2 * 2;
+    float2* stage = SPLIT ? lbuf : lbuf + (region + 1) / 2 * 2;
     peak_lds pl;  // aliases the staging area (dead once the resampler has run)
     pl.ckc = reinterpret_cast<double2*>(stage);
     pl.ckp = reinterpret_cast<double*>(pl.ckc + (region + 15) / 16 + 2);
     pl.met = reinterpret_cast<float*>(pl.ckp + (region + 15) / 16 + 2);
-    if (LR > 1)
-        stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, blockDim.x);
+    // loop registers: the initial state, or the state a split launch saved
+    sync_state S0{4u, A.stf_len + A.pattern, 0u, 0u, 0u, 0u, 0.f, 0.f};
+    if (!A.first) S0 = A.state[w];
+    if (S0.pend == 2) return;  // uniform: finished in an earlier launch
+    if (!SPLIT && LR > 1) stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, blockDim.x);
     __syncthreads();
     const float* Pw = A.P + static_cast<size_t>(w) * A.n_ant * A.n_steps;
     const float2* Cw = A.Cs + static_cast<size_t>(w) * A.n_ant * A.n_steps;
@@ -816,66 +833,91 @@ __global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_ker
     const uint32_t det_p = (SYNC_THREADS + np + 3) / 4 * 4, det_c = SYNC_THREADS + nc;
     float2* dc = stage;
     float* dp = reinterpret_cast<float*>(dc + A.n_ant * det_c);
-    uint32_t nrep = 0, s_cur = 4, ignore = A.stf_len + A.pattern;
+    uint32_t nrep = S0.nrep, s_cur = S0.s_cur, ignore = S0.ignore;
+    bool resume = S0.pend == 1;  // a saved detection whose coarse peaks sync_peak_kernel has searched
     SYNC_STAMP(0);
     while (nrep < A.max_reports) {
-        // ---------------- detection: first step at or after s_cur meeting the conditions
-        if (threadIdx.x == 0) s_min = 0x7FFFFFFF;
-        __syncthreads();
-        for (uint32_t base = s_cur; base < A.n_steps; base += blockDim.x) {
-            // the batch's step values of every antenna in LDS (one coalesced round trip); steps a
-            // detection can evaluate have s - (np - 1) >= 0 (ignore >= stf_len + pattern)
-            const uint32_t nb = min(blockDim.x, A.n_steps - base);
-            const uint32_t lo_p = base >= np - 1 ? base - (np - 1) : 0u, lo_c = base >= nc - 1 ? base - (nc - 1) : 0u;
-            const uint32_t len_p = base + nb - lo_p, len_c = base + nb - lo_c;
-            for (uint32_t a = 0; a < A.n_ant; ++a) {
-                for (uint32_t i = threadIdx.x; i < len_p; i += blockDim.x) dp[a * det_p + i] = Pw[a * A.n_steps + lo_p + i];
-                for (uint32_t i = threadIdx.x; i < len_c; i += blockDim.x) dc[a * det_c + i] = Cw[a * A.n_steps + lo_c + i];
+        int sd;
+        if (resume) {
+            sd = static_cast<int>(S0.sd);
+            if (threadIdx.x == 0) {
+                s_ant = S0.s_ant;
+                s_rms = S0.s_rms;
+                s_metric = S0.s_metric;
+            }
+            if (threadIdx.x < A.n_ant) {
+                const float2 r = A.pk[size_t(w) * 8 + threadIdx.x];
+                s_pk_metric[threadIdx.x] = r.x;
+                s_pk_idx[threadIdx.x] = __float_as_uint(r.y);
             }
             __syncthreads();
-            const uint32_t s = base + threadIdx.x;
-            if (s < A.n_steps && (s + 1) * A.step >= ignore) {
+        } else {
+            // ---------------- detection: first step at or after s_cur meeting the conditions
+            if (threadIdx.x == 0) s_min = 0x7FFFFFFF;
+            __syncthreads();
+            for (uint32_t base = s_cur; base < A.n_steps; base += blockDim.x) {
+                // the batch's step values of every antenna in LDS (one coalesced round trip); steps a
+                // detection can evaluate have s - (np - 1) >= 0 (ignore >= stf_len + pattern)
+                const uint32_t nb = min(blockDim.x, A.n_steps - base);
+                const uint32_t lo_p = base >= np - 1 ? base - (np - 1) : 0u, lo_c = base >= nc - 1 ? base - (nc - 1) : 0u;
+                const uint32_t len_p = base + nb - lo_p, len_c = base + nb - lo_c;
+                for (uint32_t a = 0; a < A.n_ant; ++a) {
+                    for (uint32_t i = threadIdx.x; i < len_p; i += blockDim.x) dp[a * det_p + i] = Pw[a * A.n_steps + lo_p + i];
+                    for (uint32_t i = threadIdx.x; i < len_c; i += blockDim.x) dc[a * det_c + i] = Cw[a * A.n_steps + lo_c + i];
+                }
+                __syncthreads();
+                const uint32_t s = base + threadIdx.x;
+                if (s < A.n_steps && (s + 1) * A.step >= ignore) {
+                    for (uint32_t a = 0; a < A.n_ant; ++a) {
+                        det_eval e;
+                        if (detect_eval(A, dp + a * det_p - lo_p, dc + a * det_c - lo_c, s, e)) {
+                            atomicMin(&s_min, static_cast<int>(s));
+                            break;
+                        }
+                    }
+                }
+                __syncthreads();
+                const int found = s_min;
+                __syncthreads();
+                if (found != 0x7FFFFFFF) break;
+            }
+            sd = s_min;
+            __syncthreads();
+            if (sd == 0x7FFFFFFF) break;
+            if (threadIdx.x == 0) {
                 for (uint32_t a = 0; a < A.n_ant; ++a) {
                     det_eval e;
-                    if (detect_eval(A, dp + a * det_p - lo_p, dc + a * det_c - lo_c, s, e)) {
-                        atomicMin(&s_min, static_cast<int>(s));
+                    if (detect_eval(A, Pw + a * A.n_steps, Cw + a * A.n_steps, static_cast<uint32_t>(sd), e)) {
+                        s_ant = a;
+                        s_rms = e.rms;
+                        s_metric = e.metric;
                         break;
                     }
                 }
             }
             __syncthreads();
-            const int found = s_min;
-            __syncthreads();
-            if (found != 0x7FFFFFFF) break;
-        }
-        const int sd = s_min;
-        __syncthreads();
-        if (sd == 0x7FFFFFFF) break;
-        if (threadIdx.x == 0) {
-            for (uint32_t a = 0; a < A.n_ant; ++a) {
-                det_eval e;
-                if (detect_eval(A, Pw + a * A.n_steps, Cw + a * A.n_steps, static_cast<uint32_t>(sd), e)) {
-                    s_ant = a;
-                    s_rms = e.rms;
-                    s_metric = e.metric;
-                    break;
-                }
+            if constexpr (SPLIT) {  // leave with the detection pending: sync_peak_kernel searches its peaks
+                if (threadIdx.x == 0)
+                    A.state[w] = sync_state{s_cur, ignore, nrep, 1u, static_cast<uint32_t>(sd), s_ant, s_rms, s_metric};
+                return;
             }
         }
-        __syncthreads();
         SYNC_STAMP(1);
         s_cur = static_cast<uint32_t>(sd) + 1;
         const uint32_t det_time = s_cur * A.step, r0 = det_time - prm::SYNC_JUMP_BACK_PATTERNS * A.pattern;
         const float det_metric = s_metric;
-        // ---------------- coarse peak search over one STF on every antenna
-        const int64_t yb = static_cast<int64_t>(r0) - A.stf_len - SYNC_PAD_PEAK;
-        for (uint32_t a = 0; a < A.n_ant; ++a) {
-            const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
-            sync_resample<LR, MR, HLR>(A, x, yb, region, stage, lbuf, taps, A.det_stage);
-            SYNC_STAMP(2 + 2 * min(a, 3u));
-            peak_search(A, lbuf, region, pl, r0, red, s_pk_metric[a], s_pk_idx[a]);
-            SYNC_STAMP(3 + 2 * min(a, 3u));
+        if (!SPLIT && !resume) {
+            // ---------------- coarse peak search over one STF on every antenna
+            const int64_t yb = static_cast<int64_t>(r0) - A.stf_len - SYNC_PAD_PEAK;
+            for (uint32_t a = 0; a < A.n_ant; ++a) {
+                const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
+                sync_resample<LR, MR, HLR>(A, x, yb, region, stage, lbuf, taps, A.det_stage);
+                SYNC_STAMP(2 + 2 * min(a, 3u));
+                peak_search(A, lbuf, region, pl, r0, red, s_pk_metric[a], s_pk_idx[a]);
+                SYNC_STAMP(3 + 2 * min(a, 3u));
+            }
         }
+        resume = false;
         // post_processing_validity (autocorrelator_peak.cpp:311-364), float as in the reference
         float cm[8];
         float wsum = 0.f, msum = 0.f;
@@ -893,6 +935,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_ker
             ++nvalid;
         }
         for (uint32_t a = 0; a < A.n_ant; ++a) msum += cm[a];
+        __syncthreads();  // every thread has read the peak results before the next detection overwrites them
         if (nvalid == 0) continue;  // false alarm: detection resumes after this step
         const uint32_t wpk = static_cast<uint32_t>(roundf(wsum / msum));
         if (wpk < A.stf_len - 1) continue;  // STF would start before the chunk (asserted in the reference)
@@ -932,7 +975,279 @@ __global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_ker
     if (threadIdx.x == 0) {
         A.n_found[w] = nrep;
         for (uint32_t k = nrep; k < A.max_reports; ++k) out[k].found = 0;
+        if (A.state) A.state[w].pend = 2u;
     }
+}
+
+// ---- coarse-peak search of the split rounds (sync_peak_kernel)
+// autocorrelator_peak.cpp:145-264 for the pending detection of one (window, antenna), one workgroup
+// each. The per-sample metric is the same expression as peak_search's (exact prefix differences in
+// double, sliding by one sample), laid out for parallel latency:
+//  - the STF region is resampled straight from the window (pp_direct: each thread one polyphase block
+//    of L outputs from its W inputs by range-checked buffer loads; no staging round trips);
+//  - thread v owns the 8 positions [8v, 8v + 8): every prefix its first position needs sits on the
+//    grid z = 8g + 1 (P, the window Lw = P n_uw and stf_len are multiples of 16), so its initial sums
+//    are single LDS reads of the inclusive prefixes Q (products) and R (powers) at grid points;
+//  - the region buffer is padded by one slot per 32 samples (pidx) and the metric row by one per 8
+//    (midx), so the stride-8 accesses of a wave hit distinct banks;
+//  - the smoother's initial window sums whole 8-position blocks (blk) instead of 2 bos + 1 samples.
+// Double sums in a different order than peak_search: the metric and the smoothed maxima agree to
+// double rounding, the argmax to the same tie rules.
+__device__ __forceinline__ uint32_t pidx(uint32_t j) { return j + (j >> 5); }
+__device__ __forceinline__ uint32_t midx(uint32_t i) { return i + (i >> 3); }
+
+__host__ __device__ inline uint32_t peak8_lbuf(uint32_t region) { return (region + region / 32 + 2) / 2 * 2; }
+__host__ __device__ inline uint32_t peak8_nq(uint32_t region, uint32_t P) { return (region - P) / 8 + 2; }
+__host__ __device__ inline uint32_t peak8_nr(uint32_t region) { return region / 8 + 2; }
+__host__ __device__ inline size_t peak8_alias(uint32_t region, uint32_t P, uint32_t D) {
+    const size_t qr = size_t(peak8_nq(region, P)) * 16 + size_t(peak8_nr(region)) * 8;
+    const size_t mb = (size_t(D) + D / 8 + 2) / 2 * 2 * 4 + size_t(D / 8) * 8;
+    return qr > mb ? qr : mb;
+}
+
+// CT: the 9/10 sync resampler's taps compiled in (pp_const<taps_sync_9_10>, host-checked bit for
+// bit): immediates next to their FMAs instead of 225 run-time taps held in SGPRs (which spill)
+template <int LR, int MR, int HLR, bool CT, int NUW>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) sync_peak_kernel(sync_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    sync_shared& sh = *reinterpret_cast<sync_shared*>(smem);
+    double* red = sh.red;
+    const uint32_t w = blockIdx.x / A.n_ant, a = blockIdx.x % A.n_ant;
+    const sync_state S0 = A.state[w];
+    if (S0.pend != 1) return;  // uniform: no detection pending in this window
+#ifdef DNRP_SYNC_PROFILE
+#define PEAK_STAMP(i) \
+    if (threadIdx.x == 0 && a == 0 && A.prof) A.prof[size_t(w) * 32 + 16 + (i)] = wall_clock64()
+#else
+#define PEAK_STAMP(i)
+#endif
+    PEAK_STAMP(0);
+    const uint32_t P = A.pattern, D = A.D, yoff = A.stf_len + SYNC_PAD_PEAK;
+    const uint32_t region = A.stf_len + D + SYNC_PAD_PEAK, nprod = region - P;
+    float2* lbuf = smem + SYNC_SHARED_F2;
+    double2* Q = reinterpret_cast<double2*>(lbuf + peak8_lbuf(region));
+    double* R = reinterpret_cast<double*>(Q + peak8_nq(region, P));
+    float* met = reinterpret_cast<float*>(Q);  // after the metric pass (Q, R dead)
+    double* blk = reinterpret_cast<double*>(met + (D + D / 8 + 2) / 2 * 2);
+    const uint32_t tid = threadIdx.x, T = blockDim.x;
+    const uint32_t det_time = (S0.sd + 1) * A.step, r0 = det_time - prm::SYNC_JUMP_BACK_PATTERNS * A.pattern;
+    const int64_t yb = static_cast<int64_t>(r0) - A.stf_len - SYNC_PAD_PEAK;
+    const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
+    // ---- resampled region lb[yb + i] -> lbuf[pidx(i)] (sync_resample's outputs, bit for bit)
+    if constexpr (LR > 1) {
+        using PD = pp_direct<LR, MR, HLR>;
+        constexpr int W = PD::W;
+        const int64_t ms = A.m_star;
+        const int64_t q0 = floordiv(yb - ms, LR), q1 = floordiv(yb + region - ms + LR - 1, LR);
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(x), 0, static_cast<int>(A.S_win * 8u), 0x00020000);
+        for (int64_t q = q0 + tid; q < q1; q += T) {
+            const int64_t in0 = static_cast<int64_t>(A.p_star) + MR * q - HLR;
+            float2 xv[W];
+#pragma unroll
+            for (int i = 0; i < W; ++i) {  // outside [0, S_win): the range check returns zeros
+                typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+                const u2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, static_cast<uint32_t>((in0 + i) * 8), 0, 0);
+                xv[i] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+            }
+            float2 y[LR];
+            if constexpr (CT) {
+                static_assert(taps_sync_9_10::L == LR && taps_sync_9_10::M == MR && taps_sync_9_10::HL == HLR, "taps");
+                pp_const<taps_sync_9_10>::run(xv, y);
+            } else {
+                const float* tp = A.taps;
+                asm volatile("" : "+s"(tp));
+                PD::run(xv, (ctap_ptr)(tp), y);
+            }
+            const int64_t mb = ms + LR * q;
+#pragma unroll
+            for (int k = 0; k < LR; ++k) {
+                const int64_t idx = mb + k - yb;
+                if (idx >= 0 && idx < static_cast<int64_t>(region))
+                    lbuf[pidx(static_cast<uint32_t>(idx))] = (mb + k >= 0) ? y[k] : make_float2(0.f, 0.f);
+            }
+        }
+    } else {
+        for (uint32_t i = tid; i < region; i += T) {
+            const int64_t yy = yb + i;
+            float2 acc = make_float2(0.f, 0.f);
+            if constexpr (LR == 1) {
+                if (yy >= 0 && yy < static_cast<int64_t>(A.S_win)) acc = x[yy];
+            } else if (yy >= 0) {  // generic L/M: sync_resample's direct FIR
+                const uint64_t t = A.delay + static_cast<uint64_t>(yy) * A.M;
+                const int64_t p = static_cast<int64_t>(t / A.L);
+                const uint32_t ph = static_cast<uint32_t>(t % A.L);
+                for (uint32_t d = 0; d <= A.hl; ++d) {
+                    const int64_t q = p - d;
+                    if (q < 0 || q >= static_cast<int64_t>(A.S_win)) continue;
+                    const float h = A.taps[ph + d * A.L];
+                    acc.x = fmaf(x[q].x, h, acc.x);
+                    acc.y = fmaf(x[q].y, h, acc.y);
+                }
+            }
+            lbuf[pidx(i)] = acc;
+        }
+    }
+    __syncthreads();
+    PEAK_STAMP(1);
+    // ---- 8-sample segment sums: products prod[j] = lb[j] conj(lb[j + P]), powers |lb[j]|^2; segment
+    // g >= 1 holds j in [8g - 7, 8g], segment 0 j = 0, so the inclusive scan at g is the prefix < 8g + 1
+    const uint32_t nq = peak8_nq(region, P) - 1, nr = peak8_nr(region) - 1;
+    // all 8 loads of a segment issued together (out-of-range terms read a valid slot and are masked)
+    for (uint32_t h = tid; h < nq; h += T) {
+        const uint32_t j0 = h == 0 ? 0u : 8 * h - 7, cnt = h == 0 ? 1u : 8u;
+        float2 c[8];
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t) {
+            const uint32_t j = min(j0 + t, nprod - 1);
+            c[t] = cmulc(lbuf[pidx(j)], lbuf[pidx(j + P)]);
+        }
+        double sx = 0.0, sy = 0.0;
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t)
+            if (t < cnt && j0 + t < nprod) {
+                sx += c[t].x;
+                sy += c[t].y;
+            }
+        Q[h] = make_double2(sx, sy);
+    }
+    for (uint32_t h = tid; h < nr; h += T) {
+        const uint32_t j0 = h == 0 ? 0u : 8 * h - 7, cnt = h == 0 ? 1u : 8u;
+        float p[8];
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t) p[t] = cnorm(lbuf[pidx(min(j0 + t, region - 1))]);
+        double sp = 0.0;
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t)
+            if (t < cnt && j0 + t < region) sp += p[t];
+        R[h] = sp;
+    }
+    __syncthreads();
+    PEAK_STAMP(2);
+    const uint32_t wv = tid >> 6, lane = tid & 63u;
+    if (wv == 0) wave_scan_d2(Q, nq, lane);  // exclusive: Q[g + 1] = prefix < 8g + 1
+    if (wv == 1) {
+        const uint32_t per = (nr + 63) / 64;
+        const uint32_t b = lane * per, e = min(b + per, nr);
+        double sp = 0.0;
+        for (uint32_t i = b; i < e; ++i) sp += R[i];
+        double inc = sp;
+        for (int o = 1; o < 64; o <<= 1) {
+            const double t = __shfl_up(inc, o);
+            if (static_cast<int>(lane) >= o) inc += t;
+        }
+        double rr = inc - sp;
+        for (uint32_t i = b; i < e; ++i) {
+            const double t = R[i];
+            R[i] = rr;
+            rr += t;
+        }
+        if (lane == 63) R[nr] = inc;
+    }
+    __syncthreads();
+    PEAK_STAMP(3);
+    // ---- metric of the thread's 8 positions (registers)
+    const uint32_t Lw = P * A.n_uw, nv = D / 8;
+    const double pf = static_cast<double>(A.prefactor);
+    float m8[8];
+    if (tid < nv) {
+        // cover weights ck of the NUW + 1 prefix points (uniform); a zero weight adds an exact zero
+        float ck[NUW + 1];
+#pragma unroll
+        for (int k = 0; k <= NUW; ++k) ck[k] = (k > 0 ? A.uw[k - 1] : 0.f) - (k < NUW ? A.uw[k] : 0.f);
+        const uint32_t xb = 8 * tid;
+        const uint32_t zb = yoff + xb - P + 1 - Lw;  // = 8g + 1
+        double cr = 0.0, ci = 0.0;
+        double2 q[NUW + 1];
+#pragma unroll
+        for (int k = 0; k <= NUW; ++k) q[k] = Q[(zb + P * k - 1) / 8 + 1];
+#pragma unroll
+        for (int k = 0; k <= NUW; ++k) {
+            cr += ck[k] * q[k].x;
+            ci += ck[k] * q[k].y;
+        }
+        double pw = R[(yoff + xb) / 8 + 1] - R[(yoff + xb - A.stf_len) / 8 + 1];
+        m8[0] = static_cast<float>(pf * pf * (cr * cr + ci * ci) / (pw * pw));
+#pragma unroll
+        for (uint32_t ii = 1; ii < 8; ++ii) {
+            const uint32_t i = xb + ii;
+            const uint32_t pe = yoff + i - P - Lw;  // product index entering (y = x) for k = 0
+            float2 u[NUW + 2];
+#pragma unroll
+            for (int k = 0; k <= NUW + 1; ++k) u[k] = lbuf[pidx(pe + P * k)];
+            const float2 s1 = lbuf[pidx(yoff + i)], s0 = lbuf[pidx(yoff + i - A.stf_len)];
+#pragma unroll
+            for (int k = 0; k <= NUW; ++k) {
+                const float2 v = cmulc(u[k], u[k + 1]);
+                cr += ck[k] * static_cast<double>(v.x);
+                ci += ck[k] * static_cast<double>(v.y);
+            }
+            pw += static_cast<double>(cnorm(s1)) - static_cast<double>(cnorm(s0));
+            m8[ii] = static_cast<float>(pf * pf * (cr * cr + ci * ci) / (pw * pw));
+            if (ii & 1) asm volatile("" ::: "memory");  // two slides' loads in flight, not seven (VGPRs)
+        }
+    }
+    __syncthreads();  // Q, R read by every thread: the metric row may overwrite them
+    PEAK_STAMP(4);
+    if (tid < nv) {
+        double bs = 0.0;
+#pragma unroll
+        for (uint32_t ii = 0; ii < 8; ++ii) {
+            met[midx(8 * tid + ii)] = m8[ii];
+            bs += m8[ii];
+        }
+        blk[tid] = bs;
+    }
+    __syncthreads();
+    PEAK_STAMP(5);
+    // ---- smoother (length ns = 2 bos + 1, zero history) and last-maximum argmax
+    const uint32_t ns = (prm::SYNC_PEAK_SMOOTH_LEFT + prm::SYNC_PEAK_SMOOTH_RIGHT) * A.bos + 1;
+    double best = -1.0;
+    uint32_t bidx = 0;
+    if (tid < nv) {
+        const uint32_t xb = 8 * tid, F = (ns - 1) / 8;
+        double sm = m8[0];
+        for (uint32_t u = 1; u <= F && u <= tid; ++u) sm += blk[tid - u];
+        for (uint32_t j = 8 * F + 1; j < ns && j <= xb; ++j) sm += met[midx(xb - j)];
+#pragma unroll
+        for (uint32_t ii = 0; ii < 8; ++ii) {
+            const uint32_t i = xb + ii;
+            if (ii > 0) {
+                sm += m8[ii];
+                if (i >= ns) sm -= met[midx(i - ns)];
+            }
+            const double mean = sm / static_cast<double>(ns);
+            if (mean >= best) {
+                best = mean;
+                bidx = i;
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const uint32_t oi = __shfl_xor(bidx, o);
+        if (ob > best || (ob == best && oi > bidx)) {
+            best = ob;
+            bidx = oi;
+        }
+    }
+    if (lane == 0) {
+        red[wv] = best;  // up to 16 waves: best in red[0, 16), indices in red[16, 24)
+        reinterpret_cast<uint32_t*>(red + 16)[wv] = bidx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (uint32_t v = 1; v < (T >> 6); ++v) {
+            const double ob = red[v];
+            const uint32_t oi = reinterpret_cast<uint32_t*>(red + 16)[v];
+            if (ob > best || (ob == best && oi > bidx)) {
+                best = ob;
+                bidx = oi;
+            }
+        }
+        const uint32_t pk_idx = r0 + bidx - prm::SYNC_PEAK_SMOOTH_RIGHT * A.bos;  // metric_smoother_bos_offset_to_center_samples
+        A.pk[size_t(w) * 8 + a] = make_float2(static_cast<float>(best), __uint_as_float(pk_idx));
+    }
+    PEAK_STAMP(6);
 }
 
 // ===================================================================== coarse-peak post-processing
@@ -1166,9 +1481,83 @@ hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
     return hipGetLastError();
 }
 
+#define SYNC_DETECT_INLINE(LR, MR, HLR) sync_detect_kernel<LR, MR, HLR, false>
+#define SYNC_DETECT_SPLIT(LR, MR, HLR) sync_detect_kernel<LR, MR, HLR, true>
+#define SYNC_DISPATCH2(KERNEL, GRID, LDS)                                                  \
+    do {                                                                                   \
+        if (a.L == 9 && a.M == 10 && a.hl == 24)                                           \
+            hipLaunchKernelGGL((KERNEL(9, 10, 24)), GRID, dim3(SYNC_THREADS), LDS, st, a); \
+        else if (a.L == 9 && a.M == 10 && a.hl == 4)                                       \
+            hipLaunchKernelGGL((KERNEL(9, 10, 4)), GRID, dim3(SYNC_THREADS), LDS, st, a);  \
+        else if (a.L == 1 && a.M == 1)                                                     \
+            hipLaunchKernelGGL((KERNEL(1, 1, 0)), GRID, dim3(SYNC_THREADS), LDS, st, a);   \
+        else                                                                               \
+            hipLaunchKernelGGL((KERNEL(0, 0, 0)), GRID, dim3(SYNC_THREADS), LDS, st, a);   \
+    } while (0)
+
 hipError_t launch_sync_detect(const sync_args& a, uint32_t n, hipStream_t st) {
     const dim3 g(n);
-    SYNC_DISPATCH(sync_detect_kernel, g, sync_detect_lds(a));
+    SYNC_DISPATCH2(SYNC_DETECT_INLINE, g, sync_detect_lds(a));
+    return hipGetLastError();
+}
+
+// split round: detection conditions only (LDS: the block scalars and the detection staging)
+hipError_t launch_sync_detect_split(const sync_args& a, uint32_t n, hipStream_t st) {
+    const size_t det = a.n_ant * ((SYNC_THREADS + 4 * a.n_uw) * sizeof(float2) +
+                                  (SYNC_THREADS + 4 * a.n_pattern + 3) / 4 * 4 * sizeof(float));
+    SYNC_DISPATCH2(SYNC_DETECT_SPLIT, dim3(n), SYNC_SHARED_F2 * sizeof(float2) + det);
+    return hipGetLastError();
+}
+
+// split round: coarse-peak search of the pending detections, one workgroup per (window, antenna)
+// one thread per 8 metric positions and, up to 512 threads, one per polyphase block of the region
+// (the resampling is one load round trip per block: DNRP_PEAK_T sweep on MI355X, C4 per 4096
+// windows: 320 threads 0.98 ms, 384 0.93, 512 0.85, 576 1.20)
+uint32_t sync_peak_threads(const sync_args& a) {
+    const uint32_t region = a.stf_len + a.D + SYNC_PAD_PEAK, nblk = a.L > 1 ? region / a.L + 2 : 0u;
+    const uint32_t t = std::max({128u, (a.D / 8 + 63) / 64 * 64, std::min(512u, (nblk + 63) / 64 * 64)});
+    const char* e = std::getenv("DNRP_PEAK_T");  // experiment: a larger workgroup (multiple of 64)
+    const uint32_t te = e ? static_cast<uint32_t>(std::atoi(e)) : 0u;
+    return te >= t && te <= 1024 && te % 64 == 0 ? te : t;
+}
+
+size_t sync_peak_lds(const sync_args& a) {
+    const uint32_t region = a.stf_len + a.D + SYNC_PAD_PEAK;
+    return SYNC_SHARED_F2 * sizeof(float2) + size_t(peak8_lbuf(region)) * sizeof(float2) + peak8_alias(region, a.pattern, a.D);
+}
+
+bool sync_taps_match(const float* h, size_t n) {  // run-time sync taps == compiled-in taps, bitwise
+    if (n != static_cast<size_t>(taps_sync_9_10::N)) return false;
+    for (size_t i = 0; i < n; ++i)
+        if (__builtin_bit_cast(uint32_t, h[i]) != __builtin_bit_cast(uint32_t, taps_sync_9_10::h[i])) return false;
+    return true;
+}
+
+bool sync_peak_ok(const sync_args& a) {  // the grid layout's preconditions (every DECT geometry meets them)
+    return a.D % 8 == 0 && a.pattern % 8 == 0 && (a.stf_len + SYNC_PAD_PEAK) % 8 == 0 && a.D / 8 <= 1024 &&
+           (a.n_uw == 6 || a.n_uw == 8) && sync_peak_lds(a) <= 160 * 1024;
+}
+
+hipError_t launch_sync_peak(const sync_args& a, uint32_t n, hipStream_t st) {
+    const dim3 g(n * a.n_ant), b(sync_peak_threads(a));
+    const size_t lds = sync_peak_lds(a);
+    auto go = [&](auto nuw) {
+        constexpr int U = decltype(nuw)::value;
+        if (a.L == 9 && a.M == 10 && a.hl == 24 && a.ct_taps)
+            hipLaunchKernelGGL((sync_peak_kernel<9, 10, 24, true, U>), g, b, lds, st, a);
+        else if (a.L == 9 && a.M == 10 && a.hl == 24)
+            hipLaunchKernelGGL((sync_peak_kernel<9, 10, 24, false, U>), g, b, lds, st, a);
+        else if (a.L == 9 && a.M == 10 && a.hl == 4)
+            hipLaunchKernelGGL((sync_peak_kernel<9, 10, 4, false, U>), g, b, lds, st, a);
+        else if (a.L == 1 && a.M == 1)
+            hipLaunchKernelGGL((sync_peak_kernel<1, 1, 0, false, U>), g, b, lds, st, a);
+        else
+            hipLaunchKernelGGL((sync_peak_kernel<0, 0, 0, false, U>), g, b, lds, st, a);
+    };
+    if (a.n_uw == 6)  // n_pattern 7 (u = 1)
+        go(std::integral_constant<int, 6>{});
+    else  // n_pattern 9
+        go(std::integral_constant<int, 8>{});
     return hipGetLastError();
 }
 

@@ -130,7 +130,20 @@ def _sync_parity(name, S_win, chunk, stream_layout):
             assert int(res[w, 0]["N_eff_TX"]) == O.packet_sizes(O.psdef(*psd))["N_eff_TX"]
 
 
-def test_sync_two_packets_per_window():
+@pytest.mark.parametrize("name,rounds", [("C4", "0"), ("C4", "1"), ("tm10_u8b16", "1"), ("C3", "3")])
+def test_sync_parity_detect_rounds(name, rounds, monkeypatch):
+    """Detection + coarse peak with DNRP_SYNC_ROUNDS split rounds (detection-only workgroups, then one
+    coarse-peak workgroup per window and antenna) before the inline kernel finishes: 0 = the inline
+    kernel alone, 1 = every window's first report resolved by the inline kernel's resume path."""
+    monkeypatch.setenv("DNRP_SYNC_ROUNDS", rounds)
+    _sync_parity(name, 20480, 4096, False)
+
+
+@pytest.mark.parametrize("rounds", ["0", "1", "2", "4"])
+def test_sync_two_packets_per_window(rounds, monkeypatch):
+    """Two packets per window: with 1 or 2 split rounds the second (or the empty tail search) is left
+    to the inline kernel, with 4 the split rounds finish every window."""
+    monkeypatch.setenv("DNRP_SYNC_ROUNDS", rounds)
     import dnrp
     rng = np.random.default_rng(23)
     phy = _phy("C2")

@@ -32,7 +32,7 @@ def main():
     sc = dnrp.SyncCfg(psd[0], psd[1], n_ant, bench.sync_chunk_len(S_rx, psd, L, M), 1)
     phy.rx_sync_batch(sc, iq, chunk, S_rx, n_ant * S_rx, S_rx)
     phy.sync()
-    names = ["sync_steps", "sync_detect", "sync_post", "sync_fine"]
+    names = ["sync_steps", "sync_detect", "sync_peak", "sync_post", "sync_fine"]
     for nm in names:
         phy.kernel_time_total(nm, reset=True)
     for _ in range(reps):
