@@ -979,6 +979,68 @@ __global__ void __launch_bounds__(SYNC_THREADS) SYNC_DETECT_ATTR sync_detect_ker
     }
 }
 
+// lb[y] for y in [y0, y0 + cnt) of one antenna straight from the window (no LDS staging): each thread
+// one polyphase block of L outputs from its W inputs by range-checked buffer loads (zeros outside
+// [0, S_win)), put(i, lb[y0 + i]). sync_resample's outputs bit for bit (pp_direct / pp_const sum in
+// pp_block's order). CT: the compile-time 9/10 sync taps. No barrier.
+template <int LR, int MR, int HLR, bool CT, class PUT>
+__device__ __forceinline__ void resample_direct(const sync_args& A, const float2* x, int64_t y0, uint32_t cnt, PUT put) {
+    const uint32_t tid = threadIdx.x, T = blockDim.x;
+    if constexpr (LR > 1) {
+        using PD = pp_direct<LR, MR, HLR>;
+        constexpr int W = PD::W;
+        const int64_t ms = A.m_star;
+        const int64_t q0 = floordiv(y0 - ms, LR), q1 = floordiv(y0 + cnt - ms + LR - 1, LR);
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(x), 0, static_cast<int>(A.S_win * 8u), 0x00020000);
+        for (int64_t q = q0 + tid; q < q1; q += T) {
+            const int64_t in0 = static_cast<int64_t>(A.p_star) + MR * q - HLR;
+            float2 xv[W];
+#pragma unroll
+            for (int i = 0; i < W; ++i) {  // outside [0, S_win): the range check returns zeros
+                typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+                const u2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, static_cast<uint32_t>((in0 + i) * 8), 0, 0);
+                xv[i] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+            }
+            float2 y[LR];
+            if constexpr (CT) {
+                static_assert(taps_sync_9_10::L == LR && taps_sync_9_10::M == MR && taps_sync_9_10::HL == HLR, "taps");
+                pp_const<taps_sync_9_10>::run(xv, y);
+            } else {
+                const float* tp = A.taps;
+                asm volatile("" : "+s"(tp));
+                PD::run(xv, (ctap_ptr)(tp), y);
+            }
+            const int64_t mb = ms + LR * q;
+#pragma unroll
+            for (int k = 0; k < LR; ++k) {
+                const int64_t idx = mb + k - y0;
+                if (idx >= 0 && idx < static_cast<int64_t>(cnt))
+                    put(static_cast<uint32_t>(idx), (mb + k >= 0) ? y[k] : make_float2(0.f, 0.f));
+            }
+        }
+    } else {
+        for (uint32_t i = tid; i < cnt; i += T) {
+            const int64_t yy = y0 + i;
+            float2 acc = make_float2(0.f, 0.f);
+            if constexpr (LR == 1) {
+                if (yy >= 0 && yy < static_cast<int64_t>(A.S_win)) acc = x[yy];
+            } else if (yy >= 0) {  // generic L/M: sync_resample's direct FIR
+                const uint64_t t = A.delay + static_cast<uint64_t>(yy) * A.M;
+                const int64_t p = static_cast<int64_t>(t / A.L);
+                const uint32_t ph = static_cast<uint32_t>(t % A.L);
+                for (uint32_t d = 0; d <= A.hl; ++d) {
+                    const int64_t q = p - d;
+                    if (q < 0 || q >= static_cast<int64_t>(A.S_win)) continue;
+                    const float h = A.taps[ph + d * A.L];
+                    acc.x = fmaf(x[q].x, h, acc.x);
+                    acc.y = fmaf(x[q].y, h, acc.y);
+                }
+            }
+            put(i, acc);
+        }
+    }
+}
+
 // ---- coarse-peak search of the split rounds (sync_peak_kernel)
 // autocorrelator_peak.cpp:145-264 for the pending detection of one (window, antenna), one workgroup
 // each. The per-sample metric is the same expression as peak_search's (exact prefix differences in
@@ -1034,59 +1096,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const int64_t yb = static_cast<int64_t>(r0) - A.stf_len - SYNC_PAD_PEAK;
     const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
     // ---- resampled region lb[yb + i] -> lbuf[pidx(i)] (sync_resample's outputs, bit for bit)
-    if constexpr (LR > 1) {
-        using PD = pp_direct<LR, MR, HLR>;
-        constexpr int W = PD::W;
-        const int64_t ms = A.m_star;
-        const int64_t q0 = floordiv(yb - ms, LR), q1 = floordiv(yb + region - ms + LR - 1, LR);
-        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(x), 0, static_cast<int>(A.S_win * 8u), 0x00020000);
-        for (int64_t q = q0 + tid; q < q1; q += T) {
-            const int64_t in0 = static_cast<int64_t>(A.p_star) + MR * q - HLR;
-            float2 xv[W];
-#pragma unroll
-            for (int i = 0; i < W; ++i) {  // outside [0, S_win): the range check returns zeros
-                typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-                const u2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, static_cast<uint32_t>((in0 + i) * 8), 0, 0);
-                xv[i] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
-            }
-            float2 y[LR];
-            if constexpr (CT) {
-                static_assert(taps_sync_9_10::L == LR && taps_sync_9_10::M == MR && taps_sync_9_10::HL == HLR, "taps");
-                pp_const<taps_sync_9_10>::run(xv, y);
-            } else {
-                const float* tp = A.taps;
-                asm volatile("" : "+s"(tp));
-                PD::run(xv, (ctap_ptr)(tp), y);
-            }
-            const int64_t mb = ms + LR * q;
-#pragma unroll
-            for (int k = 0; k < LR; ++k) {
-                const int64_t idx = mb + k - yb;
-                if (idx >= 0 && idx < static_cast<int64_t>(region))
-                    lbuf[pidx(static_cast<uint32_t>(idx))] = (mb + k >= 0) ? y[k] : make_float2(0.f, 0.f);
-            }
-        }
-    } else {
-        for (uint32_t i = tid; i < region; i += T) {
-            const int64_t yy = yb + i;
-            float2 acc = make_float2(0.f, 0.f);
-            if constexpr (LR == 1) {
-                if (yy >= 0 && yy < static_cast<int64_t>(A.S_win)) acc = x[yy];
-            } else if (yy >= 0) {  // generic L/M: sync_resample's direct FIR
-                const uint64_t t = A.delay + static_cast<uint64_t>(yy) * A.M;
-                const int64_t p = static_cast<int64_t>(t / A.L);
-                const uint32_t ph = static_cast<uint32_t>(t % A.L);
-                for (uint32_t d = 0; d <= A.hl; ++d) {
-                    const int64_t q = p - d;
-                    if (q < 0 || q >= static_cast<int64_t>(A.S_win)) continue;
-                    const float h = A.taps[ph + d * A.L];
-                    acc.x = fmaf(x[q].x, h, acc.x);
-                    acc.y = fmaf(x[q].y, h, acc.y);
-                }
-            }
-            lbuf[pidx(i)] = acc;
-        }
-    }
+    resample_direct<LR, MR, HLR, CT>(A, x, yb, region, [&](uint32_t i, float2 v) { lbuf[pidx(i)] = v; });
     __syncthreads();
     PEAK_STAMP(1);
     // ---- 8-sample segment sums: products prod[j] = lb[j] conj(lb[j + P]), powers |lb[j]|^2; segment
@@ -1256,22 +1266,19 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 // detection kernel ran, so the same doubles) -> rms[a] into the report and the antenna's CFO term
 // m_a atan2(c_a) / P into A.post; sync_fine_kernel sums the terms in antenna order. One workgroup
 // per (report, antenna) instead of four serial passes inside the detection workgroup.
-template <int LR, int MR, int HLR>
+template <int LR, int MR, int HLR, bool CT>
 __global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     double* red = reinterpret_cast<double*>(smem);  // [24]
-    float* taps = reinterpret_cast<float*>(smem + 12);
-    const uint32_t tap_f2 = (A.npp + 3) / 4 * 2;
-    float2* lbuf = smem + 12 + tap_f2;
-    float2* stage = lbuf + (A.stf_len + 1) / 2 * 2;
+    float2* lbuf = smem + 12;
     const uint32_t rep = blockIdx.x / A.n_ant, a = blockIdx.x % A.n_ant, w = rep / A.max_reports;
     sync_res* rp = A.res + rep;
     const float m = rp->coarse_metric[a];
     if (!rp->found || !(m > 0.f)) return;  // uniform: the whole workgroup leaves
-    if (LR > 1) stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, blockDim.x);
-    __syncthreads();
     const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
-    sync_resample<LR, MR, HLR>(A, x, rp->coarse_local, A.stf_len, stage, lbuf, taps, A.det_stage);
+    // the STF at the coarse peak, resampled straight from the window (sync_resample's values)
+    resample_direct<LR, MR, HLR, CT>(A, x, rp->coarse_local, A.stf_len, [&](uint32_t i, float2 v) { lbuf[i] = v; });
+    __syncthreads();
     double cr = 0.0, ci = 0.0, pw = 0.0;
     const uint32_t Lw = A.pattern * A.n_uw;
     for (uint32_t i = threadIdx.x; i < A.stf_len; i += blockDim.x) {
@@ -1291,10 +1298,12 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
 }
 
 // ===================================================================== fine peak
-__global__ void __launch_bounds__(SYNC_THREADS) sync_fine_kernel(sync_args A) {
+constexpr uint32_t SYNC_FINE_THREADS = 512;  // 8 waves: the FFT passes' butterflies 2 per thread
+
+__global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    float* s_val = reinterpret_cast<float*>(smem);  // [4]
-    uint32_t* s_idx = reinterpret_cast<uint32_t*>(smem + 2);  // [4]
+    float* s_val = reinterpret_cast<float*>(smem);  // [8]
+    uint32_t* s_idx = reinterpret_cast<uint32_t*>(smem + 4);  // [8]
     sync_res* rp = A.res + blockIdx.x;
     if (!rp->found) return;
     const uint32_t w = blockIdx.x / A.max_reports;
@@ -1311,7 +1320,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_fine_kernel(sync_args A) {
         __syncthreads();
     }
     const uint32_t nf = 1u << A.log2_fft;
-    float2* xb = smem + 4;
+    float2* xb = smem + 8;
     float2* yb = xb + nf;
     // the forward spectrum is read once per template: kept in a global scratch row (L2-resident
     // while the workgroup runs) instead of a third LDS buffer, for two workgroups per CU
@@ -1324,12 +1333,19 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_fine_kernel(sync_args A) {
     const int64_t base = rp->coarse_64 - static_cast<int64_t>(A.xc_l);
     const uint32_t stage_len = A.xc_len - 1 + A.tmpl_len;
     const float2* x = A.iq + w * A.win_stride + best * A.ant_stride;
-    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) {
-        float2 v = make_float2(0.f, 0.f);
-        const int64_t q = base + i;
-        if (i < stage_len && q >= 0 && q < static_cast<int64_t>(A.S_win))
-            v = cmul(x[q], phasor(static_cast<double>(cfo_hw) * static_cast<double>(i)));
-        xb[i] = v;
+    for (uint32_t i0 = 0; i0 < nf; i0 += 8 * blockDim.x) {  // 8 loads in flight per thread
+        float2 v[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+            const uint32_t i = i0 + u * blockDim.x + threadIdx.x;
+            const int64_t q = base + i;
+            v[u] = (i < stage_len && q >= 0 && q < static_cast<int64_t>(A.S_win)) ? x[q] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+            const uint32_t i = i0 + u * blockDim.x + threadIdx.x;
+            if (i < nf) xb[i] = i < stage_len ? cmul(v[u], phasor(static_cast<double>(cfo_hw) * static_cast<double>(i))) : v[u];
+        }
     }
     __syncthreads();
     const float2* S = fft_pow2<-1>(xb, yb, A.tw_fft, A.log2_fft);
@@ -1561,19 +1577,27 @@ hipError_t launch_sync_peak(const sync_args& a, uint32_t n, hipStream_t st) {
     return hipGetLastError();
 }
 
-size_t sync_post_lds(const sync_args& a) {
-    return (12 + (a.npp + 3) / 4 * 2 + (a.stf_len + 1) / 2 * 2) * sizeof(float2) + size_t(a.det_stage) * sizeof(float2);
-}
+size_t sync_post_lds(const sync_args& a) { return (12 + (a.stf_len + 1) / 2 * 2) * sizeof(float2); }
 
 hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st) {
     const dim3 g(n * a.max_reports * a.n_ant);
-    SYNC_DISPATCH(sync_post_kernel, g, sync_post_lds(a));
+    const size_t lds = sync_post_lds(a);
+    if (a.L == 9 && a.M == 10 && a.hl == 24 && a.ct_taps)
+        hipLaunchKernelGGL((sync_post_kernel<9, 10, 24, true>), g, dim3(SYNC_THREADS), lds, st, a);
+    else if (a.L == 9 && a.M == 10 && a.hl == 24)
+        hipLaunchKernelGGL((sync_post_kernel<9, 10, 24, false>), g, dim3(SYNC_THREADS), lds, st, a);
+    else if (a.L == 9 && a.M == 10 && a.hl == 4)
+        hipLaunchKernelGGL((sync_post_kernel<9, 10, 4, false>), g, dim3(SYNC_THREADS), lds, st, a);
+    else if (a.L == 1 && a.M == 1)
+        hipLaunchKernelGGL((sync_post_kernel<1, 1, 0, false>), g, dim3(SYNC_THREADS), lds, st, a);
+    else
+        hipLaunchKernelGGL((sync_post_kernel<0, 0, 0, false>), g, dim3(SYNC_THREADS), lds, st, a);
     return hipGetLastError();
 }
 
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st) {
-    const size_t lds = (4 + 2 * (size_t(1) << a.log2_fft)) * sizeof(float2);
-    hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(SYNC_THREADS), lds, st, a);
+    const size_t lds = (8 + 2 * (size_t(1) << a.log2_fft)) * sizeof(float2);
+    hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(SYNC_FINE_THREADS), lds, st, a);
     return hipGetLastError();
 }
 
