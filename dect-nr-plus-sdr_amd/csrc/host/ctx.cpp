@@ -422,6 +422,13 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, con
     a.pin = ctx->rx_in.as<dev::rx_pkt_in>();
     a.st = ctx->rx_st.as<dev::rx_pkt_state>();
     a.Y = ctx->Y.as<float2>();
+    {  // STF per (packet, antenna) scratch (dnrp_rx_pcc_batch sizes it): cs | rms | cells
+        const size_t mb = ctx->cfg.max_batch;
+        a.stf_cs = ctx->stf_part.as<double2>();
+        a.stf_rms = reinterpret_cast<float*>(a.stf_cs + mb * 8);
+        a.stf_ys = reinterpret_cast<float2*>(a.stf_rms + mb * 8);
+        a.stf_ys_stride = 14 * ctx->cfg.b_max;
+    }
     // compile-time-tap front end (rx.hip rx_fft_wave_kernel<.., true>) where the run-time taps are
     // the generated ones bit for bit; DNRP_RX_CT=0 forces the tap-table variant (A/B)
     static const int ct_env = [] {
@@ -797,7 +804,8 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
     const size_t pbytes = size_t(n) * (ctx->rx_nsym_cap + 1) * ctx->cfg.N_TX_max * 8 * sizeof(double2);
     if (!ctx->Y.ensure(ybytes) || !ctx->snr_part.ensure(pbytes) || !ctx->rx_in.ensure(sizeof(dev::rx_pkt_in) * ctx->cfg.max_batch) ||
         !ctx->rx_st.ensure(sizeof(dev::rx_pkt_state) * ctx->cfg.max_batch) ||
-        !ctx->rx_sel.ensure(2 * sizeof(uint32_t) * ctx->cfg.max_batch))
+        !ctx->rx_sel.ensure(2 * sizeof(uint32_t) * ctx->cfg.max_batch) ||
+        !ctx->stf_part.ensure(size_t(ctx->cfg.max_batch) * 8 * (sizeof(double2) + sizeof(float) + 14 * ctx->cfg.b_max * sizeof(float2))))
         return DNRP_ENOMEM;
     auto* pin = static_cast<dev::rx_pkt_in*>(ctx->st_rxin.get(sizeof(dev::rx_pkt_in) * n));
     auto* sel = static_cast<uint32_t*>(ctx->st_sel.get(2 * sizeof(uint32_t) * n));

@@ -194,6 +194,7 @@ struct dnrp_ctx {
     dbuf pcc_seq;
     // batch scratch
     dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d, nv_d, mimo_out;
+    dbuf stf_part;  // [max_batch][8] double2 cs | [max_batch][8] float rms | [max_batch][8][14 b_max] float2 cells
     dbuf snr_part;  // [slot][n_sym_total][N_RX][8] double2: front-end DRS SNR partial sums
     uint32_t rx_mode = 0;  // DNRP_RX_MODE_* (dnrp_ctx_set_rx_mode)
     pinned st_tx, st_rxin, st_seq, st_rep;

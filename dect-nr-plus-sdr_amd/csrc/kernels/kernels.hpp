@@ -114,6 +114,12 @@ struct rx_front_args {
     uint64_t drs_neg;          // bit j: y_b_1[j] = -1 (drs.hpp)
     const uint16_t* sym_op;    // [n_sym_op]: first DRS op of symbol l, 0xFFFF: none
     uint32_t n_dops, n_drs, n_sym_op;
+    // STF front end per (packet, antenna) (rx_stf_ant_kernel -> rx_stf_kernel): per slot and antenna
+    // the cover-reverted pattern correlation sum, the RMS and the b*14 STF cells
+    double2* stf_cs;           // [slot][8]
+    float* stf_rms;            // [slot][8]
+    float2* stf_ys;            // [slot][8][stf_ys_stride]
+    uint32_t stf_ys_stride;
 };
 bool rx_fft_wave_path(const rx_front_args& a);  // launch_rx_fft takes rx_fft_wave_kernel (snr_part supported)
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);

@@ -80,52 +80,75 @@ __host__ __device__ inline uint32_t rx_stf_in(uint32_t n_stf, uint32_t Nd, uint3
     return n_in > 2 * Nd ? n_in : 2 * Nd;
 }
 
+// One workgroup per (packet, antenna): resampling + mixer of the antenna's STF, its RMS, the cover
+// revert, its pattern correlation sum and its STF cells (FFT + extraction) -> A.stf_cs / stf_rms /
+// stf_ys. The antennas of a packet run in parallel instead of in series inside one workgroup; the
+// arithmetic of each antenna is the one the single-workgroup form ran (same 256-thread loops and
+// block sums), so rx_stf_kernel's results are unchanged.
 template <int HL>
+__global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    __shared__ double red[16];
+    const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / A.N_RX), a = blockIdx.x % A.N_RX;
+    const uint32_t Nd = A.plan.N;
+    const uint32_t n_stf = A.STF_CP + Nd, n = A.b * 14;  // n: STF cells per antenna
+    float2* sbuf = smem;                                    // n_stf
+    float2* inbuf = sbuf + n_stf;                           // rx_stf_in(...)
+    float2* fa = inbuf;                                     // Nd
+    float2* fb = inbuf + Nd;                                // Nd
+    float* taps = reinterpret_cast<float*>(inbuf + rx_stf_in(n_stf, Nd, A.M, A.L, A.hl));
+    stage_copy<4>(taps, A.taps, (A.hl + 1) * A.L, threadIdx.x, blockDim.x);
+    const rx_pkt_in in = A.pin[pkt];
+    const uint32_t P = n_stf / A.n_pattern;
+    const float2* x = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in;
+    resample_block<HL>(A, x, in.fine_peak, 0, n_stf, inbuf, sbuf, taps, 0.0, in.inc0);
+    double e = 0.0, pr = 0.0, pi = 0.0;
+    for (uint32_t i = threadIdx.x; i < n_stf; i += blockDim.x) e += cnorm(sbuf[i]);
+    e = block_sum(e, red);
+    for (uint32_t i = threadIdx.x; i < n_stf; i += blockDim.x)
+        sbuf[i] = cscale(sbuf[i], k_cover_rx[min(i / A.pattern_len, 8u)]);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < (A.n_pattern - 1) * P; i += blockDim.x) {
+        const float2 c = cmulc(sbuf[i], sbuf[i + P]);
+        pr += c.x;
+        pi += c.y;
+    }
+    pr = block_sum(pr, red);
+    pi = block_sum(pi, red);
+    for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) fa[i] = sbuf[A.STF_CP + i];
+    __syncthreads();
+    const float2* F = fft_any<-1>(fa, fb, A.tw, A.plan);
+    float2* ys = A.stf_ys + (size_t(pkt) * 8 + a) * A.stf_ys_stride;
+    for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) extract_bins(A, F, &ys[w], w < n / 2 ? 4 * w : 4 * w + 4);
+    if (threadIdx.x == 0) {
+        A.stf_rms[size_t(pkt) * 8 + a] = sqrtf(static_cast<float>(e / n_stf));
+        A.stf_cs[size_t(pkt) * 8 + a] = make_double2(pr, pi);
+    }
+}
+
+// One workgroup per packet: the antennas' STF results combined (rx_synced.cpp:503-709): fractional
+// CFO re-estimate, STF zero-forcing, fractional STO, STF SNR -> the packet state.
 __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     __shared__ double red[16];
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x);
     const uint32_t Nd = A.plan.N, N = A.N_occ;
-    const uint32_t n_stf = A.STF_CP + Nd, n = A.b * 14;  // n: STF cells per antenna
-    // LDS (rx_stf_lds): the FFT's two buffers alias the resampler's input staging (free once the
-    // STF is resampled), twiddles come through the L1, and only the STF cells of every antenna's
-    // spectrum are kept: three workgroups per CU instead of one
-    float2* sbuf = smem;                                    // n_stf
-    float2* inbuf = sbuf + n_stf;                           // rx_stf_in(...)
-    float2* fa = inbuf;                                     // Nd
-    float2* fb = inbuf + Nd;                                // Nd
-    float2* Ys = inbuf + rx_stf_in(n_stf, Nd, A.M, A.L, A.hl);  // [N_RX][n]: STF cells
-    float* taps = reinterpret_cast<float*>(Ys + A.N_RX * n);
-    stage_copy<4>(taps, A.taps, (A.hl + 1) * A.L, threadIdx.x, blockDim.x);
+    const uint32_t n_stf = A.STF_CP + Nd, n = A.b * 14;
+    float2* Ys = smem;  // [N_RX][n]
+    for (uint32_t a = 0; a < A.N_RX; ++a)
+        for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) Ys[a * n + w] = A.stf_ys[(size_t(pkt) * 8 + a) * A.stf_ys_stride + w];
     const rx_pkt_in in = A.pin[pkt];
     const uint32_t P = n_stf / A.n_pattern;
     double cs_re = 0.0, cs_im = 0.0;
     rx_pkt_state S;
-
-    for (uint32_t a = 0; a < A.N_RX; ++a) {
-        const float2* x = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in;
-        resample_block<HL>(A, x, in.fine_peak, 0, n_stf, inbuf, sbuf, taps, 0.0, in.inc0);
-        double e = 0.0, pr = 0.0, pi = 0.0;
-        for (uint32_t i = threadIdx.x; i < n_stf; i += blockDim.x) e += cnorm(sbuf[i]);
-        e = block_sum(e, red);
-        if (a < 8) S.rms[a] = sqrtf(static_cast<float>(e / n_stf));
-        for (uint32_t i = threadIdx.x; i < n_stf; i += blockDim.x)
-            sbuf[i] = cscale(sbuf[i], k_cover_rx[min(i / A.pattern_len, 8u)]);
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < (A.n_pattern - 1) * P; i += blockDim.x) {
-            const float2 c = cmulc(sbuf[i], sbuf[i + P]);
-            pr += c.x;
-            pi += c.y;
-        }
-        cs_re += block_sum(pr, red);
-        cs_im += block_sum(pi, red);
-        for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) fa[i] = sbuf[A.STF_CP + i];
-        __syncthreads();
-        const float2* F = fft_any<-1>(fa, fb, A.tw, A.plan);
-        for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) extract_bins(A, F, &Ys[a * n + w], w < n / 2 ? 4 * w : 4 * w + 4);
-        __syncthreads();
+    for (uint32_t a = 0; a < A.N_RX; ++a) {  // antenna order, as the single-workgroup form summed
+        const double2 c = A.stf_cs[size_t(pkt) * 8 + a];
+        cs_re += c.x;
+        cs_im += c.y;
+        if (a < 8) S.rms[a] = A.stf_rms[size_t(pkt) * 8 + a];
     }
     for (uint32_t a = A.N_RX; a < 8; ++a) S.rms[a] = 0.f;
+    __syncthreads();
     // fractional CFO re-estimate (rx_synced.cpp:523-558) and mixer adjustment (mixer.cpp:35-39)
     const float delta = atan2f(static_cast<float>(cs_im), static_cast<float>(cs_re)) / static_cast<float>(P);
     {
@@ -289,9 +312,9 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
 
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
     const uint32_t Nd = a.plan.N, n_stf = a.STF_CP + Nd;
-    const size_t lds = (n_stf + rx_stf_in(n_stf, Nd, a.M, a.L, a.hl) + size_t(a.N_RX) * a.b * 14) * sizeof(float2) +
-                       (a.hl + 1) * a.L * sizeof(float);
-    DNRP_HL_DISPATCH(rx_stf_kernel, dim3(n), dim3(256), lds, st, a);
+    const size_t lds = (n_stf + rx_stf_in(n_stf, Nd, a.M, a.L, a.hl)) * sizeof(float2) + (a.hl + 1) * a.L * sizeof(float);
+    DNRP_HL_DISPATCH(rx_stf_ant_kernel, dim3(n * a.N_RX), dim3(256), lds, st, a);
+    hipLaunchKernelGGL(rx_stf_kernel, dim3(n), dim3(256), size_t(a.N_RX) * a.b * 14 * sizeof(float2), st, a);
     return hipGetLastError();
 }
 

@@ -394,7 +394,7 @@ __global__ void __launch_bounds__(64 * SS_WPG) sync_steps_stream_kernel(sync_arg
 // stored the same way, and a chunk completes at most 10 steps (576 outputs), so every chunk issues
 // a fixed number of memory instructions. The waits for a chunk's loads are then counted vmcnt(n)
 // with the next chunk's loads still in flight, instead of draining the queue.
-template <int LR, int MR, int HLR>
+template <int LR, int MR, int HLR, bool CT>
 __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, float2* ring, float2 (&pre)[MR],
                                               __amdgpu_buffer_rsrc_t xr, __amdgpu_buffer_rsrc_t pr,
                                               __amdgpu_buffer_rsrc_t cr, int64_t ib0, int64_t qa, uint32_t c,
@@ -418,7 +418,9 @@ __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, f
     if constexpr ((MR & 1) == 0) PD::template load<true>(inb + MR * lane, xv);
     else PD::template load<false>(inb + MR * lane, xv);
     float2 y[LR];
-    {
+    if constexpr (CT) {
+        pp_const<taps_sync_9_10>::run(xv, y);
+    } else {
         const float* tp = A.taps;
         asm volatile("" : "+s"(tp));
         PD::run(xv, (ctap_ptr)(tp), y);
@@ -476,7 +478,7 @@ __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, f
     __builtin_amdgcn_wave_barrier();
 }
 
-template <int LR, int MR, int HLR>
+template <int LR, int MR, int HLR, bool CT>
 __global__ void __launch_bounds__(64) sync_steps_pipe_kernel(sync_args A, uint32_t seg_steps, uint32_t n_seg) {
     using PD = pp_direct<LR, MR, HLR>;
     constexpr int W = PD::W, CARRY = W - MR, NEW = 64 * MR;
@@ -515,8 +517,8 @@ __global__ void __launch_bounds__(64) sync_steps_pipe_kernel(sync_args A, uint32
     if (lane < CARRY) inb[lane] = ldb(ib0 + lane);
     uint32_t s_next = s_a;
     for (uint32_t c = 0; c < nch; c += 2) {  // chunk c + 1 >= nch: harmless work, no stores
-        ss_pipe_chunk<LR, MR, HLR>(A, inb, ring, pa, xr, pr, cr, ib0, qa, c, s_b, s_next, lane);
-        ss_pipe_chunk<LR, MR, HLR>(A, inb, ring, pb, xr, pr, cr, ib0, qa, c + 1, s_b, s_next, lane);
+        ss_pipe_chunk<LR, MR, HLR, CT>(A, inb, ring, pa, xr, pr, cr, ib0, qa, c, s_b, s_next, lane);
+        ss_pipe_chunk<LR, MR, HLR, CT>(A, inb, ring, pb, xr, pr, cr, ib0, qa, c + 1, s_b, s_next, lane);
     }
 }
 
@@ -1300,10 +1302,10 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
 // ===================================================================== fine peak
 constexpr uint32_t SYNC_FINE_THREADS = 512;  // 8 waves: the FFT passes' butterflies 2 per thread
 
-__global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args A) {
+__global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    float* s_val = reinterpret_cast<float*>(smem);  // [8]
-    uint32_t* s_idx = reinterpret_cast<uint32_t*>(smem + 4);  // [8]
+    float* s_val = reinterpret_cast<float*>(smem);  // [16]
+    uint32_t* s_idx = reinterpret_cast<uint32_t*>(smem + 8);  // [16]
     sync_res* rp = A.res + blockIdx.x;
     if (!rp->found) return;
     const uint32_t w = blockIdx.x / A.max_reports;
@@ -1320,8 +1322,21 @@ __global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args 
         __syncthreads();
     }
     const uint32_t nf = 1u << A.log2_fft;
-    float2* xb = smem + 8;
-    float2* yb = xb + nf;
+    // DNRP_FINE_R16 builds: 4096 points in three radix-16 passes (wg_fft4096, padded buffers). Not the
+    // default: 0.69 vs 0.54 ms per C4 chunk for the radix-4 passes (MI355X, 512 threads)
+#ifdef DNRP_FINE_R16
+    const bool r16 = A.log2_fft == 12;
+#else
+    constexpr bool r16 = false;
+#endif
+    const uint32_t nbuf = r16 ? nf + nf / 16 : nf;
+    auto ix = [&](uint32_t i) { return r16 ? wfft_pad(i) : i; };
+    auto fft = [&](auto sign, float2* a, float2* b) -> const float2* {
+        constexpr int SG = decltype(sign)::value;
+        return r16 ? wg_fft4096<SG>(a, b, A.tw_fft) : fft_pow2<SG>(a, b, A.tw_fft, A.log2_fft);
+    };
+    float2* xb = smem + 16;
+    float2* yb = xb + nbuf;
     // the forward spectrum is read once per template: kept in a global scratch row (L2-resident
     // while the workgroup runs) instead of a third LDS buffer, for two workgroups per CU
     float2* Sb = A.spec + static_cast<size_t>(blockIdx.x) * nf;
@@ -1344,24 +1359,24 @@ __global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args 
 #pragma unroll
         for (uint32_t u = 0; u < 8; ++u) {
             const uint32_t i = i0 + u * blockDim.x + threadIdx.x;
-            if (i < nf) xb[i] = i < stage_len ? cmul(v[u], phasor(static_cast<double>(cfo_hw) * static_cast<double>(i))) : v[u];
+            if (i < nf) xb[ix(i)] = i < stage_len ? cmul(v[u], phasor(static_cast<double>(cfo_hw) * static_cast<double>(i))) : v[u];
         }
     }
     __syncthreads();
-    const float2* S = fft_pow2<-1>(xb, yb, A.tw_fft, A.log2_fft);
-    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) Sb[i] = S[i];
+    const float2* S = fft(std::integral_constant<int, -1>{}, xb, yb);
+    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) Sb[i] = S[ix(i)];
     __syncthreads();  // S's buffer is overwritten below; each thread re-reads only its own Sb[i]
     float xm[4];
     uint32_t xi[4];
     for (uint32_t k = 0; k < A.n_templates; ++k) {
         const float2* T = A.tmpl_f + static_cast<size_t>(k) * nf;
-        for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) xb[i] = cmul(Sb[i], T[i]);
+        for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) xb[ix(i)] = cmul(Sb[i], T[i]);
         __syncthreads();
-        const float2* R = fft_pow2<+1>(xb, yb, A.tw_fft, A.log2_fft);
+        const float2* R = fft(std::integral_constant<int, 1>{}, xb, yb);
         float bv = -1.f;
         uint32_t bi = 0xFFFFFFFFu;
         for (uint32_t j = threadIdx.x; j < A.xc_len; j += blockDim.x) {
-            const float m = cnorm(R[j]);
+            const float m = cnorm(R[ix(j)]);
             if (m > bv) {  // first maximum (volk_32fc_index_max_32u)
                 bv = m;
                 bi = j;
@@ -1469,8 +1484,16 @@ hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
         const char* pp_e = std::getenv("DNRP_SYNC_PIPE");
         const bool pipe = !pp_e || std::atoi(pp_e);
         if (a.step == 64 && wpg == 1 && pipe && a.pattern % 16 == 0)
-            hipLaunchKernelGGL((sync_steps_pipe_kernel<9, 10, 24>), dim3(static_cast<uint32_t>(waves)), dim3(64),
-                               lds / SS_WPG, st, a, seg_steps, n_seg);
+            {
+            // compile-time sync taps (DNRP_SYNC_CT=0: the run-time taps through SGPRs)
+            const char* ct_e = std::getenv("DNRP_SYNC_CT");
+            if (a.ct_taps && !(ct_e && !std::atoi(ct_e)))
+                hipLaunchKernelGGL((sync_steps_pipe_kernel<9, 10, 24, true>), dim3(static_cast<uint32_t>(waves)), dim3(64),
+                                   lds / SS_WPG, st, a, seg_steps, n_seg);
+            else
+                hipLaunchKernelGGL((sync_steps_pipe_kernel<9, 10, 24, false>), dim3(static_cast<uint32_t>(waves)), dim3(64),
+                                   lds / SS_WPG, st, a, seg_steps, n_seg);
+            }
         else if (a.step == 64 && wpg == 1)
             hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 16, 1>), dim3(static_cast<uint32_t>(waves)), dim3(64),
                                lds / SS_WPG, st, a, seg_steps, n_seg);
@@ -1596,8 +1619,15 @@ hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st) {
 }
 
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st) {
-    const size_t lds = (8 + 2 * (size_t(1) << a.log2_fft)) * sizeof(float2);
-    hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(SYNC_FINE_THREADS), lds, st, a);
+#ifdef DNRP_FINE_R16
+    const size_t nbuf = a.log2_fft == 12 ? 4096 + 256 : size_t(1) << a.log2_fft;
+#else
+    const size_t nbuf = size_t(1) << a.log2_fft;
+#endif
+    const size_t lds = (16 + 2 * nbuf) * sizeof(float2);
+    const char* e = std::getenv("DNRP_FINE_T");  // experiment: 256 / 512 / 1024 threads
+    const uint32_t t = e && (std::atoi(e) == 256 || std::atoi(e) == 1024) ? static_cast<uint32_t>(std::atoi(e)) : SYNC_FINE_THREADS;
+    hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(t), lds, st, a);
     return hipGetLastError();
 }
 
