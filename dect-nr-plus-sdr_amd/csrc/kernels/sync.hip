@@ -1071,8 +1071,11 @@ __host__ __device__ inline size_t peak8_alias(uint32_t region, uint32_t P, uint3
 
 // CT: the 9/10 sync resampler's taps compiled in (pp_const<taps_sync_9_10>, host-checked bit for
 // bit): immediates next to their FMAs instead of 225 run-time taps held in SGPRs (which spill)
+#ifndef DNRP_PEAK_WPE
+#define DNRP_PEAK_WPE 4  // waves per SIMD the register budget allows
+#endif
 template <int LR, int MR, int HLR, bool CT, int NUW>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) sync_peak_kernel(sync_args A) {
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(DNRP_PEAK_WPE))) sync_peak_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     sync_shared& sh = *reinterpret_cast<sync_shared*>(smem);
     double* red = sh.red;
