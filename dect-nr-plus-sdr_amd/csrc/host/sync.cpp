@@ -247,9 +247,12 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     // detection + coarse peak: `rounds` split rounds (detection-only workgroups, then one coarse-peak
     // workgroup per (window, antenna) of every pending detection), then the inline form finishes what
     // is left (windows with more detections than rounds); DNRP_SYNC_ROUNDS=0: the inline form alone.
-    // Read per call (tests switch it at run time).
+    // Default: split with several antennas (their peak searches run in parallel instead of in series:
+    // C4 4 antennas 199k -> 205k slot-pairs/s), inline with one (no series to break up, and the extra
+    // dependent launches lengthen the sync chain the host waits on: C3 654k inline vs 573k split,
+    // C2 equal; same-box A/B on MI355X). Read per call (tests switch it at run time).
     const char* rd_e = std::getenv("DNRP_SYNC_ROUNDS");
-    const int rounds = !dev::sync_peak_ok(a) ? 0 : rd_e ? std::max(0, std::atoi(rd_e)) : 2;
+    const int rounds = !dev::sync_peak_ok(a) ? 0 : rd_e ? std::max(0, std::atoi(rd_e)) : (a.n_ant > 1 ? 2 : 0);
     a.first = 1;
     for (int r = 0; r < rounds; ++r) {
         ctx->tic("sync_detect", st);
