@@ -497,10 +497,18 @@ __global__ void __launch_bounds__(64) sync_steps_pipe_kernel(sync_args A, uint32
     const int64_t ms = A.m_star;
     const int64_t qa = floordiv(m_lo - ms, LR), qb = floordiv(m_hi - 1 - ms, LR);
     const uint32_t nch = static_cast<uint32_t>((qb - qa + 64) / 64);
-    // range-checked rows: the window row (zeros outside [0, S_win)) and the step-value rows
+    // range-checked rows: the window row (zeros outside [0, S_win)) and the step-value rows. The
+    // window row's range ends at the segment's last input: the prefetches past the segment (the two
+    // chunks after its last) return zeros without a memory request (they were 6 % of the bytes)
     const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
     const size_t orow = (static_cast<size_t>(w) * A.n_ant + a) * A.n_steps;
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(x), 0, static_cast<int>(A.S_win * 8u), 0x00020000);
+    const int64_t ib0 = static_cast<int64_t>(A.p_star) + MR * qa - HLR;
+#ifdef DNRP_SYNC_NOCLAMP  // A/B build: the whole window row in range
+    const int64_t in_end = A.S_win;
+#else
+    const int64_t in_end = min<int64_t>(A.S_win, max<int64_t>(0, ib0 + int64_t(NEW) * nch + CARRY));
+#endif
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(x), 0, static_cast<int>(in_end * 8), 0x00020000);
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(A.P + orow, 0, static_cast<int>(A.n_steps * 4u), 0x00020000);
     const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(A.Cs + orow, 0, static_cast<int>(A.n_steps * 8u), 0x00020000);
     typedef uint32_t u2 __attribute__((ext_vector_type(2)));
@@ -508,7 +516,6 @@ __global__ void __launch_bounds__(64) sync_steps_pipe_kernel(sync_args A, uint32
         const u2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, static_cast<uint32_t>(q * 8), 0, 0);
         return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
     };
-    const int64_t ib0 = static_cast<int64_t>(A.p_star) + MR * qa - HLR;
     float2 pa[MR], pb[MR];
 #pragma unroll
     for (int j = 0; j < MR; ++j) pa[j] = ldb(ib0 + CARRY + j * 64 + lane);
