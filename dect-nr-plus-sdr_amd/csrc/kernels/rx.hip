@@ -85,7 +85,9 @@ __host__ __device__ inline uint32_t rx_stf_in(uint32_t n_stf, uint32_t Nd, uint3
 // stf_ys. The antennas of a packet run in parallel instead of in series inside one workgroup; the
 // arithmetic of each antenna is the one the single-workgroup form ran (same 256-thread loops and
 // block sums), so rx_stf_kernel's results are unchanged.
-template <int HL>
+__device__ __forceinline__ int64_t floordiv_rx(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+template <int HL, bool CT = false>
 __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     __shared__ double red[16];
@@ -97,11 +99,48 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
     float2* fa = inbuf;                                     // Nd
     float2* fb = inbuf + Nd;                                // Nd
     float* taps = reinterpret_cast<float*>(inbuf + rx_stf_in(n_stf, Nd, A.M, A.L, A.hl));
-    stage_copy<4>(taps, A.taps, (A.hl + 1) * A.L, threadIdx.x, blockDim.x);
+    if (!CT) stage_copy<4>(taps, A.taps, (A.hl + 1) * A.L, threadIdx.x, blockDim.x);
     const rx_pkt_in in = A.pin[pkt];
     const uint32_t P = n_stf / A.n_pattern;
     const float2* x = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in;
-    resample_block<HL>(A, x, in.fine_peak, 0, n_stf, inbuf, sbuf, taps, 0.0, in.inc0);
+    if (CT) {
+        // compile-time 9/10 taps: the span staged once, then thread q one polyphase block of 9 outputs
+        // from its 33-input window in registers (each tap an immediate, summed newest input first as
+        // resample_block does), mixed with a phasor at the block start stepped by the increment
+        using PD = pp_direct<9, 10, 24>;
+        constexpr int W = PD::W;
+        const int64_t ms = A.m_star;
+        const int64_t q0 = floordiv_rx(0 - ms, 9), q1 = floordiv_rx(static_cast<int64_t>(n_stf) - ms + 8, 9);
+        const int64_t in0 = static_cast<int64_t>(A.p_star) + 10 * q0 - 24;  // relative to the fine peak
+        const uint32_t n_in = static_cast<uint32_t>(10 * (q1 - 1 - q0) + W);
+        stage_span_lo<8>(inbuf, x + in.fine_peak, in0, n_in, in.fine_peak < 0 ? -in.fine_peak : 0,
+                         static_cast<int64_t>(A.S_in) - in.fine_peak, threadIdx.x, blockDim.x);
+        __syncthreads();
+        const float2 step1 = phasor(in.inc0);
+        for (int64_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+            float2 xv[W];
+            PD::template load<true>(inbuf + 10 * (q - q0), xv);
+            const int64_t mb = ms + 9 * q;
+            float2 r = phasor(static_cast<double>(mb) * in.inc0);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const int o = (k * 10) / 9, ph = (k * 10) % 9;
+                float ar = 0.f, ai = 0.f;
+#pragma unroll
+                for (int d = 0; d <= 24; ++d) {
+                    const float h = taps_rx_9_10::h[ph + d * 9];
+                    ar = fmaf(xv[24 + o - d].x, h, ar);
+                    ai = fmaf(xv[24 + o - d].y, h, ai);
+                }
+                const int64_t m = mb + k;
+                if (m >= 0 && m < static_cast<int64_t>(n_stf)) sbuf[m] = cmul(make_float2(ar, ai), r);
+                r = cmul(r, step1);
+            }
+        }
+        __syncthreads();
+    } else {
+        resample_block<HL>(A, x, in.fine_peak, 0, n_stf, inbuf, sbuf, taps, 0.0, in.inc0);
+    }
     double e = 0.0, pr = 0.0, pi = 0.0;
     for (uint32_t i = threadIdx.x; i < n_stf; i += blockDim.x) e += cnorm(sbuf[i]);
     e = block_sum(e, red);
@@ -313,7 +352,12 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
     const uint32_t Nd = a.plan.N, n_stf = a.STF_CP + Nd;
     const size_t lds = (n_stf + rx_stf_in(n_stf, Nd, a.M, a.L, a.hl)) * sizeof(float2) + (a.hl + 1) * a.L * sizeof(float);
-    DNRP_HL_DISPATCH(rx_stf_ant_kernel, dim3(n * a.N_RX), dim3(256), lds, st, a);
+    // DNRP_RX_STF_CT=0: the table-tap resampler (resample_block) also for compiled-in taps (A/B)
+    const char* ct_e = std::getenv("DNRP_RX_STF_CT");
+    if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24 && !(ct_e && !std::atoi(ct_e)))
+        hipLaunchKernelGGL((rx_stf_ant_kernel<24, true>), dim3(n * a.N_RX), dim3(256), lds, st, a);
+    else
+        DNRP_HL_DISPATCH(rx_stf_ant_kernel, dim3(n * a.N_RX), dim3(256), lds, st, a);
     hipLaunchKernelGGL(rx_stf_kernel, dim3(n), dim3(256), size_t(a.N_RX) * a.b * 14 * sizeof(float2), st, a);
     return hipGetLastError();
 }
