@@ -377,7 +377,7 @@ __host__ __device__ inline uint32_t rxw_region(uint32_t L, uint32_t M, uint32_t 
 
 // WPG symbols (= wavefronts) per workgroup: the compile-time-tap path shares nothing between its
 // waves, so it can run one wave per workgroup and free each wave's LDS region when that wave retires
-template <int LR, int MR, int HLR, bool CT, int WPG = RXW_SYMS>
+template <int LR, int MR, int HLR, bool CT, int WPG = RXW_SYMS, bool RT = false>
 __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu(4))) rx_fft_wave_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     using PB = pp_block<LR, MR, HLR>;
@@ -414,6 +414,11 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
         const auto* sop = reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(reinterpret_cast<uintptr_t>(A.sym_op));
         so = (sop[l >> 1] >> (16 * (l & 1u))) & 0xFFFFu;
     }
+    float2 w1 = make_float2(1.f, 0.f), wl = w1;
+    if constexpr (RT) {  // the FFT's two lane twiddles, in flight with the staging loads
+        w1 = wfft_tw<-1>(A.tw, 4 * (lane & 15u));
+        wl = wfft_tw<-1>(A.tw, lane);
+    }
     if (active) stage_span_lo<20>(R, src, sp.in0, sp.n_in, q_lo, q_hi, lane, 64);
     if constexpr (CT)
         __builtin_amdgcn_wave_barrier();  // only the wave's own staging
@@ -425,10 +430,10 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
     if constexpr (CT) {
         rx_resample_ct<LR, MR, HLR>(A, in, S, sp, R, lane);
         // one instantiation of the (large, unrolled) FFT for both kinds of symbol: instruction cache
-        rx_fft_bins(A, S, R, lane, [&](uint32_t k, float2 v) {
+        rx_fft_bins<RT>(A, S, R, lane, [&](uint32_t k, float2 v) {
             Yrow[k] = v;
             if (drs) R[k] = v;
-        });
+        }, w1, wl);
         if (drs) {
             __builtin_amdgcn_wave_barrier();
             rx_drs_partials(A, pkt, a, l, so, R, lane);
@@ -508,7 +513,17 @@ hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
             }();
             const size_t lds1 = size_t(rxw_region(9, 10, W)) * sizeof(float2);
             auto grid = [&](uint32_t per) { return dim3(n * a.N_RX * ((a.sym_count + per - 1) / per)); };
-            if (wpg == 1)
+            // the FFT with two lane twiddles loaded with the staging (wave_fft1024_rt) instead of 27
+            // inside its passes: 92 instead of 99 VGPRs (17 waves per CU, the LDS limit, not 16) and
+            // no twiddle-load latency in the passes (same box: PDC launch 5.44 -> 5.30 ms per C4
+            // chunk); DNRP_RX_FFT_RT=0: the table-twiddle FFT
+            static const int rt = [] {
+                const char* e = std::getenv("DNRP_RX_FFT_RT");
+                return e ? std::atoi(e) : 1;
+            }();
+            if (wpg == 1 && rt)
+                hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 1, true>), grid(1), dim3(64), lds1, st, a);
+            else if (wpg == 1)
                 hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 1>), grid(1), dim3(64), lds1, st, a);
             else if (wpg == 2)
                 hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 2>), grid(2), dim3(128), 2 * lds1, st, a);

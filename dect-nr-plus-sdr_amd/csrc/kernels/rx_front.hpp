@@ -75,14 +75,19 @@ __device__ __forceinline__ void rx_resample_ct(const rx_front_args& A, const rx_
 // amplitude sqrt(N_b_OCC)/N_b_DFT_os, STO derotation exp(j sto_inc (k - N/2)) by two running
 // phasors stepped by 64 bins. put(k, value) for every k in [0, N_b_OCC]; R is free again when
 // put is called (all exchange reads have completed).
-template <class Put>
+// RT: wave_fft1024_rt with the lane's two twiddles w1 = W^(4 (lane & 15)), wl = W^lane loaded by the
+// caller (e.g. before its input staging) instead of 27 twiddle loads inside the passes
+template <bool RT = false, class Put>
 __device__ __forceinline__ void rx_fft_bins(const rx_front_args& A, const rx_pkt_state& S, float2* R, uint32_t lane,
-                                            Put&& put) {
+                                            Put&& put, float2 w1 = float2{}, float2 wl = float2{}) {
     float2 v[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = R[lane + 64 * m];
     __builtin_amdgcn_wave_barrier();
-    wave_fft1024<-1>(v, R, A.tw, lane);  // twiddles through the L1 (8 KB, every wave)
+    if constexpr (RT)
+        wave_fft1024_rt<-1>(v, R, w1, wl, lane);
+    else
+        wave_fft1024<-1>(v, R, A.tw, lane);  // twiddles through the L1 (8 KB, every wave)
     __builtin_amdgcn_wave_barrier();
     const uint32_t N = A.N_occ;
     const float2 s64 = phasor(64.0 * S.sto_inc);
