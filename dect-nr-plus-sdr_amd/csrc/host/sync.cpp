@@ -216,7 +216,7 @@ extern "C" int dnrp_rx_sync_batch(dnrp_ctx* ctx, const dnrp_sync_cfg* sc, uint32
     a.u = sc->u;
     a.b = sc->b;
     a.det_stage = dev::sync_detect_stage(a);
-    if (dev::sync_detect_lds(a) > 160 * 1024 || (16 + 2 * ((size_t(1) << a.log2_fft) + (a.log2_fft == 12 ? 256 : 0))) * sizeof(float2) > 160 * 1024)
+    if (dev::sync_detect_lds(a) > 160 * 1024 || (16 + 2 * (size_t(1) << a.log2_fft)) * sizeof(float2) > 160 * 1024)
         return DNRP_EUNSUPPORTED;
     const size_t nsa = size_t(n) * a.n_ant * a.n_steps;
     if (!ctx->sy_P.ensure(nsa * sizeof(float)) || !ctx->sy_C.ensure(nsa * sizeof(float2)) ||

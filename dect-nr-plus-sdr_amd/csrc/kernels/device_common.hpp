@@ -444,38 +444,6 @@ __device__ __forceinline__ void dft16(float2 (&v)[16]) {
     for (int k = 0; k < 16; ++k) v[k] = o[k];
 }
 
-// Workgroup FFT of N = 4096 = 16^3 points in three radix-16 Stockham passes (instead of six
-// radix-4 ones): pass s (Ns = 16^s) butterfly j < 256 reads x[j + 256 r], r = 0..15, twiddles
-// W_(16 Ns)^(r k) (k = j mod Ns) from the forward table tw of N entries, dft16, writes
-// y[(j - k) 16 + k + Ns m]. Buffers indexed through wfft_pad (>= N + N/16 float2 each: pass 1's
-// stride-16 writes on distinct banks). Any blockDim.x (multiple of 64); ends with a barrier.
-// Returns the buffer holding X in natural order (index wfft_pad(k)).
-template <int SIGN>
-__device__ float2* wg_fft4096(float2* x, float2* y, const float2* tw) {
-    for (uint32_t Ns = 1; Ns < 4096; Ns *= 16) {
-        for (uint32_t j = threadIdx.x; j < 256; j += blockDim.x) {
-            const uint32_t k = j & (Ns - 1);
-            float2 v[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = x[wfft_pad(j + 256 * r)];
-            if (Ns > 1) {
-                const uint32_t e = k * (4096 / (16 * Ns));
-#pragma unroll
-                for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], wfft_tw<SIGN>(tw, r * e));
-            }
-            dft16<SIGN>(v);
-            const uint32_t ob = (j - k) * 16 + k;
-#pragma unroll
-            for (int m = 0; m < 16; ++m) y[wfft_pad(ob + Ns * m)] = v[m];
-        }
-        __syncthreads();
-        float2* t = x;
-        x = y;
-        y = t;
-    }
-    return x;
-}
-
 template <int SIGN>
 __device__ __forceinline__ void wave_fft1024(float2 (&v)[16], float2* xb, const float2* tw, uint32_t lane) {
     // pass 1: radix 16, Ns = 1, butterfly j = lane on x[j + 64 r] -> y[16 j + k]

@@ -1310,6 +1310,40 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
 }
 
 // ===================================================================== fine peak
+// In-place radix-4 decimation-in-time FFT of N = 4^p points on one buffer: the input sits at base-4
+// digit-reversed positions, pass s (quarter Q = 4^(s/2)) combines four Q-point transforms per
+// butterfly with the twiddles W_N^(r k N/(4Q)) of fft_pow2's pass s, output in natural order. Every
+// butterfly reads and writes its own four slots (no second buffer: half the LDS of fft_pow2).
+template <int SIGN>
+__device__ void fft_r4_inplace(float2* x, const float2* tw, uint32_t log2N) {
+    const uint32_t NB = 1u << (log2N - 2);
+    for (uint32_t s = 0; s < log2N; s += 2) {
+        const uint32_t Q = 1u << s, tsh = log2N - s - 2;
+        for (uint32_t j = threadIdx.x; j < NB; j += blockDim.x) {
+            const uint32_t k = j & (Q - 1u), i0 = ((j >> s) << (s + 2)) + k;
+            float2 a0 = x[i0], a1 = x[i0 + Q], a2 = x[i0 + 2 * Q], a3 = x[i0 + 3 * Q];
+            if (s) {
+                const uint32_t e = k << tsh;
+                float2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
+                if (SIGN > 0) {
+                    w1 = cconj(w1);
+                    w2 = cconj(w2);
+                    w3 = cconj(w3);
+                }
+                a1 = cmul(a1, w1);
+                a2 = cmul(a2, w2);
+                a3 = cmul(a3, w3);
+            }
+            dft4<SIGN>(a0, a1, a2, a3);
+            x[i0] = a0;
+            x[i0 + Q] = a1;
+            x[i0 + 2 * Q] = a2;
+            x[i0 + 3 * Q] = a3;
+        }
+        __syncthreads();
+    }
+}
+
 constexpr uint32_t SYNC_FINE_THREADS = 512;  // 8 waves: the FFT passes' butterflies 2 per thread
 
 __global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
@@ -1332,19 +1366,23 @@ __global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
         __syncthreads();
     }
     const uint32_t nf = 1u << A.log2_fft;
-    // DNRP_FINE_R16 builds: 4096 points in three radix-16 passes (wg_fft4096, padded buffers). Not the
-    // default: 0.69 vs 0.54 ms per C4 chunk for the radix-4 passes (MI355X, 512 threads)
-#ifdef DNRP_FINE_R16
-    const bool r16 = A.log2_fft == 12;
-#else
-    constexpr bool r16 = false;
-#endif
-    const uint32_t nbuf = r16 ? nf + nf / 16 : nf;
-    auto ix = [&](uint32_t i) { return r16 ? wfft_pad(i) : i; };
+    // power-of-4 sizes (4096 for C3 / C4): in-place radix-4 DIT on one LDS buffer, the inputs stored
+    // at their base-4 digit-reversed positions (ip); otherwise the two-buffer Stockham passes
+    const bool ip = (A.log2_fft & 1u) == 0;
+    auto ix = [&](uint32_t i) {
+        if (!ip) return i;
+        const uint32_t b = __brev(i) >> (32 - A.log2_fft);
+        return ((b & 0x55555555u) << 1) | ((b >> 1) & 0x55555555u);
+    };
     auto fft = [&](auto sign, float2* a, float2* b) -> const float2* {
         constexpr int SG = decltype(sign)::value;
-        return r16 ? wg_fft4096<SG>(a, b, A.tw_fft) : fft_pow2<SG>(a, b, A.tw_fft, A.log2_fft);
+        if (ip) {
+            fft_r4_inplace<SG>(a, A.tw_fft, A.log2_fft);
+            return a;
+        }
+        return fft_pow2<SG>(a, b, A.tw_fft, A.log2_fft);
     };
+    const uint32_t nbuf = nf;
     float2* xb = smem + 16;
     float2* yb = xb + nbuf;
     // the forward spectrum is read once per template: kept in a global scratch row (L2-resident
@@ -1374,7 +1412,7 @@ __global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
     }
     __syncthreads();
     const float2* S = fft(std::integral_constant<int, -1>{}, xb, yb);
-    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) Sb[i] = S[ix(i)];
+    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) Sb[i] = S[i];
     __syncthreads();  // S's buffer is overwritten below; each thread re-reads only its own Sb[i]
     float xm[4];
     uint32_t xi[4];
@@ -1386,7 +1424,7 @@ __global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
         float bv = -1.f;
         uint32_t bi = 0xFFFFFFFFu;
         for (uint32_t j = threadIdx.x; j < A.xc_len; j += blockDim.x) {
-            const float m = cnorm(R[ix(j)]);
+            const float m = cnorm(R[j]);
             if (m > bv) {  // first maximum (volk_32fc_index_max_32u)
                 bv = m;
                 bi = j;
@@ -1629,12 +1667,8 @@ hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st) {
 }
 
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st) {
-#ifdef DNRP_FINE_R16
-    const size_t nbuf = a.log2_fft == 12 ? 4096 + 256 : size_t(1) << a.log2_fft;
-#else
     const size_t nbuf = size_t(1) << a.log2_fft;
-#endif
-    const size_t lds = (16 + 2 * nbuf) * sizeof(float2);
+    const size_t lds = (16 + ((a.log2_fft & 1u) == 0 ? 1 : 2) * nbuf) * sizeof(float2);  // in-place: one buffer
     const char* e = std::getenv("DNRP_FINE_T");  // experiment: 256 / 512 / 1024 threads
     const uint32_t t = e && (std::atoi(e) == 256 || std::atoi(e) == 1024) ? static_cast<uint32_t>(std::atoi(e)) : SYNC_FINE_THREADS;
     hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(t), lds, st, a);
