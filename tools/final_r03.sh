@@ -10,9 +10,9 @@ bash tools/gpu_tests.sh
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > $out/smoke.log 2>&1
 tail -1 $out/smoke.log
 timeout -k 10 400 python bench.py > $out/bench_default.log 2>&1
-tail -1 $out/bench_default.log > $out/bench_default.json
+grep '^{"metric"' $out/bench_default.log | tail -1 > $out/bench_default.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- python3 bench.py --no-cpu-baseline > $out/bench_rocprof.log 2>&1
-tail -1 $out/bench_rocprof.log > $out/bench_under_rocprof.json
+grep '^{"metric"' $out/bench_rocprof.log | tail -1 > $out/bench_under_rocprof.json
 stats=$(find $out/trace -name "*kernel_stats.csv" | head -1)
 trace=$(find $out/trace -name "*kernel_trace.csv" | head -1)
 cp $stats $out/kernel_stats.csv
