@@ -444,6 +444,46 @@ __device__ __forceinline__ void dft16(float2 (&v)[16]) {
     for (int k = 0; k < 16; ++k) v[k] = o[k];
 }
 
+// In-place radix-4 decimation-in-time FFT of N = 4^p points on one buffer: the input sits at base-4
+// digit-reversed positions, pass s (quarter Q = 4^(s/2)) combines four Q-point transforms per
+// butterfly with the twiddles W_N^(r k N/(4Q)) of fft_pow2's pass s, output in natural order. Every
+// butterfly reads and writes its own four slots (no second buffer: half the LDS of fft_pow2).
+template <int SIGN>
+__device__ void fft_r4_inplace(float2* x, const float2* tw, uint32_t log2N) {
+    const uint32_t NB = 1u << (log2N - 2);
+    for (uint32_t s = 0; s < log2N; s += 2) {
+        const uint32_t Q = 1u << s, tsh = log2N - s - 2;
+        for (uint32_t j = threadIdx.x; j < NB; j += blockDim.x) {
+            const uint32_t k = j & (Q - 1u), i0 = ((j >> s) << (s + 2)) + k;
+            float2 a0 = x[i0], a1 = x[i0 + Q], a2 = x[i0 + 2 * Q], a3 = x[i0 + 3 * Q];
+            if (s) {
+                const uint32_t e = k << tsh;
+                float2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
+                if (SIGN > 0) {
+                    w1 = cconj(w1);
+                    w2 = cconj(w2);
+                    w3 = cconj(w3);
+                }
+                a1 = cmul(a1, w1);
+                a2 = cmul(a2, w2);
+                a3 = cmul(a3, w3);
+            }
+            dft4<SIGN>(a0, a1, a2, a3);
+            x[i0] = a0;
+            x[i0 + Q] = a1;
+            x[i0 + 2 * Q] = a2;
+            x[i0 + 3 * Q] = a3;
+        }
+        __syncthreads();
+    }
+}
+
+// base-4 digit reversal of the log2N / 2 digits of i (fft_r4_inplace's input position)
+__device__ __forceinline__ uint32_t rev4(uint32_t i, uint32_t log2N) {
+    const uint32_t b = __brev(i) >> (32 - log2N);
+    return ((b & 0x55555555u) << 1) | ((b >> 1) & 0x55555555u);
+}
+
 template <int SIGN>
 __device__ __forceinline__ void wave_fft1024(float2 (&v)[16], float2* xb, const float2* tw, uint32_t lane) {
     // pass 1: radix 16, Ns = 1, butterfly j = lane on x[j + 64 r] -> y[16 j + k]

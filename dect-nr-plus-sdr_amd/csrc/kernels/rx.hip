@@ -86,6 +86,8 @@ __host__ __device__ inline uint32_t rx_stf_in(uint32_t n_stf, uint32_t Nd, uint3
 // arithmetic of each antenna is the one the single-workgroup form ran (same 256-thread loops and
 // block sums), so rx_stf_kernel's results are unchanged.
 __device__ __forceinline__ int64_t floordiv_rx(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+// float2 slots of rx_stf_ant_kernel's compact area: the 9/10 input span of n_stf outputs (upper bound)
+__host__ __device__ inline uint32_t rx_stf_area(uint32_t n_stf) { return ((n_stf + 18) * 10) / 9 + 33 + 10 + 2; }
 
 template <int HL, bool CT = false>
 __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
@@ -94,6 +96,11 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / A.N_RX), a = blockIdx.x % A.N_RX;
     const uint32_t Nd = A.plan.N;
     const uint32_t n_stf = A.STF_CP + Nd, n = A.b * 14;  // n: STF cells per antenna
+    // compact layout (compiled-in taps, N a power of 4): one area holds the input span at its top and
+    // the resampled STF from its bottom (a block's outputs stay below every window: 9 outputs per 10
+    // inputs), and the FFT runs in place on its first N slots; otherwise sbuf | inbuf (FFT buffers) | taps
+    const uint32_t lgN = 31u - __clz(Nd);
+    const bool compact = CT && (lgN & 1u) == 0 && A.STF_CP >= Nd;  // the host sizes the LDS by the same test
     float2* sbuf = smem;                                    // n_stf
     float2* inbuf = sbuf + n_stf;                           // rx_stf_in(...)
     float2* fa = inbuf;                                     // Nd
@@ -113,13 +120,16 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
         const int64_t q0 = floordiv_rx(0 - ms, 9), q1 = floordiv_rx(static_cast<int64_t>(n_stf) - ms + 8, 9);
         const int64_t in0 = static_cast<int64_t>(A.p_star) + 10 * q0 - 24;  // relative to the fine peak
         const uint32_t n_in = static_cast<uint32_t>(10 * (q1 - 1 - q0) + W);
-        stage_span_lo<8>(inbuf, x + in.fine_peak, in0, n_in, in.fine_peak < 0 ? -in.fine_peak : 0,
+        float2* span = compact ? smem + ((rx_stf_area(n_stf) - n_in) & ~1u) : inbuf;
+        stage_span_lo<8>(span, x + in.fine_peak, in0, n_in, in.fine_peak < 0 ? -in.fine_peak : 0,
                          static_cast<int64_t>(A.S_in) - in.fine_peak, threadIdx.x, blockDim.x);
         __syncthreads();
         const float2 step1 = phasor(in.inc0);
-        for (int64_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+        for (int64_t q = q0 + threadIdx.x, rd = 0; rd == 0 || q < q1; q += blockDim.x, ++rd) {  // round 0: all threads
             float2 xv[W];
-            PD::template load<true>(inbuf + 10 * (q - q0), xv);
+            PD::template load<true>(span + 10 * min<int64_t>(q - q0, q1 - 1 - q0), xv);
+            if (rd == 0) __syncthreads();  // every first-round window read before outputs overwrite the area
+            if (q >= q1) continue;
             const int64_t mb = ms + 9 * q;
             float2 r = phasor(static_cast<double>(mb) * in.inc0);
 #pragma unroll
@@ -154,9 +164,17 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
     }
     pr = block_sum(pr, red);
     pi = block_sum(pi, red);
-    for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) fa[i] = sbuf[A.STF_CP + i];
-    __syncthreads();
-    const float2* F = fft_any<-1>(fa, fb, A.tw, A.plan);
+    const float2* F;
+    if (compact) {  // in place on sbuf[0, N): the inputs sbuf[STF_CP + i] (STF_CP >= N) at digit-reversed slots
+        for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) sbuf[rev4(i, lgN)] = sbuf[A.STF_CP + i];
+        __syncthreads();
+        fft_r4_inplace<-1>(sbuf, A.tw, lgN);
+        F = sbuf;
+    } else {
+        for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) fa[i] = sbuf[A.STF_CP + i];
+        __syncthreads();
+        F = fft_any<-1>(fa, fb, A.tw, A.plan);
+    }
     float2* ys = A.stf_ys + (size_t(pkt) * 8 + a) * A.stf_ys_stride;
     for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) extract_bins(A, F, &ys[w], w < n / 2 ? 4 * w : 4 * w + 4);
     if (threadIdx.x == 0) {
@@ -354,8 +372,12 @@ hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
     const size_t lds = (n_stf + rx_stf_in(n_stf, Nd, a.M, a.L, a.hl)) * sizeof(float2) + (a.hl + 1) * a.L * sizeof(float);
     // DNRP_RX_STF_CT=0: the table-tap resampler (resample_block) also for compiled-in taps (A/B)
     const char* ct_e = std::getenv("DNRP_RX_STF_CT");
+    uint32_t lgN = 0;
+    while ((1u << lgN) < Nd) ++lgN;
+    const bool compact = lgN % 2 == 0 && a.STF_CP >= Nd;
     if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24 && !(ct_e && !std::atoi(ct_e)))
-        hipLaunchKernelGGL((rx_stf_ant_kernel<24, true>), dim3(n * a.N_RX), dim3(256), lds, st, a);
+        hipLaunchKernelGGL((rx_stf_ant_kernel<24, true>), dim3(n * a.N_RX), dim3(256),
+                           compact ? size_t(std::max(rx_stf_area(n_stf), n_stf)) * sizeof(float2) : lds, st, a);
     else
         DNRP_HL_DISPATCH(rx_stf_ant_kernel, dim3(n * a.N_RX), dim3(256), lds, st, a);
     hipLaunchKernelGGL(rx_stf_kernel, dim3(n), dim3(256), size_t(a.N_RX) * a.b * 14 * sizeof(float2), st, a);

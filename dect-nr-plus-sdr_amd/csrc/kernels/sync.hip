@@ -1310,40 +1310,6 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
 }
 
 // ===================================================================== fine peak
-// In-place radix-4 decimation-in-time FFT of N = 4^p points on one buffer: the input sits at base-4
-// digit-reversed positions, pass s (quarter Q = 4^(s/2)) combines four Q-point transforms per
-// butterfly with the twiddles W_N^(r k N/(4Q)) of fft_pow2's pass s, output in natural order. Every
-// butterfly reads and writes its own four slots (no second buffer: half the LDS of fft_pow2).
-template <int SIGN>
-__device__ void fft_r4_inplace(float2* x, const float2* tw, uint32_t log2N) {
-    const uint32_t NB = 1u << (log2N - 2);
-    for (uint32_t s = 0; s < log2N; s += 2) {
-        const uint32_t Q = 1u << s, tsh = log2N - s - 2;
-        for (uint32_t j = threadIdx.x; j < NB; j += blockDim.x) {
-            const uint32_t k = j & (Q - 1u), i0 = ((j >> s) << (s + 2)) + k;
-            float2 a0 = x[i0], a1 = x[i0 + Q], a2 = x[i0 + 2 * Q], a3 = x[i0 + 3 * Q];
-            if (s) {
-                const uint32_t e = k << tsh;
-                float2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
-                if (SIGN > 0) {
-                    w1 = cconj(w1);
-                    w2 = cconj(w2);
-                    w3 = cconj(w3);
-                }
-                a1 = cmul(a1, w1);
-                a2 = cmul(a2, w2);
-                a3 = cmul(a3, w3);
-            }
-            dft4<SIGN>(a0, a1, a2, a3);
-            x[i0] = a0;
-            x[i0 + Q] = a1;
-            x[i0 + 2 * Q] = a2;
-            x[i0 + 3 * Q] = a3;
-        }
-        __syncthreads();
-    }
-}
-
 constexpr uint32_t SYNC_FINE_THREADS = 512;  // 8 waves: the FFT passes' butterflies 2 per thread
 
 __global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
@@ -1369,11 +1335,7 @@ __global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
     // power-of-4 sizes (4096 for C3 / C4): in-place radix-4 DIT on one LDS buffer, the inputs stored
     // at their base-4 digit-reversed positions (ip); otherwise the two-buffer Stockham passes
     const bool ip = (A.log2_fft & 1u) == 0;
-    auto ix = [&](uint32_t i) {
-        if (!ip) return i;
-        const uint32_t b = __brev(i) >> (32 - A.log2_fft);
-        return ((b & 0x55555555u) << 1) | ((b >> 1) & 0x55555555u);
-    };
+    auto ix = [&](uint32_t i) { return ip ? rev4(i, A.log2_fft) : i; };
     auto fft = [&](auto sign, float2* a, float2* b) -> const float2* {
         constexpr int SG = decltype(sign)::value;
         if (ip) {
