@@ -448,14 +448,19 @@ __device__ __forceinline__ void dft16(float2 (&v)[16]) {
 // digit-reversed positions, pass s (quarter Q = 4^(s/2)) combines four Q-point transforms per
 // butterfly with the twiddles W_N^(r k N/(4Q)) of fft_pow2's pass s, output in natural order. Every
 // butterfly reads and writes its own four slots (no second buffer: half the LDS of fft_pow2).
-template <int SIGN>
-__device__ void fft_r4_inplace(float2* x, const float2* tw, uint32_t log2N) {
+// PAD: slot i at x[i + i / 32] (the stride-4 accesses of the first passes and the digit-reversed
+// input writes on distinct banks: the caller allocates N + N / 32 slots and indexes through r4pad)
+__device__ __forceinline__ uint32_t r4pad(uint32_t i) { return i + (i >> 5); }
+
+template <int SIGN, bool PAD = false>
+__device__ void fft_r4_inplace(float2* x_, const float2* tw, uint32_t log2N) {
+    auto x = [&](uint32_t i) -> float2& { return x_[PAD ? r4pad(i) : i]; };
     const uint32_t NB = 1u << (log2N - 2);
     for (uint32_t s = 0; s < log2N; s += 2) {
         const uint32_t Q = 1u << s, tsh = log2N - s - 2;
         for (uint32_t j = threadIdx.x; j < NB; j += blockDim.x) {
             const uint32_t k = j & (Q - 1u), i0 = ((j >> s) << (s + 2)) + k;
-            float2 a0 = x[i0], a1 = x[i0 + Q], a2 = x[i0 + 2 * Q], a3 = x[i0 + 3 * Q];
+            float2 a0 = x(i0), a1 = x(i0 + Q), a2 = x(i0 + 2 * Q), a3 = x(i0 + 3 * Q);
             if (s) {
                 const uint32_t e = k << tsh;
                 float2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
@@ -469,10 +474,10 @@ __device__ void fft_r4_inplace(float2* x, const float2* tw, uint32_t log2N) {
                 a3 = cmul(a3, w3);
             }
             dft4<SIGN>(a0, a1, a2, a3);
-            x[i0] = a0;
-            x[i0 + Q] = a1;
-            x[i0 + 2 * Q] = a2;
-            x[i0 + 3 * Q] = a3;
+            x(i0) = a0;
+            x(i0 + Q) = a1;
+            x(i0 + 2 * Q) = a2;
+            x(i0 + 3 * Q) = a3;
         }
         __syncthreads();
     }

@@ -1335,16 +1335,18 @@ __global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
     // power-of-4 sizes (4096 for C3 / C4): in-place radix-4 DIT on one LDS buffer, the inputs stored
     // at their base-4 digit-reversed positions (ip); otherwise the two-buffer Stockham passes
     const bool ip = (A.log2_fft & 1u) == 0;
-    auto ix = [&](uint32_t i) { return ip ? rev4(i, A.log2_fft) : i; };
+    // in place: bank-padded slots (r4pad), inputs written at their digit-reversed slots
+    auto ix = [&](uint32_t i) { return ip ? r4pad(rev4(i, A.log2_fft)) : i; };
+    auto ox = [&](uint32_t i) { return ip ? r4pad(i) : i; };
     auto fft = [&](auto sign, float2* a, float2* b) -> const float2* {
         constexpr int SG = decltype(sign)::value;
         if (ip) {
-            fft_r4_inplace<SG>(a, A.tw_fft, A.log2_fft);
+            fft_r4_inplace<SG, true>(a, A.tw_fft, A.log2_fft);
             return a;
         }
         return fft_pow2<SG>(a, b, A.tw_fft, A.log2_fft);
     };
-    const uint32_t nbuf = nf;
+    const uint32_t nbuf = ip ? nf + nf / 32 : nf;  // (the host sizes the LDS the same way)
     float2* xb = smem + 16;
     float2* yb = xb + nbuf;
     // the forward spectrum is read once per template: kept in a global scratch row (L2-resident
@@ -1374,7 +1376,7 @@ __global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
     }
     __syncthreads();
     const float2* S = fft(std::integral_constant<int, -1>{}, xb, yb);
-    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) Sb[i] = S[i];
+    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) Sb[i] = S[ox(i)];
     __syncthreads();  // S's buffer is overwritten below; each thread re-reads only its own Sb[i]
     float xm[4];
     uint32_t xi[4];
@@ -1386,7 +1388,7 @@ __global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
         float bv = -1.f;
         uint32_t bi = 0xFFFFFFFFu;
         for (uint32_t j = threadIdx.x; j < A.xc_len; j += blockDim.x) {
-            const float m = cnorm(R[j]);
+            const float m = cnorm(R[ox(j)]);
             if (m > bv) {  // first maximum (volk_32fc_index_max_32u)
                 bv = m;
                 bi = j;
@@ -1630,7 +1632,7 @@ hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st) {
 
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st) {
     const size_t nbuf = size_t(1) << a.log2_fft;
-    const size_t lds = (16 + ((a.log2_fft & 1u) == 0 ? 1 : 2) * nbuf) * sizeof(float2);  // in-place: one buffer
+    const size_t lds = (16 + ((a.log2_fft & 1u) == 0 ? nbuf + nbuf / 32 : 2 * nbuf)) * sizeof(float2);  // in place: one padded buffer
     const char* e = std::getenv("DNRP_FINE_T");  // experiment: 256 / 512 / 1024 threads
     const uint32_t t = e && (std::atoi(e) == 256 || std::atoi(e) == 1024) ? static_cast<uint32_t>(std::atoi(e)) : SYNC_FINE_THREADS;
     hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(t), lds, st, a);
