@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
     // the resampled STF from its bottom (a block's outputs stay below every window: 9 outputs per 10
     // inputs), and the FFT runs in place on its first N slots; otherwise sbuf | inbuf (FFT buffers) | taps
     const uint32_t lgN = 31u - __clz(Nd);
-    const bool compact = CT && (lgN & 1u) == 0 && A.STF_CP >= Nd;  // the host sizes the LDS by the same test
+    const bool compact = CT && (lgN & 1u) == 0 && A.STF_CP >= Nd + Nd / 32;  // the host sizes the LDS by the same test
     float2* sbuf = smem;                                    // n_stf
     float2* inbuf = sbuf + n_stf;                           // rx_stf_in(...)
     float2* fa = inbuf;                                     // Nd
@@ -165,18 +165,26 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
     pr = block_sum(pr, red);
     pi = block_sum(pi, red);
     const float2* F;
-    if (compact) {  // in place on sbuf[0, N): the inputs sbuf[STF_CP + i] (STF_CP >= N) at digit-reversed slots
-        for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) sbuf[rev4(i, lgN)] = sbuf[A.STF_CP + i];
+    if (compact) {  // in place on sbuf[0, N + N/32) (bank-padded slots, below STF_CP >= N + N/32): the
+                    // inputs sbuf[STF_CP + i] at digit-reversed slots
+        for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) sbuf[r4pad(rev4(i, lgN))] = sbuf[A.STF_CP + i];
         __syncthreads();
-        fft_r4_inplace<-1>(sbuf, A.tw, lgN);
-        F = sbuf;
+        fft_r4_inplace<-1, true>(sbuf, A.tw, lgN);
+        const uint32_t N = A.N_occ;
+        float2* ys = A.stf_ys + (size_t(pkt) * 8 + a) * A.stf_ys_stride;
+        for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) {  // extract_bins on the padded slots
+            const uint32_t k = w < n / 2 ? 4 * w : 4 * w + 4;
+            ys[w] = cscale(k >= N / 2 ? sbuf[r4pad(k - N / 2)] : sbuf[r4pad(A.off_lower + k)], A.amp_scale);
+        }
+        F = nullptr;
     } else {
         for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) fa[i] = sbuf[A.STF_CP + i];
         __syncthreads();
         F = fft_any<-1>(fa, fb, A.tw, A.plan);
     }
     float2* ys = A.stf_ys + (size_t(pkt) * 8 + a) * A.stf_ys_stride;
-    for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) extract_bins(A, F, &ys[w], w < n / 2 ? 4 * w : 4 * w + 4);
+    if (!compact)
+        for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) extract_bins(A, F, &ys[w], w < n / 2 ? 4 * w : 4 * w + 4);
     if (threadIdx.x == 0) {
         A.stf_rms[size_t(pkt) * 8 + a] = sqrtf(static_cast<float>(e / n_stf));
         A.stf_cs[size_t(pkt) * 8 + a] = make_double2(pr, pi);
@@ -374,7 +382,7 @@ hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
     const char* ct_e = std::getenv("DNRP_RX_STF_CT");
     uint32_t lgN = 0;
     while ((1u << lgN) < Nd) ++lgN;
-    const bool compact = lgN % 2 == 0 && a.STF_CP >= Nd;
+    const bool compact = lgN % 2 == 0 && a.STF_CP >= Nd + Nd / 32;
     if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24 && !(ct_e && !std::atoi(ct_e)))
         hipLaunchKernelGGL((rx_stf_ant_kernel<24, true>), dim3(n * a.N_RX), dim3(256),
                            compact ? size_t(std::max(rx_stf_area(n_stf), n_stf)) * sizeof(float2) : lds, st, a);
