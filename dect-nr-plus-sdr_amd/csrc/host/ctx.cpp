@@ -239,6 +239,9 @@ std::vector<uint16_t> pcc_cell_symbols(const geo::maps_t& m) {
     return sym;
 }
 
+dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, const uint32_t* sel,
+                              const rx_plan_dev* plan = nullptr);
+
 rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, int* err) {
     const auto key = std::make_tuple(u, b, N_eff_TX);
     auto it = ctx->rx1t.find(key);
@@ -298,6 +301,12 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
                                   t->lut_nw[mode][p]};
     if (!ok || !t->luts.upload(luts)) {
         *err = DNRP_ENOMEM;
+        return nullptr;
+    }
+    // the STF front end of N_b_DFT_os = 8192 (a u = 1 packet at a u_max = 8 / b_max = 16 rate, or
+    // os_min 8) needs more than one CU's LDS: not supported
+    if (!dev::rx_front_fits(front_args(ctx, t.get(), nullptr, nullptr))) {
+        *err = DNRP_EUNSUPPORTED;
         return nullptr;
     }
     auto* r = t.get();
@@ -378,6 +387,80 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
             *err = DNRP_ENOMEM;
             return nullptr;
         }
+        // the same cells in the fused receiver's zero-forced pilots: DRS op of the phase plan, cell index
+        std::vector<uint32_t> zc(NTS * NW, 0);
+        for (uint32_t ts = 0; ts < NTS; ++ts) {
+            const geo::drs_sym_t* last = nullptr;
+            for (const auto& d : t->maps.drs)
+                if (d.ts_first <= ts && ts <= d.ts_last) last = &d;
+            uint32_t dop = 0;
+            while (last && dop < plan.dl.size() && plan.dl[dop] != last->l) ++dop;
+            for (uint32_t c = 0; c < NW; ++c) zc[ts * NW + c] = (dop << 16) | (off + c * step);
+        }
+        if (!t->mimo_zcells.upload(zc)) {
+            *err = DNRP_ENOMEM;
+            return nullptr;
+        }
+    }
+    // fused PDC receiver (kernels/rx_fused.hip): one entry per PDC-bearing symbol with the event of
+    // its plan segment and the pilot sources of its epoch. Holds where every segment is a run of whole
+    // symbols and, for transmit diversity, every symbol has an even cell count (SFBC pairs do not
+    // straddle symbols); otherwise the Y path runs.
+    {
+        const auto& m = t->maps;
+        auto is_drs = [&](uint32_t l) {
+            for (const auto& d : m.drs)
+                if (d.l == l) return true;
+            return false;
+        };
+        const bool pairs = tm.N_eff_TX > 1;
+        bool ok = !sm && (tm.N_eff_TX == 1 || tm.N_eff_TX == 2 || tm.N_eff_TX == 4) && plan.dl.size() <= dev::RX_MAX_DOPS;
+        std::vector<dev::rx_fsym> fs;
+        for (const auto& e : plan.epochs)
+            for (uint32_t s = e.seg0; s < e.seg1 && ok; ++s) {
+                const auto& g = plan.segs[s];
+                ok = g.kind == geo::OP_PDC && g.drs_cnt > 0;
+                uint32_t j = g.j0;
+                for (uint32_t l = 0; l <= t->q.N_DF_symb && j < g.j1 && ok; ++l) {
+                    const uint32_t c0 = m.pdc_sym_off[l], c1 = m.pdc_sym_off[l + 1];
+                    if (c1 <= j || c0 == c1) continue;
+                    if (c0 != j || c1 > g.j1 || (pairs && ((c0 | c1) & 1u))) {
+                        ok = false;
+                        break;
+                    }
+                    dev::rx_fsym f{};
+                    f.l = l;
+                    f.j0 = c0;
+                    f.j1 = c1;
+                    const bool from_y = l <= pm || is_drs(l);
+                    // every occupied subcarrier but DC in order: the kernel computes the subcarriers
+                    const uint32_t N = 56 * d.b;
+                    bool full = c1 - c0 == N;
+                    for (uint32_t c = 0; c < N && full; ++c) full = m.pdc_k[c0 + c] == c + (c >= N / 2 ? 1u : 0u);
+                    f.info = (g.mode & 1u) | (g.swap & 3u) << 1 | (g.off & 0xFFu) << 4 | (from_y ? 1u : 0u) << 12 |
+                             (full ? 1u : 0u) << 13;
+                    f.rel = g.rel;
+                    f.drs_cnt = g.drs_cnt;
+                    std::memcpy(f.src, e.src, sizeof(f.src));
+                    fs.push_back(f);
+                    j = c1;
+                }
+                ok = ok && j == g.j1;
+            }
+        std::vector<uint16_t> dsy;
+        for (const auto& d : m.drs)
+            if (d.l > pm && d.l <= t->q.N_DF_symb) {
+                dsy.push_back(static_cast<uint16_t>(d.l));
+                if (m.pdc_sym_off[d.l + 1] > m.pdc_sym_off[d.l]) t->drs_y = true;
+            }
+        if (dsy.empty()) dsy.push_back(0);  // keeps the upload non-empty; n_drs_syms stays 0
+        t->n_drs_syms = static_cast<uint32_t>(dsy.size()) - (dsy[0] == 0 ? 1u : 0u);
+        t->n_fsym = static_cast<uint32_t>(fs.size());
+        t->fused_ok = ok && !fs.empty();
+        if (t->fused_ok && (!t->fsym.upload(fs) || !t->drs_syms.upload(dsy))) {
+            *err = DNRP_ENOMEM;
+            return nullptr;
+        }
     }
     auto* r = t.get();
     ctx->rx2t[key] = std::move(t);
@@ -389,7 +472,7 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
 bool snr_from_front(dnrp_ctx* ctx, rx1_tables* t);
 
 dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, const uint32_t* sel,
-                              const rx_plan_dev* plan = nullptr) {
+                              const rx_plan_dev* plan) {
     dev::rx_front_args a{};
     a.plan = t->plan;
     a.N_occ = t->N_occ;
@@ -430,12 +513,8 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, con
         a.stf_ys_stride = 14 * ctx->cfg.b_max;
     }
     // compile-time-tap front end (rx.hip rx_fft_wave_kernel<.., true>) where the run-time taps are
-    // the generated ones bit for bit; DNRP_RX_CT=0 forces the tap-table variant (A/B)
-    static const int ct_env = [] {
-        const char* e = std::getenv("DNRP_RX_CT");
-        return e ? std::atoi(e) : 1;
-    }();
-    a.stream = (ct_env && dev::rx_stream_taps_match(t->rs.h.data(), t->rs.h.size())) ? 1u : 0u;
+    // the generated ones bit for bit (the tap-table variant measured slower)
+    a.stream = dev::rx_stream_taps_match(t->rs.h.data(), t->rs.h.size()) ? 1u : 0u;
     if (plan && dev::rx_fft_wave_path(a)) {
         a.snr_part = ctx->snr_part.as<double2>();
         a.dl = plan->dl.as<uint32_t>();
@@ -445,21 +524,35 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, con
         a.drs_neg = geo::drs_neg_mask();
         a.sym_op = plan->sym_op.as<uint16_t>();
         a.n_sym_op = plan->n_sym_op;
+        // the zero-forced pilots next to the SNR sums (the fused PDC receiver's source), where the
+        // plan's ops fit below the zero op
+        if (ctx->zd.p && plan->n_dops + 1 <= ctx->zd_dops) {
+            a.zd = ctx->zd.as<float2>();
+            a.zd_dops = ctx->zd_dops;
+            a.zd_row = ctx->zd_row;
+        }
     }
+    a.n_drs = t->N_occ / 4;
     return a;
 }
 
 bool snr_from_front(dnrp_ctx* ctx, rx1_tables* t) {
-    const char* e = std::getenv("DNRP_RX_SNR_FRONT");  // A/B: 0 -> rx_snr gathers the DRS cells from Y
-    return (!e || std::atoi(e)) && t->drs_arith && dev::rx_fft_wave_path(front_args(ctx, t, nullptr, nullptr));
+    return ctx->rx_snr_front && t->drs_arith && dev::rx_fft_wave_path(front_args(ctx, t, nullptr, nullptr));
 }
 
-// back-end launches of one phase: SNR chain, then cells (rx_back.hip)
+// back-end launches of one phase: SNR chain, then cells (rx_back.hip); cells = false: the SNR chain
+// only (the fused PDC receiver equalises)
 int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t n, const uint32_t* sel, bool pdc,
                 uint32_t N_bps, const uint32_t* kk, const uint16_t* cell_sym, int16_t* llr, uint32_t llr_stride,
-                hipStream_t st, bool sm = false) {
+                hipStream_t st, bool sm = false, bool cells = true) {
     const char* name = pdc ? "rx_pdc" : "rx_pcc";
-    if (plan.n_dops > dev::RX_MAX_DOPS || !plan.cells_ok) return DNRP_EUNSUPPORTED;
+    if (plan.n_dops > dev::RX_MAX_DOPS || (cells && !plan.cells_ok)) return DNRP_EUNSUPPORTED;
+    if (cells && sm) {  // the MMSE cells kernel's instantiations and its LDS staging (rx_back.hip)
+        const uint32_t R = ctx->cfg.N_TX_max, T = t->N_eff_TX;
+        if (!((R == 2 || R == 4 || R == 8) && (T == 2 || T == 4) && T <= R) ||
+            dev::cell_lds_bytes(R, T, t->N_occ / 4, t->wcap[0], t->wcap[1]) > 160 * 1024)
+            return DNRP_EUNSUPPORTED;
+    }
     if (!ctx->lut_d.ensure(size_t(ctx->cfg.max_batch) * dev::RX_MAX_DOPS) ||
         !ctx->nv_d.ensure(size_t(ctx->cfg.max_batch) * dev::RX_MAX_DOPS * sizeof(float)))
         return DNRP_ENOMEM;
@@ -516,8 +609,9 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     c.sel = sel;
     ctx->tic(name, st);
     if (dev::launch_rx_snr(s, n, st) != hipSuccess) return DNRP_EDEVICE;
-    if (plan.n_epochs && (sm ? dev::launch_rx_cells_sm(c, n, st) : dev::launch_rx_cells(c, n, st)) != hipSuccess)
-        return sm ? DNRP_EUNSUPPORTED : DNRP_EDEVICE;
+    if (cells && plan.n_epochs &&
+        (sm ? dev::launch_rx_cells_sm(c, n, st) : dev::launch_rx_cells(c, n, st)) != hipSuccess)
+        return DNRP_EDEVICE;
     ctx->toc(name, st);
     return DNRP_OK;
 }
@@ -666,14 +760,9 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     // symbol runs (tx.hip): K symbols per WG plus the preceding symbol as resampler history
     // wave path (one wavefront per symbol slot): K = 6 symbols + history per 7-wave workgroup
     // (C4, 4096 slots per launch: K=3 12.3 ms, K=4 16.6, K=5 15.2, K=6 11.4, K=7 15.9 — LDS sets
-    // 4 / 2 / 2 / 2 / 1 workgroups per CU); block path K = 3. DNRP_TX_RUN overrides.
-    static const int K_env = [] {
-        const char* e = std::getenv("DNRP_TX_RUN");
-        return e ? std::atoi(e) : 0;
-    }();
+    // 4 / 2 / 2 / 2 / 1 workgroups per CU); block path K = 3.
     const bool wave = t->dm.Nd == 1024;
-    const uint32_t K_max = wave ? 7u : 3u;  // wave path: one wavefront per symbol slot, <= 8 slots
-    const uint32_t K = (K_env >= 1 && static_cast<uint32_t>(K_env) <= K_max) ? static_cast<uint32_t>(K_env) : (wave ? 6u : 3u);
+    const uint32_t K = wave ? 6u : 3u;
     a.K = K;
     a.n_runs = (t->q.N_DF_symb + 1 + K - 1) / K;
     a.m_star = 0;
@@ -713,13 +802,9 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     a.pdc_d = pdc_d;
     a.out = iq_out;
     a.pk = ctx->tx_pk.as<dev::tx_pkt>();
-    // streaming kernel (tx.hip tx_stream_kernel) where its geometry holds; DNRP_TX_STREAM=0 disables
-    static const int stream_env = [] {
-        const char* e = std::getenv("DNRP_TX_STREAM");
-        return e ? std::atoi(e) : 1;
-    }();
+    // streaming kernel (tx.hip tx_stream_kernel) where its geometry holds
     a.stream = 0;
-    if (stream_env && wave && t->code_bin.p && dev::tx_stream_taps_match(t->rs.h.data(), t->rs.h.size()) && a.L == 10 && a.M == 9 && a.hl == 22 && a.CP == 128 && a.STF_CP == 1280 &&
+    if (wave && t->code_bin.p && dev::tx_stream_taps_match(t->rs.h.data(), t->rs.h.size()) && a.L == 10 && a.M == 9 && a.hl == 22 && a.CP == 128 && a.STF_CP == 1280 &&
         a.pattern_len * 9 == a.STF_CP + 1024 && S % 2 == 0 && (reinterpret_cast<uintptr_t>(iq_out) & 15u) == 0) {
         // every symbol's PDC bytes (SFBC partners included) within its 1024-byte staging window
         const uint32_t bpc = t->tm.N_SS * t->q.N_bps;
@@ -807,6 +892,26 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         !ctx->rx_sel.ensure(2 * sizeof(uint32_t) * ctx->cfg.max_batch) ||
         !ctx->stf_part.ensure(size_t(ctx->cfg.max_batch) * 8 * (sizeof(double2) + sizeof(float) + 14 * ctx->cfg.b_max * sizeof(float2))))
         return DNRP_ENOMEM;
+    {
+        // A/B switches, read once per PCC call so that its PDC call agrees with it:
+        // DNRP_RX_SNR_FRONT=0 -> rx_snr gathers the DRS cells from Y (no front-end sums, no pilots,
+        // so no fused receiver); DNRP_RX_FUSED=0 -> the PDC phase through Y and rx_cells
+        const char* e = std::getenv("DNRP_RX_SNR_FRONT");
+        ctx->rx_snr_front = !e || std::atoi(e);
+        const char* f = std::getenv("DNRP_RX_FUSED");
+        ctx->rx_fused = ctx->rx_snr_front && (!f || std::atoi(f));
+        // zero-forced DRS pilots of every slot: at most one DRS symbol per 5 symbols (N_eff_TX <= 4)
+        // plus the zero op
+        ctx->zd_row = 14 * ctx->cfg.b_max;
+        ctx->zd_dops = std::min<uint32_t>(dev::RX_MAX_DOPS, (cap_max + 4) / 5 + 2) + 1;
+        const size_t zbytes = size_t(n) * ctx->zd_dops * ctx->cfg.N_TX_max * 4 * ctx->zd_row * sizeof(float2);
+        if (!ctx->zd.ensure(zbytes)) return DNRP_ENOMEM;
+        const auto key = std::make_tuple(ctx->zd.p, ctx->zd_dops, ctx->zd_row, ctx->cfg.N_TX_max);
+        if (key != ctx->zd_key) {  // a new layout: the zero op of every slot (and all else) zeroed once
+            HIPCHK(hipMemsetAsync(ctx->zd.p, 0, ctx->zd.n, st));
+            ctx->zd_key = key;
+        }
+    }
     auto* pin = static_cast<dev::rx_pkt_in*>(ctx->st_rxin.get(sizeof(dev::rx_pkt_in) * n));
     auto* sel = static_cast<uint32_t*>(ctx->st_sel.get(2 * sizeof(uint32_t) * n));
     if (!pin || !sel) return DNRP_ENOMEM;
@@ -931,16 +1036,60 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
         const uint32_t* gsel = ctx->rx_sel2.as<uint32_t>() + 2 * off;
         off += ng;
         auto fa = front_args(ctx, t, iq_in, gsel, snr_from_front(ctx, t) ? &t2->bplan : nullptr);
-        fa.sym_first = t->pcc_max + 1;
-        if (t2->q.N_DF_symb > t->pcc_max) {
-            fa.sym_count = t2->q.N_DF_symb - t->pcc_max;
-            ctx->tic("rx_fft_pdc", st);
-            if (dev::launch_rx_fft(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
-            ctx->toc("rx_fft_pdc", st);
+        // fused receiver (kernels/rx_fused.hip): the front end's pilots in zd, the compile-time-tap
+        // wave front end, an instantiated (N_RX, N_eff_TX) pair
+        const bool fused = ctx->rx_fused && t2->fused_ok && fa.zd && fa.stream && dev::rx_fft_wave_path(fa) &&
+                           dev::rx_fused_supported(fa.N_RX, t->N_eff_TX);
+        if (fused) {
+            // the phase's DRS symbols first (pilots, SNR sums; their bins to Y only where they carry
+            // PDC cells), then the SNR chain / LUT picks, then one fused launch for every PDC symbol
+            fa.sym_first = 0;
+            fa.sym_list = t2->drs_syms.as<uint16_t>();
+            fa.sym_count = t2->n_drs_syms;
+            fa.no_y = t2->drs_y ? 0u : 1u;
+            if (fa.sym_count) {
+                ctx->tic("rx_fft_pdc", st);
+                if (dev::launch_rx_fft(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
+                ctx->toc("rx_fft_pdc", st);
+            }
+            if ((err = launch_back(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps, nullptr, nullptr, pdc_llr,
+                                   llr_stride, st, false, false)) != DNRP_OK)
+                return err;
+            dev::rx_fused_args x{};
+            x.F = fa;
+            x.F.sym_list = nullptr;
+            x.n_pkt = ng;
+            x.n_fsym = t2->n_fsym;
+            x.NT = t->N_eff_TX;
+            x.N_bps = t2->q.N_bps;
+            {
+                uint32_t pr[12];
+                fill_pairs(t->N_eff_TX, pr, x.mod);
+                for (uint32_t i = 0; i < x.mod && i < 8; ++i) x.pair_bits |= uint64_t(pr[i] & 0xFFu) << (8 * i);
+            }
+            x.fsym = t2->fsym.as<dev::rx_fsym>();
+            x.kk = t2->pdc_k.as<uint32_t>();
+            x.luts = t->luts.as<dev::rx_lut>();
+            x.lut_d = ctx->lut_d.as<uint8_t>();
+            x.pdc_seq = static_cast<const uint8_t* const*>(ctx->pdc_seq_ptrs.p);
+            x.llr = pdc_llr;
+            x.llr_stride = llr_stride;
+            ctx->tic("rx_fused", st);
+            if (dev::launch_rx_fused(x, st) != hipSuccess) return DNRP_EDEVICE;
+            ctx->toc("rx_fused", st);
+        } else {
+            fa.zd = nullptr;  // no reader
+            fa.sym_first = t->pcc_max + 1;
+            if (t2->q.N_DF_symb > t->pcc_max) {
+                fa.sym_count = t2->q.N_DF_symb - t->pcc_max;
+                ctx->tic("rx_fft_pdc", st);
+                if (dev::launch_rx_fft(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
+                ctx->toc("rx_fft_pdc", st);
+            }
+            if ((err = launch_back(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps, t2->pdc_k.as<uint32_t>(),
+                                   t2->pdc_sym.as<uint16_t>(), pdc_llr, llr_stride, st, t2->sm)) != DNRP_OK)
+                return err;
         }
-        if ((err = launch_back(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps, t2->pdc_k.as<uint32_t>(),
-                               t2->pdc_sym.as<uint16_t>(), pdc_llr, llr_stride, st, t2->sm)) != DNRP_OK)
-            return err;
         if (rep) {
             // MIMO report at the packet end (rx_synced.cpp:417-436; the reference runs it after a
             // successful CRC, which is the caller's decision here)
@@ -962,6 +1111,12 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
             ma.Y = ctx->Y.as<float2>();
             ma.out = ctx->mimo_out.as<uint32_t>();
             ma.sel = gsel;
+            if (fused) {  // the DRS bins of this phase are not in Y: the pilots hold the same values
+                ma.zd = fa.zd;
+                ma.zcells = t2->mimo_zcells.as<uint32_t>();
+                ma.zd_dops = fa.zd_dops;
+                ma.zd_row = fa.zd_row;
+            }
             if (dev::launch_rx_mimo(ma, ng, st) != hipSuccess) return DNRP_EDEVICE;
         }
     }

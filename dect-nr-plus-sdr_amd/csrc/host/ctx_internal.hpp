@@ -160,6 +160,12 @@ struct rx2_tables {  // per (psdef): PDC phase
     // MIMO report (estimator_mimo_t): wideband DRS cells, single-stream codebooks
     uint32_t N_TS = 1, ncb_tx = 0, A_tx = 0, ncb_rx = 0, A_rx = 0;
     dbuf mimo_cells, mimo_signs, Wtx, stx, Wrx, srx;
+    // fused PDC receiver (kernels/rx_fused.hip): its symbol table, the phase's DRS symbols the front
+    // end runs first (after the PCC phase's), whether those carry PDC cells (their bins then go to Y),
+    // and the MIMO report's wideband cells in the zero-forced pilots (op << 16 | DRS cell)
+    bool fused_ok = false, drs_y = false;
+    uint32_t n_fsym = 0, n_drs_syms = 0;
+    dbuf fsym, drs_syms, mimo_zcells;
 };
 
 struct netid_seq {
@@ -196,6 +202,14 @@ struct dnrp_ctx {
     dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d, nv_d, mimo_out;
     dbuf stf_part;  // [max_batch][8] double2 cs | [max_batch][8] float rms | [max_batch][8][14 b_max] float2 cells
     dbuf snr_part;  // [slot][n_sym_total][N_RX][8] double2: front-end DRS SNR partial sums
+    // zero-forced DRS pilots [slot][zd_dops][N_RX][4][zd_row] (rx_front_args::zd); op zd_dops - 1 of
+    // every slot stays zero (the fused receiver's op-less interlace slots), zd_key: layout it was zeroed for
+    dbuf zd;
+    uint32_t zd_dops = 0, zd_row = 0;
+    std::tuple<void*, uint32_t, uint32_t, uint32_t> zd_key{};
+    // per PCC call: the DRS SNR sums (and pilots) come from the front end (DNRP_RX_SNR_FRONT, read
+    // once per PCC call so that its PDC call agrees), and the PDC phase may take the fused receiver
+    bool rx_snr_front = true, rx_fused = true;
     uint32_t rx_mode = 0;  // DNRP_RX_MODE_* (dnrp_ctx_set_rx_mode)
     pinned st_tx, st_rxin, st_seq, st_rep;
     // retained RX phase-1 state: per PCC-batch slot its (u, b, N_eff_TX) tables and symbol

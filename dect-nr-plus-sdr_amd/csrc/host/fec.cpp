@@ -633,16 +633,10 @@ int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* ll
 }  // extern "C"
 
 // ---- device turbo decoding -----------------------------------------------------------------------
-// PDC decoding runs the first kPdcSplit iterations for every code block, then continues the undecided
-// ones in dense waves (run_tdec)
-// (DNRP_FEC_SPLIT overrides it for A/B runs; 0 = one pass)
-static uint32_t pdc_split() {
-    static const uint32_t v = [] {
-        const char* e = std::getenv("DNRP_FEC_SPLIT");
-        return e ? (uint32_t)std::atoi(e) : 3u;
-    }();
-    return v;
-}
+// PDC decoding runs the first 3 iterations for every code block, then continues the undecided ones in
+// dense waves (run_tdec; same-box A/B at 5 dB: a split after 2 / 3 / 4 iterations 156 / 145 / 161 ms
+// per 4096 C4 TBs, one pass 0.95 s)
+static uint32_t pdc_split() { return 3u; }
 
 static int fec_tables(dnrp_ctx* ctx) {
     if (!ctx->fec_valid_off.empty()) return DNRP_OK;

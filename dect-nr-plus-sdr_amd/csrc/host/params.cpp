@@ -203,6 +203,20 @@ int dnrp_query_table(const char* name, const uint32_t* arg, uint32_t n_arg, floa
             }
         } else if (n == "stf_cover_sequence") {
             v.assign(prm::STF_COVER, prm::STF_COVER + 9);
+        } else if (n == "symbol_cells") {  // (b, N_TS, N_eff_TX, N_DF): per symbol l = 0..N_DF: PCC, PDC, DRS cells
+            if (n_arg != 4 || a(0) == 0 || a(0) > 16 || a(1) == 0 || a(1) > 8 || a(2) == 0 || a(2) > 8 || a(3) > 1024)
+                return DNRP_EINVAL;
+            const auto m = geo::build_maps(a(0), a(1), a(2), a(3));
+            for (uint32_t l = 0; l <= a(3); ++l) {
+                uint32_t pcc = 0, drs = 0;
+                for (uint32_t s = 0; s < m.pcc_l.size(); ++s)
+                    if (m.pcc_l[s] == l) pcc = m.pcc_sym_off[s + 1] - m.pcc_sym_off[s];
+                for (const auto& d : m.drs)
+                    if (d.l == l) drs += (d.ts_last - d.ts_first + 1) * static_cast<uint32_t>(m.drs_v.size() / 8);
+                v.push_back(static_cast<float>(pcc));
+                v.push_back(static_cast<float>(m.pdc_sym_off[l + 1] - m.pdc_sym_off[l]));
+                v.push_back(static_cast<float>(drs));
+            }
         } else {
             return DNRP_EINVAL;
         }

@@ -120,9 +120,20 @@ struct rx_front_args {
     float* stf_rms;            // [slot][8]
     float2* stf_ys;            // [slot][8][stf_ys_stride]
     uint32_t stf_ys_stride;
+    // symbol list of the launch (rx_fft_wave_kernel): launch symbol i is sym_list[i] instead of
+    // sym_first + i (the PDC phase's DRS symbols ahead of the fused receiver, rx_fused.hip)
+    const uint16_t* sym_list;
+    uint32_t no_y;             // 1: the bins are not stored to Y (nothing reads them there)
+    // zero-forced DRS pilots taken with the SNR partial sums (rx_drs_partials), the fused PDC
+    // receiver's pilot source: zd[((slot zd_dops + d) N_RX + rx) 4 + t][zd_row] (DRS op d of the phase
+    // plan; the PCC plan's ops are the prefix of the PDC plan's), null: not written
+    float2* zd;
+    uint32_t zd_dops, zd_row;
+    uint32_t fft_pass, fft_tw_lds;  // rx_fft_kernel layout (launch_rx_fft: symbols per pass, LDS twiddles)
 };
 bool rx_fft_wave_path(const rx_front_args& a);  // launch_rx_fft takes rx_fft_wave_kernel (snr_part supported)
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);
+bool rx_front_fits(const rx_front_args& a);  // the STF and FFT front-end launches fit the 160 KiB LDS
 bool rx_stream_taps_match(const float* h, size_t n);  // compiled-in 9/10 taps == run-time taps
 hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st);
 
@@ -218,6 +229,31 @@ __host__ __device__ constexpr size_t cell_lds_bytes(uint32_t N_RX, uint32_t NT, 
 }
 
 
+// ---- fused PDC receiver (rx_fused.hip): one workgroup per (packet, PDC symbol), one wavefront per RX
+// antenna resamples, mixes and transforms its antenna's symbol into LDS (or loads the bins a
+// preceding launch left in Y), then the workgroup equalises the symbol's cells from LDS with the
+// Wiener-interpolated channel of the zero-forced DRS pilots (zd) and writes the LLRs: no Y round trip.
+struct rx_fsym {                // one PDC-bearing symbol of the phase plan
+    uint32_t l, j0, j1;         // OFDM symbol, its PDC cells [j0, j1)
+    uint32_t info;              // mode | swap << 1 | off << 4 | from_y << 12 (bins from Y: PCC-phase or DRS symbol)
+    uint32_t rel, drs_cnt;      // LUT row, DRS ops before the event (LUT profile pick)
+    uint16_t src[4][2];         // epoch pilot sources: DRS op of (stream, interlace slot), 0xFFFF none
+};
+struct rx_fused_args {
+    rx_front_args F;            // front end (F.sym_* unused), Y, zd
+    uint32_t n_pkt, n_fsym, NT, N_bps, mod, pad0;
+    uint64_t pair_bits;         // SFBC pair i (A | B << 4) in bits 8i..8i+7 (mod <= 6 for N_eff_TX <= 4)
+    const rx_fsym* fsym;
+    const uint32_t* kk;         // pdc_k
+    const rx_lut* luts;         // [mode][profile]
+    const uint8_t* lut_d;       // [slot][RX_MAX_DOPS] profile after each DRS op (rx_snr_kernel)
+    const uint8_t* const* pdc_seq;  // per output row
+    int16_t* llr;
+    uint32_t llr_stride;
+};
+hipError_t launch_rx_fused(const rx_fused_args& a, hipStream_t st);
+bool rx_fused_supported(uint32_t N_RX, uint32_t NT);  // instantiated (N_RX, N_eff_TX) pairs
+
 struct rx_mimo_args {  // estimator_mimo_t::process_drs at the packet end, one wavefront per packet
     uint32_t N_RX, N_TS, Nf_pad, n_sym_total;
     uint32_t ncb_tx, A_tx, ncb_rx, A_rx;  // single-stream codebooks (1, N_TS) and (1, N_RX): size, first used
@@ -230,6 +266,11 @@ struct rx_mimo_args {  // estimator_mimo_t::process_drs at the packet end, one w
     const float2* Y;
     uint32_t* out;          // [row][3]: N_TS_other, tm_3_7_beamforming_idx, tm_3_7_beamforming_reciprocal_idx
     const uint32_t* sel;    // launch packet -> slot / output row
+    // fused PDC receiver: the cells from the zero-forced pilots zd (rx_front_args::zd) instead of Y;
+    // zcells[N_TS][4] = DRS op << 16 | DRS cell index
+    const float2* zd;
+    const uint32_t* zcells;
+    uint32_t zd_dops, zd_row;
 };
 hipError_t launch_rx_mimo(const rx_mimo_args& a, uint32_t n, hipStream_t st);
 

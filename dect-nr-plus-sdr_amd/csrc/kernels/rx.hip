@@ -8,8 +8,6 @@
 //                  + CP removal + FFT + bin extraction + amplitude scaling + STO derotation
 //                  (rx_synced.cpp:711-771) into the frequency-domain grid Y in HBM.
 // The back end (channel estimation, equalisation, demapping) is in rx_back.hip.
-#include <cstdlib>
-
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
@@ -125,10 +123,17 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
                          static_cast<int64_t>(A.S_in) - in.fine_peak, threadIdx.x, blockDim.x);
         __syncthreads();
         const float2 step1 = phasor(in.inc0);
-        for (int64_t q = q0 + threadIdx.x, rd = 0; rd == 0 || q < q1; q += blockDim.x, ++rd) {  // round 0: all threads
+        // rounds of blockDim blocks, the same count for every thread: each round's windows are read
+        // by every wave before any wave writes that round's outputs (a wave one round ahead would
+        // otherwise overwrite windows a slower wave has still to read: with Nd = 4096 a round's
+        // outputs reach into the previous round's windows), and a round's outputs stay below every
+        // later round's windows
+        const uint32_t rounds = static_cast<uint32_t>((q1 - q0 + blockDim.x - 1) / blockDim.x);
+        for (uint32_t rd = 0; rd < rounds; ++rd) {
+            const int64_t q = q0 + threadIdx.x + int64_t(rd) * blockDim.x;
             float2 xv[W];
             PD::template load<true>(span + 10 * min<int64_t>(q - q0, q1 - 1 - q0), xv);
-            if (rd == 0) __syncthreads();  // every first-round window read before outputs overwrite the area
+            __syncthreads();
             if (q >= q1) continue;
             const int64_t mb = ms + 9 * q;
             float2 r = phasor(static_cast<double>(mb) * in.inc0);
@@ -273,16 +278,20 @@ __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
 }
 
 // ===================================================================== data-symbol FFTs
-// One WG per (packet, antenna, run of sym_per_block symbols); the symbols are processed in pairs
-// (RX_SYM_PASS): resampling of both into LDS, one batched FFT, bin extraction + STO derotation.
-// Register-blocked path (LR > 0): the hw-rate input span of the symbol pair is staged in LDS with
-// coalesced loads, then thread j computes the L outputs of aligned block j (polyphase.hpp).
+// One WG per (packet, antenna, run of sym_per_block symbols); the symbols are processed in passes of
+// A.fft_pass (2, or 1 where two do not fit the LDS: N_b_DFT_os >= 4096): resampling into LDS, one
+// batched FFT, bin extraction + STO derotation. Register-blocked path (LR > 0): the hw-rate input span
+// of the pass is staged in LDS with coalesced loads, then thread j computes the L outputs of aligned
+// block j (polyphase.hpp). LDS: fa [pass][Nd] | fb [pass][Nd], aliased by the input span (free once the
+// pass is resampled; the next pass stages after the extraction's barrier) | rot [Nf] | twiddles [Nd]
+// (A.fft_tw_lds; else read through the L1) | taps.
 constexpr uint32_t RX_THREADS = 256;
 constexpr uint32_t RX_SYM_PASS = 2;
 
 // LDS samples for one pass's input span (host and device agree on this bound)
-__host__ __device__ inline uint32_t rx_in_cap(uint32_t Nd, uint32_t CP, uint32_t L, uint32_t M, uint32_t W) {
-    return ((RX_SYM_PASS * (Nd + CP)) * M + L - 1) / L + W + 2 * M + 2 * L;
+__host__ __device__ inline uint32_t rx_in_cap(uint32_t Nd, uint32_t CP, uint32_t L, uint32_t M, uint32_t W,
+                                              uint32_t pass = RX_SYM_PASS) {
+    return ((pass * (Nd + CP)) * M + L - 1) / L + W + 2 * M + 2 * L;
 }
 
 template <int LR, int MR, int HLR>
@@ -294,14 +303,16 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
     const uint32_t a = (blockIdx.x / nblk) % A.N_RX;
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / (nblk * A.N_RX));
     using PB = pp_block<(LR > 0 ? LR : 1), (LR > 0 ? MR : 1), (LR > 0 ? HLR : 0)>;
-    float2* fa = smem;                         // [RX_SYM_PASS][Nd]
-    float2* fb = fa + RX_SYM_PASS * Nd;        // [RX_SYM_PASS][Nd]
-    float2* twl = fb + RX_SYM_PASS * Nd;       // Nd
-    float2* rot = twl + Nd;                    // Nf: STO derotation per subcarrier
-    float2* inbuf = rot + Nf;                  // input span of a pass
-    const uint32_t in_cap = LR > 0 ? rx_in_cap(Nd, A.CP, LR, MR, PB::W) : (Nd * A.M) / A.L + A.hl + 4;
-    float* taps = reinterpret_cast<float*>(inbuf + in_cap);
-    stage_copy<4>(twl, A.tw, Nd, threadIdx.x, RX_THREADS);
+    const uint32_t SP = A.fft_pass;
+    const uint32_t in_cap = LR > 0 ? rx_in_cap(Nd, A.CP, LR, MR, PB::W, SP) : (Nd * A.M) / A.L + A.hl + 4;
+    float2* fa = smem;                                    // [SP][Nd]
+    float2* fb = fa + SP * Nd;                            // [SP][Nd]
+    float2* inbuf = fb;                                   // input span of a pass
+    float2* rot = fb + max(SP * Nd, in_cap);              // Nf: STO derotation per subcarrier
+    float2* twl = rot + Nf;                               // Nd (fft_tw_lds)
+    const float2* tw = A.fft_tw_lds ? twl : A.tw;
+    float* taps = reinterpret_cast<float*>(twl + (A.fft_tw_lds ? Nd : 0u));
+    if (A.fft_tw_lds) stage_copy<4>(twl, A.tw, Nd, threadIdx.x, RX_THREADS);
     if (LR == 0)
         for (uint32_t i = threadIdx.x; i < (A.hl + 1) * A.L; i += RX_THREADS) taps[i] = A.taps[i];
     else
@@ -319,8 +330,8 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
     // valid input window relative to the fine peak: history is zero before it (rx_synced.cpp:711-740)
     const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
     auto m_first = [&](uint32_t l) { return static_cast<int>(n_stf + (l - 1) * (A.CP + Nd) + A.CP); };
-    for (uint32_t lp = l0; lp < l1; lp += RX_SYM_PASS) {
-        const uint32_t ns = min(RX_SYM_PASS, l1 - lp);
+    for (uint32_t lp = l0; lp < l1; lp += SP) {
+        const uint32_t ns = min(SP, l1 - lp);
         if constexpr (LR > 0) {
             const int m_a = m_first(lp), m_b = m_first(lp + ns - 1) + static_cast<int>(Nd);
             const int qb0 = (m_a - static_cast<int>(A.m_star)) / LR;  // m_a >= m_star
@@ -356,7 +367,7 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
                                    phi_stf + static_cast<double>(m0 - n_stf) * S.inc1, S.inc1);
             }
         }
-        const float2* F = fft_any<-1>(fa, fb, twl, A.plan, ns);
+        const float2* F = fft_any<-1>(fa, fb, tw, A.plan, ns);
         for (uint32_t i = threadIdx.x; i < ns * Nf; i += RX_THREADS) {
             const uint32_t s = i / Nf, k = i - s * Nf;
             float2 v;
@@ -375,17 +386,28 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
         default: hipLaunchKernelGGL(KERNEL<-1>, G, B, LDS, ST, ARGS); break;  \
     }
 
-hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
+static bool rx_fft_layout(rx_front_args& a);
+
+// LDS bytes of rx_stf_ant_kernel's launch (compact: the compiled-in taps' in-place layout)
+static size_t rx_stf_lds(const rx_front_args& a) {
     const uint32_t Nd = a.plan.N, n_stf = a.STF_CP + Nd;
-    const size_t lds = (n_stf + rx_stf_in(n_stf, Nd, a.M, a.L, a.hl)) * sizeof(float2) + (a.hl + 1) * a.L * sizeof(float);
-    // DNRP_RX_STF_CT=0: the table-tap resampler (resample_block) also for compiled-in taps (A/B)
-    const char* ct_e = std::getenv("DNRP_RX_STF_CT");
     uint32_t lgN = 0;
     while ((1u << lgN) < Nd) ++lgN;
-    const bool compact = lgN % 2 == 0 && a.STF_CP >= Nd + Nd / 32;
-    if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24 && !(ct_e && !std::atoi(ct_e)))
-        hipLaunchKernelGGL((rx_stf_ant_kernel<24, true>), dim3(n * a.N_RX), dim3(256),
-                           compact ? size_t(std::max(rx_stf_area(n_stf), n_stf)) * sizeof(float2) : lds, st, a);
+    const bool ct = a.stream && a.L == 9 && a.M == 10 && a.hl == 24;
+    if (ct && lgN % 2 == 0 && a.STF_CP >= Nd + Nd / 32) return size_t(std::max(rx_stf_area(n_stf), n_stf)) * sizeof(float2);
+    return (n_stf + rx_stf_in(n_stf, Nd, a.M, a.L, a.hl)) * sizeof(float2) + (a.hl + 1) * a.L * sizeof(float);
+}
+
+bool rx_front_fits(const rx_front_args& a_in) {  // every RX front-end launch of the geometry fits the LDS
+    rx_front_args a = a_in;
+    return rx_stf_lds(a) <= 160 * 1024 && (rx_fft_wave_path(a) || rx_fft_layout(a));
+}
+
+hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
+    const size_t lds = rx_stf_lds(a);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24)  // compiled-in taps (table taps: 0.50 vs 0.38 ms)
+        hipLaunchKernelGGL((rx_stf_ant_kernel<24, true>), dim3(n * a.N_RX), dim3(256), lds, st, a);
     else
         DNRP_HL_DISPATCH(rx_stf_ant_kernel, dim3(n * a.N_RX), dim3(256), lds, st, a);
     hipLaunchKernelGGL(rx_stf_kernel, dim3(n), dim3(256), size_t(a.N_RX) * a.b * 14 * sizeof(float2), st, a);
@@ -398,12 +420,6 @@ hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
 // the same region as FFT input, runs wave_fft1024 there, and stores the occupied bins, amplitude
 // scaled and STO-derotated, straight to Y.
 constexpr uint32_t RXW_SYMS = 4;  // symbols (= wavefronts) per workgroup
-
-__host__ __device__ inline uint32_t rxw_region(uint32_t L, uint32_t M, uint32_t W) {
-    const uint32_t n_in = ((1024 + 2 * L) * M) / L + W + M;  // one symbol's input span, upper bound
-    const uint32_t r = n_in > WFFT_XB ? n_in : WFFT_XB;
-    return (r + 15) / 16 * 16;
-}
 
 // WPG symbols (= wavefronts) per workgroup: the compile-time-tap path shares nothing between its
 // waves, so it can run one wave per workgroup and free each wave's LDS region when that wave retires
@@ -428,8 +444,9 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
         stage_copy<4>(taps, A.taps_pp, A.npp, threadIdx.x, RX_THREADS);
     }
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t l = A.sym_first + blk * WPG + w;
-    const bool active = l < A.sym_first + A.sym_count;
+    const uint32_t li = blk * WPG + w;  // launch symbol
+    const bool active = li < A.sym_count;
+    const uint32_t l = A.sym_list ? A.sym_list[min(li, A.sym_count - 1)] : A.sym_first + li;
     const rx_pkt_in in = A.pin[pkt];
     const rx_pkt_state S = A.st[pkt];
     const rx_span_t sp = rx_span<LR, MR, HLR>(A, l);
@@ -460,8 +477,9 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
     if constexpr (CT) {
         rx_resample_ct<LR, MR, HLR>(A, in, S, sp, R, lane);
         // one instantiation of the (large, unrolled) FFT for both kinds of symbol: instruction cache
+        const bool to_y = !A.no_y;
         rx_fft_bins<RT>(A, S, R, lane, [&](uint32_t k, float2 v) {
-            Yrow[k] = v;
+            if (to_y) Yrow[k] = v;
             if (drs) R[k] = v;
         }, w1, wl);
         if (drs) {
@@ -522,55 +540,59 @@ bool rx_fft_wave_path(const rx_front_args& a) {
     return a.plan.N == 1024 && a.L == 9 && a.M == 10 && a.hl == 24 && a.sym_per_block == RXW_SYMS;
 }
 
-hipError_t launch_rx_fft(const rx_front_args& a, uint32_t n, hipStream_t st) {
+// LDS bytes of rx_fft_kernel for a pass size and twiddle placement
+static size_t rx_fft_lds(const rx_front_args& a, uint32_t pass, bool tw_lds) {
+    const uint32_t Nd = a.plan.N, Nf = a.N_occ + 1;
+    const bool blocked = a.L == 9 && a.M == 10 && (a.hl == 24 || a.hl == 4);
+    const uint32_t in_cap = blocked ? rx_in_cap(Nd, a.CP, a.L, a.M, a.hl == 24 ? pp_block<9, 10, 24>::W : pp_block<9, 10, 4>::W, pass)
+                                    : (Nd * a.M) / a.L + a.hl + 4;
+    const size_t taps = blocked ? size_t(a.npp) * sizeof(float) : size_t(a.hl + 1) * a.L * sizeof(float);
+    return (size_t(pass) * Nd + std::max(pass * Nd, in_cap) + Nf + (tw_lds ? Nd : 0u)) * sizeof(float2) + taps;
+}
+
+// the generic front end's layout: two symbols per pass with LDS twiddles where they fit, else one
+// symbol and / or twiddles through the L1; false: no layout fits the 160 KiB
+static bool rx_fft_layout(rx_front_args& a) {
+    for (uint32_t pass = RX_SYM_PASS; pass >= 1; --pass)
+        for (int tw = 1; tw >= 0; --tw)
+            if (rx_fft_lds(a, pass, tw) <= 160 * 1024) {
+                a.fft_pass = pass;
+                a.fft_tw_lds = static_cast<uint32_t>(tw);
+                return true;
+            }
+    return false;
+}
+
+hipError_t launch_rx_fft(const rx_front_args& a_in, uint32_t n, hipStream_t st) {
+    rx_front_args a = a_in;
     const uint32_t Nd = a.plan.N;
     const uint32_t nblk = (a.sym_count + a.sym_per_block - 1) / a.sym_per_block;
     const dim3 g(n * a.N_RX * nblk), b(RX_THREADS);
-    const size_t base = ((2 * RX_SYM_PASS + 1) * size_t(Nd) + a.N_occ + 1) * sizeof(float2);
-    auto fast = [&](auto kern, uint32_t W) {
-        const size_t lds = base + rx_in_cap(Nd, a.CP, a.L, a.M, W) * sizeof(float2) + a.npp * sizeof(float);
-        hipLaunchKernelGGL(kern, g, b, lds, st, a);
-    };
+    const bool generic = !rx_fft_wave_path(a);
+    if (generic && !rx_fft_layout(a)) return hipErrorInvalidValue;
+    auto fast = [&](auto kern) { hipLaunchKernelGGL(kern, g, b, rx_fft_lds(a, a.fft_pass, a.fft_tw_lds), st, a); };
     if (rx_fft_wave_path(a)) {  // os_min 1
         const uint32_t W = pp_block<9, 10, 24>::W;
         if (a.stream) {  // host: run-time taps == compiled-in taps bit for bit
-            // one wave per workgroup by default: each wave's LDS region is freed when it retires
-            // instead of with its slowest sibling (A/B on MI355X: 179.4k vs 176.4k slot-pairs/s);
-            // DNRP_RX_WPG = 2 / 4 for the grouped launches
-            static const int wpg = [] {
-                const char* e = std::getenv("DNRP_RX_WPG");
-                return e ? std::atoi(e) : 1;
-            }();
+            // one wave per workgroup: each wave's LDS region is freed when it retires instead of with
+            // its slowest sibling (A/B on MI355X: 179.4k vs 176.4k slot-pairs/s for 4 waves per
+            // workgroup); the FFT with two lane twiddles loaded with the staging (wave_fft1024_rt)
+            // instead of 27 inside its passes: 92 instead of 99 VGPRs (17 waves per CU, the LDS limit,
+            // not 16) and no twiddle-load latency in the passes (PDC launch 5.44 -> 5.30 ms per C4
+            // chunk, same box)
             const size_t lds1 = size_t(rxw_region(9, 10, W)) * sizeof(float2);
-            auto grid = [&](uint32_t per) { return dim3(n * a.N_RX * ((a.sym_count + per - 1) / per)); };
-            // the FFT with two lane twiddles loaded with the staging (wave_fft1024_rt) instead of 27
-            // inside its passes: 92 instead of 99 VGPRs (17 waves per CU, the LDS limit, not 16) and
-            // no twiddle-load latency in the passes (same box: PDC launch 5.44 -> 5.30 ms per C4
-            // chunk); DNRP_RX_FFT_RT=0: the table-twiddle FFT
-            static const int rt = [] {
-                const char* e = std::getenv("DNRP_RX_FFT_RT");
-                return e ? std::atoi(e) : 1;
-            }();
-            if (wpg == 1 && rt)
-                hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 1, true>), grid(1), dim3(64), lds1, st, a);
-            else if (wpg == 1)
-                hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 1>), grid(1), dim3(64), lds1, st, a);
-            else if (wpg == 2)
-                hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 2>), grid(2), dim3(128), 2 * lds1, st, a);
-            else
-                hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true>), g, b, RXW_SYMS * lds1, st, a);
+            hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 1, true>), dim3(n * a.N_RX * a.sym_count), dim3(64),
+                               lds1, st, a);
         } else {
             const size_t lds = (Nd + (a.npp + 1) / 2 + RXW_SYMS * size_t(rxw_region(9, 10, W))) * sizeof(float2);
             hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, false>), g, b, lds, st, a);
         }
     } else if (a.L == 9 && a.M == 10 && a.hl == 24)  // os_min 1 (225 taps)
-        fast(rx_fft_kernel<9, 10, 24>, pp_block<9, 10, 24>::W);
+        fast(rx_fft_kernel<9, 10, 24>);
     else if (a.L == 9 && a.M == 10 && a.hl == 4)  // os_min 2
-        fast(rx_fft_kernel<9, 10, 4>, pp_block<9, 10, 4>::W);
+        fast(rx_fft_kernel<9, 10, 4>);
     else
-        hipLaunchKernelGGL((rx_fft_kernel<0, 0, 0>), g, b,
-                           base + ((Nd * a.M) / a.L + a.hl + 4) * sizeof(float2) + (a.hl + 1) * a.L * sizeof(float), st,
-                           a);
+        fast(rx_fft_kernel<0, 0, 0>);
     return hipGetLastError();
 }
 

@@ -334,6 +334,11 @@ __global__ void __launch_bounds__(64) rx_mimo_kernel(rx_mimo_args A) {
     const float2* Yp = A.Y + size_t(pkt) * A.N_RX * A.n_sym_total * A.Nf_pad;
     for (uint32_t e = lane; e < A.N_RX * A.N_TS * 4; e += 64) {
         const uint32_t rx = e / (A.N_TS * 4), tc = e % (A.N_TS * 4);
+        if (A.zd) {  // the zero-forced pilots of the fused receiver: the same values, sign applied
+            const uint32_t zc = A.zcells[tc];
+            H[e] = A.zd[(((size_t(pkt) * A.zd_dops + (zc >> 16)) * A.N_RX + rx) * 4 + tc / 4) * A.zd_row + (zc & 0xFFFFu)];
+            continue;
+        }
         const uint32_t cell = A.cells[tc];
         H[e] = cscale(Yp[(size_t(rx) * A.n_sym_total + (cell >> 16)) * A.Nf_pad + (cell & 0xFFFFu)], A.signs[tc]);
     }

@@ -15,6 +15,13 @@
 
 namespace dnrp::dev {
 
+// float2 slots of one wave's LDS region: the symbol's input span, the FFT's exchange buffer, the bins
+__host__ __device__ inline uint32_t rxw_region(uint32_t L, uint32_t M, uint32_t W) {
+    const uint32_t n_in = ((1024 + 2 * L) * M) / L + W + M;  // one symbol's input span, upper bound
+    const uint32_t r = n_in > WFFT_XB ? n_in : WFFT_XB;
+    return (r + 15) / 16 * 16;
+}
+
 struct rx_span_t {
     int m0, qb0, qb1;
     int64_t in0;
@@ -113,8 +120,11 @@ __device__ __forceinline__ void rx_fft_bins(const rx_front_args& A, const rx_pkt
 
 // DRS SNR terms of one (antenna, DRS symbol) while its bins sit in the wave's region R (R[k] = bin
 // of subcarrier k): for every DRS op of symbol l and each of its transmit streams t, the sums over
-// the stream's DRS cells i of |w_i y_i|^2 and |w_i y_i - w_i+1 y_i+1|^2 (rx_snr_kernel's terms, the
-// same float products accumulated in double) -> A.snr_part. The op list is uniform (scalar loads).
+// the stream's DRS cells i of |w_i y_i|^2 and |w_i y_i - w_i+1 y_i+1|^2 (rx_snr_kernel's terms: float
+// products, summed per lane in float -- at most 4 cells per stream and lane, nd <= 256 -- and across
+// lanes in double, where the Y-gather path sums every term in double: the two paths may differ in the
+// last float bits, the reference's own volk sums are float) -> A.snr_part; with A.zd also the zero-forced cells
+// w_i y_i themselves (the pilot values of channel_antenna.hpp:38-63). The op list is uniform (scalar loads).
 __device__ __forceinline__ void rx_drs_partials(const rx_front_args& A, uint32_t slot, uint32_t a, uint32_t l,
                                                 uint32_t d0, const float2* R, uint32_t lane) {
     const uint32_t nd = A.n_drs, half = 2 * nd;  // N_b_OCC / 2
@@ -137,10 +147,12 @@ __device__ __forceinline__ void rx_drs_partials(const rx_front_args& A, uint32_t
         // per lane at most 4 (nd <= 256) terms per stream: float sums, double across the lanes; the
         // right neighbour of cell i comes from the next lane (lane 63: the next round's first cell)
         float f1 = 0.f, f2 = 0.f;
+        float2* zrow = A.zd ? A.zd + ((size_t(slot) * A.zd_dops + d) * A.N_RX + a) * 4 * A.zd_row : nullptr;
         for (uint32_t t = tf; t <= tl; ++t)
             for (uint32_t i0 = 0; i0 < nd; i0 += 64) {
                 const uint32_t i = i0 + lane;
                 const float2 v = cell(t, par, min(i, nd - 1));
+                if (zrow && i < nd) zrow[t * A.zd_row + i] = v;  // the zero-forced pilot (build_pilots' value)
                 float2 vn = make_float2(__shfl_down(v.x, 1), __shfl_down(v.y, 1));
                 if (lane == 63) vn = cell(t, par, min(i + 1, nd - 1));
                 if (i < nd) f1 += cnorm(v);

@@ -1082,7 +1082,7 @@ __host__ __device__ inline size_t peak8_alias(uint32_t region, uint32_t P, uint3
 #define DNRP_PEAK_WPE 4  // waves per SIMD the register budget allows
 #endif
 template <int LR, int MR, int HLR, bool CT, int NUW>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(DNRP_PEAK_WPE))) sync_peak_kernel(sync_args A) {
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DNRP_PEAK_WPE))) sync_peak_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     sync_shared& sh = *reinterpret_cast<sync_shared*>(smem);
     double* red = sh.red;
@@ -1312,7 +1312,7 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
 // ===================================================================== fine peak
 constexpr uint32_t SYNC_FINE_THREADS = 512;  // 8 waves: the FFT passes' butterflies 2 per thread
 
-__global__ void __launch_bounds__(1024) sync_fine_kernel(sync_args A) {
+__global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     float* s_val = reinterpret_cast<float*>(smem);  // [16]
     uint32_t* s_idx = reinterpret_cast<uint32_t*>(smem + 8);  // [16]
@@ -1486,31 +1486,22 @@ hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
         const uint64_t waves = uint64_t(n) * a.n_ant * n_seg;
         const size_t lds = SS_WPG * size_t(ss_inbuf<9, 10, 24>() + SS_RING) * sizeof(float2);
         const dim3 g(static_cast<uint32_t>((waves + SS_WPG - 1) / SS_WPG)), b(64 * SS_WPG);
-        // one wave per workgroup by default: a retired segment frees its LDS at once (A/B on
-        // MI355X: sync_steps 4.32 -> 3.81 ms, 176.4k -> 186.0k slot-pairs/s); DNRP_SYNC_WPG=4 groups
-        static const int wpg = [] {
-            const char* e = std::getenv("DNRP_SYNC_WPG");
-            return e ? std::atoi(e) : 1;
-        }();
-        // DNRP_SYNC_PIPE=0: the single-chunk-prefetch form (read per call)
+        // one wave per workgroup: a retired segment frees its LDS at once (A/B on MI355X: sync_steps
+        // 4.32 -> 3.81 ms, 176.4k -> 186.0k slot-pairs/s against four); DNRP_SYNC_PIPE=0: the
+        // single-chunk-prefetch form (read per call: tests switch it at run time). Compile-time sync
+        // taps where the run-time taps are the generated ones (neutral, 3.48 ms both)
         const char* pp_e = std::getenv("DNRP_SYNC_PIPE");
         const bool pipe = !pp_e || std::atoi(pp_e);
-        if (a.step == 64 && wpg == 1 && pipe && a.pattern % 16 == 0)
-            {
-            // compile-time sync taps (DNRP_SYNC_CT=0: the run-time taps through SGPRs)
-            const char* ct_e = std::getenv("DNRP_SYNC_CT");
-            if (a.ct_taps && !(ct_e && !std::atoi(ct_e)))
+        if (a.step == 64 && pipe && a.pattern % 16 == 0) {
+            if (a.ct_taps)
                 hipLaunchKernelGGL((sync_steps_pipe_kernel<9, 10, 24, true>), dim3(static_cast<uint32_t>(waves)), dim3(64),
                                    lds / SS_WPG, st, a, seg_steps, n_seg);
             else
                 hipLaunchKernelGGL((sync_steps_pipe_kernel<9, 10, 24, false>), dim3(static_cast<uint32_t>(waves)), dim3(64),
                                    lds / SS_WPG, st, a, seg_steps, n_seg);
-            }
-        else if (a.step == 64 && wpg == 1)
+        } else if (a.step == 64)
             hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 16, 1>), dim3(static_cast<uint32_t>(waves)), dim3(64),
                                lds / SS_WPG, st, a, seg_steps, n_seg);
-        else if (a.step == 64)
-            hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 16>), g, b, lds, st, a, seg_steps, n_seg);
         else
             hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 0>), g, b, lds, st, a, seg_steps, n_seg);
         return hipGetLastError();
@@ -1562,14 +1553,11 @@ hipError_t launch_sync_detect_split(const sync_args& a, uint32_t n, hipStream_t 
 
 // split round: coarse-peak search of the pending detections, one workgroup per (window, antenna)
 // one thread per 8 metric positions and, up to 512 threads, one per polyphase block of the region
-// (the resampling is one load round trip per block: DNRP_PEAK_T sweep on MI355X, C4 per 4096
+// (the resampling is one load round trip per block: thread-count sweep on MI355X, C4 per 4096
 // windows: 320 threads 0.98 ms, 384 0.93, 512 0.85, 576 1.20)
 uint32_t sync_peak_threads(const sync_args& a) {
     const uint32_t region = a.stf_len + a.D + SYNC_PAD_PEAK, nblk = a.L > 1 ? region / a.L + 2 : 0u;
-    const uint32_t t = std::max({128u, (a.D / 8 + 63) / 64 * 64, std::min(512u, (nblk + 63) / 64 * 64)});
-    const char* e = std::getenv("DNRP_PEAK_T");  // experiment: a larger workgroup (multiple of 64)
-    const uint32_t te = e ? static_cast<uint32_t>(std::atoi(e)) : 0u;
-    return te >= t && te <= 1024 && te % 64 == 0 ? te : t;
+    return std::max({128u, (a.D / 8 + 63) / 64 * 64, std::min(512u, (nblk + 63) / 64 * 64)});
 }
 
 size_t sync_peak_lds(const sync_args& a) {
@@ -1585,7 +1573,7 @@ bool sync_taps_match(const float* h, size_t n) {  // run-time sync taps == compi
 }
 
 bool sync_peak_ok(const sync_args& a) {  // the grid layout's preconditions (every DECT geometry meets them)
-    return a.D % 8 == 0 && a.pattern % 8 == 0 && (a.stf_len + SYNC_PAD_PEAK) % 8 == 0 && a.D / 8 <= 1024 &&
+    return a.D % 8 == 0 && a.pattern % 8 == 0 && (a.stf_len + SYNC_PAD_PEAK) % 8 == 0 && a.D / 8 <= 512 &&
            (a.n_uw == 6 || a.n_uw == 8) && sync_peak_lds(a) <= 160 * 1024;
 }
 
@@ -1633,9 +1621,7 @@ hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st) {
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st) {
     const size_t nbuf = size_t(1) << a.log2_fft;
     const size_t lds = (16 + ((a.log2_fft & 1u) == 0 ? nbuf + nbuf / 32 : 2 * nbuf)) * sizeof(float2);  // in place: one padded buffer
-    const char* e = std::getenv("DNRP_FINE_T");  // experiment: 256 / 512 / 1024 threads
-    const uint32_t t = e && (std::atoi(e) == 256 || std::atoi(e) == 1024) ? static_cast<uint32_t>(std::atoi(e)) : SYNC_FINE_THREADS;
-    hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(t), lds, st, a);
+    hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(SYNC_FINE_THREADS), lds, st, a);
     return hipGetLastError();
 }
 

@@ -39,6 +39,9 @@ PARITY_CASES = {
     "os2": ((1, 1, 1, 1, 0, 2), (1, 1, 1, 2, 10, 9), 1, (5.0, 20.0), 0),
     "os2_u2b2_tm1": ((2, 2, 1, 1, 1, 4), (2, 2, 2, 2, 10, 9), 1, (15.0, 25.0), 0),
     "subslot_tm5": ((1, 2, 0, 3, 5, 7), (1, 2, 4, 1, 10, 9), 1, (22.0, 30.0), 0),
+    # a u = 2 packet in a u_max = 8 / b_max = 16 context: N_b_DFT_os = 4096, the STF front end's
+    # compact in-place layout over several rounds of polyphase blocks (rx_stf_ant_kernel)
+    "u2_in_u8b16": ((2, 4, 1, 1, 0, 4), (8, 16, 1, 1, 10, 9), 1, (20.0, 30.0), 0),
 }
 
 

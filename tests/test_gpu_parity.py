@@ -29,14 +29,14 @@ CASES = F.PARITY_CASES
 TX_CASES = {**F.PARITY_CASES, **F.TX_ONLY_CASES}
 
 
-def _ctx(name, max_batch=8):
+def _ctx(name, max_batch=8, stride=2):
     import dnrp
     ps, cf, lr, _, _ = TX_CASES[name]
     u_max, b_max, ntx, os_min, L, M = cf
-    phy = dnrp.Phy(u_max, b_max, ntx, os_min, L, M, chestim_mode_lr=bool(lr), max_batch=max_batch)
+    phy = dnrp.Phy(u_max, b_max, ntx, os_min, L, M, chestim_mode_lr=bool(lr), stride=stride, max_batch=max_batch)
     for nid in range(100, 106):
         phy.add_network_id(nid)
-    return phy, dnrp.psdef(*ps), O.psdef(*ps), O.cfg(u_max, b_max, os_min, L, M, lr=lr)
+    return phy, dnrp.psdef(*ps), O.psdef(*ps), O.cfg(u_max, b_max, os_min, L, M, lr=lr, stride=stride)
 
 
 def _tx_inputs(rng, n, sz):
@@ -173,10 +173,10 @@ def _check_rx(name, g_pcc, g_pdc, r1, r2, r):
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_rx_parity(name):
+def test_rx_parity(name, stride=2):
     import dnrp
     rng = np.random.default_rng(11)
-    phy, ps, ops, ocf = _ctx(name)
+    phy, ps, ops, ocf = _ctx(name, stride=stride)
     snrs, cb = CASES[name][3], CASES[name][4]
     sz = phy.packet_sizes(ps)
     S = sz["N_samples_packet_os_rs"]
@@ -204,6 +204,22 @@ def test_rx_parity(name):
         if snrs[i] >= 20.0:  # uncoded hard decisions well above the demapping noise floor
             bits = np.unpackbits(pdc[i])[: sz["G"]]
             assert np.mean(bits != (g_pdc[i] > 0)) < 2e-2, (name, i)
+
+
+@pytest.mark.parametrize("name,stride", [("tm5_u2b4", 1), ("tm5_u2b4", 3), ("C4", 1), ("C4", 3), ("mrc2_64qam", 3),
+                                         ("C3", 1), ("tm1_txdiv2", 4)])
+def test_rx_parity_stride(name, stride):
+    """chestim_mode_lr_t_stride_default other than 2 (rx_synced.cpp:85,1097: the lr-mode interpolation
+    event every `stride` symbols of a processing stage) against the oracle run with the same stride."""
+    test_rx_parity(name, stride)
+
+
+@pytest.mark.parametrize("name", ["C4", "C3", "tm5_u2b4", "mrc4_16qam", "lmode_C4", "tm1_txdiv2", "u2_in_u8b16"])
+def test_rx_parity_y_path(name, monkeypatch):
+    """DNRP_RX_FUSED=0: the PDC phase through the frequency-domain grid Y (rx_fft_wave_kernel over every
+    symbol, rx_snr, rx_cells) instead of the fused receiver (rx_fused.hip) -- same oracle and gates."""
+    monkeypatch.setenv("DNRP_RX_FUSED", "0")
+    test_rx_parity(name)
 
 
 @pytest.mark.parametrize("name", ["C4", "C3", "C2"])
@@ -383,6 +399,22 @@ def test_rx_tm10_unsupported():
     assert e.value.code == -3
 
 
+def test_rx_large_fft_unsupported():
+    """A u = 1 packet at the u_max = 8 / b_max = 16 sample rate (N_b_DFT_os = 8192): its STF front end
+    needs more LDS than a CU has, so the PCC batch declines it (DNRP_EUNSUPPORTED) instead of failing a
+    launch; u = 2 (N_b_DFT_os = 4096) runs (PARITY_CASES u2_in_u8b16)."""
+    import dnrp
+    phy = dnrp.Phy(8, 16, 1, 1, 10, 9, max_batch=2)
+    ps = dnrp.psdef(1, 16, 1, 1, 0, 4)
+    S = phy.packet_sizes(ps)["N_samples_packet_os_rs"]
+    dev = torch.device("cuda:0")
+    iq = torch.zeros((1, 1, S, 2), dtype=torch.float32, device=dev)
+    pcc_llr = torch.zeros((1, 196), dtype=torch.int16, device=dev)
+    with pytest.raises(dnrp.DnrpError) as e:
+        phy.rx_pcc_batch([dnrp.SyncReport(0, 0.0, 0.0, 1, 16, 1)], iq, pcc_llr)
+    assert e.value.code == -3
+
+
 def test_rx_negative_fine_peak():
     """A sync report whose packet starts before the window (fine_peak_time < 0): the samples before
     the window read as zero history, never memory before the window row."""
@@ -411,14 +443,15 @@ def test_rx_negative_fine_peak():
     _check_rx("neg_peak", pcc_llr[1].cpu().numpy(), pdc_llr[0].cpu().numpy(), None, None, r)
 
 
-def test_c4_full_chunk_edges():
-    """A 4096-packet C4 batch (the bench's chunk, max_batch = 4096): TX and RX of packets 0, 2047
-    and 4095 compared with the oracle, chunk-boundary indexing included."""
+@pytest.mark.parametrize("name,n", [("C4", 4096), ("C3", 8192)])
+def test_full_chunk_edges(name, n):
+    """A full bench chunk (C4: 4096 packets, C3: 8192, max_batch = chunk): TX and RX of the first,
+    middle and last packet compared with the oracle, chunk-boundary indexing included."""
     import dnrp
     import math
-    n = 4096
-    phy, ps, ops, ocf = _ctx("C4", max_batch=n)
+    phy, ps, ops, ocf = _ctx(name, max_batch=n)
     sz = phy.packet_sizes(ps)
+    n_ant = sz["N_TX"]
     S, G = sz["N_samples_packet_os_rs"], sz["G"]
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev)
@@ -428,29 +461,29 @@ def test_c4_full_chunk_edges():
     rng = np.random.default_rng(9)
     cfo_dect = rng.uniform(-1.75, 1.75, n) * 2 * math.pi / sz["N_b_DFT_os"]
     descs = [dnrp.TxDesc(0, 100 + i % 6, 1 + i % 2, 5, 1.0, 0.0, float(cfo_dect[i] * 9 / 10), 0) for i in range(n)]
-    tx = torch.empty((n, 4, S, 2), dtype=torch.float32, device=dev)
+    tx = torch.empty((n, n_ant, S, 2), dtype=torch.float32, device=dev)
     phy.tx_batch(ps, descs, pcc_d, pdc_d, tx)
     phy.sync()
-    probe = [0, 2047, 4095]
+    probe = [0, n // 2 - 1, n - 1]
     pcc_h, pdc_h = pcc_d.cpu().numpy(), pdc_d.cpu().numpy()
     for i in probe:
         ref, n_tx = O.tx(ocf, ops, pcc_h[i], pdc_h[i], S, network_id=100 + i % 6, plcf_type=1 + i % 2,
                          phase_inc=float(np.float32(descs[i].iq_phase_increment_s2s_post_resampling_rad)))
-        _check_tx(tx[i].cpu().numpy().view(np.complex64)[..., 0], ref, sz, S, n_tx, ("C4 chunk", i))
-    # channel on the device: per-packet 4x4 mixing + AWGN, in place into the windows
+        _check_tx(tx[i].cpu().numpy().view(np.complex64)[..., 0], ref, sz, S, n_tx, (name, i))
+    # channel on the device: per-packet N x N mixing + AWGN, in place into the windows
     rx = torch.empty_like(tx)
     with torch.no_grad():
         for c0 in range(0, n, 256):
             x = torch.view_as_complex(tx[c0:c0 + 256])
-            H = torch.complex(torch.randn(x.shape[0], 4, 4, device=dev, generator=gen),
-                              torch.randn(x.shape[0], 4, 4, device=dev, generator=gen)) / math.sqrt(8)
+            H = torch.complex(torch.randn(x.shape[0], n_ant, n_ant, device=dev, generator=gen),
+                              torch.randn(x.shape[0], n_ant, n_ant, device=dev, generator=gen)) / math.sqrt(2 * n_ant)
             y = torch.einsum("brt,bts->brs", H, x)
             y = y + 0.003 * torch.complex(torch.randn(y.shape, device=dev, generator=gen),
                                           torch.randn(y.shape, device=dev, generator=gen))
             rx[c0:c0 + 256] = torch.view_as_real(y)
             del x, y
     del tx
-    reps = [dnrp.SyncReport(0, float(-cfo_dect[i]), 0.0, 8, 16, 4) for i in range(n)]
+    reps = [dnrp.SyncReport(0, float(-cfo_dect[i]), 0.0, 8, 16, sz["N_eff_TX"]) for i in range(n)]
     pcc_llr = torch.zeros((n, 196), dtype=torch.int16, device=dev)
     pdc_llr = torch.zeros((n, G), dtype=torch.int16, device=dev)
     phy.rx_pcc_batch(reps, rx, pcc_llr)
@@ -459,4 +492,4 @@ def test_c4_full_chunk_edges():
     for i in probe:
         win = rx[i].cpu().numpy().view(np.complex64)[..., 0]
         r = O.rx(ocf, ops, win, 0, float(np.float32(-cfo_dect[i])), 100 + i % 6, 1 + i % 2)
-        _check_rx(("C4 chunk", i), pcc_llr[i].cpu().numpy(), pdc_llr[i].cpu().numpy(), None, None, r)
+        _check_rx((name, i), pcc_llr[i].cpu().numpy(), pdc_llr[i].cpu().numpy(), None, None, r)
