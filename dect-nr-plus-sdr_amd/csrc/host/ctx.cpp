@@ -242,6 +242,37 @@ std::vector<uint16_t> pcc_cell_symbols(const geo::maps_t& m) {
 dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, const uint32_t* sel,
                               const rx_plan_dev* plan = nullptr);
 
+// SFBC pair union windows of full symbols (rx_lut::pair_w, the fused receiver): per LUT row, stream
+// class and pair u on subcarriers 2u, 2u + 1 (DC skipped) eq_compute's mean weights 0.5f (lo + hi) per
+// tap of the union window, in the same float arithmetic. Left empty (false is only an upload failure)
+// when some union window has more than 4 taps (the low-SNR profiles).
+bool pair_windows(const geo::lut_t& L, uint32_t N_occ, dbuf& pair_w, dbuf& pair_p) {
+    const uint32_t Nf = N_occ + 1, half = N_occ / 2, np = half, n = L.n;
+    std::vector<float4> pw4(size_t(L.T) * 4 * np);
+    std::vector<uint32_t> pb(size_t(L.T) * 4 * np);
+    for (uint32_t r = 0; r < L.T; ++r)
+        for (uint32_t cl = 0; cl < 4; ++cl)
+            for (uint32_t u = 0; u < np; ++u) {
+                const uint32_t k0 = 2 * u + (2 * u >= half ? 1u : 0u), k1 = 2 * u + 1 + (2 * u + 1 >= half ? 1u : 0u);
+                const uint32_t w0 = L.pilot_weight[(size_t(r) * 4 + cl) * Nf + k0];
+                const uint32_t w1 = L.pilot_weight[(size_t(r) * 4 + cl) * Nf + k1];
+                const uint32_t p0 = w0 & 0xFFFFu, p1 = w1 & 0xFFFFu;
+                const bool up = p1 >= p0;
+                const uint32_t sh = up ? p1 - p0 : p0 - p1;
+                const uint32_t wl = (up ? w0 : w1) >> 16, wh = (up ? w1 : w0) >> 16;
+                if (n + sh > 4) return true;
+                float wv[4];
+                for (uint32_t i = 0; i < 4; ++i) {
+                    const float lo = i < n ? L.weights[size_t(wl) * n + i] : 0.f;
+                    const float hi = i >= sh && i - sh < n ? L.weights[size_t(wh) * n + i - sh] : 0.f;
+                    wv[i] = 0.5f * (lo + hi);
+                }
+                pw4[(size_t(r) * 4 + cl) * np + u] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+                pb[(size_t(r) * 4 + cl) * np + u] = up ? p0 : p1;
+            }
+    return pair_w.upload(pw4) && pair_p.upload(pb);
+}
+
 rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, int* err) {
     const auto key = std::make_tuple(u, b, N_eff_TX);
     auto it = ctx->rx1t.find(key);
@@ -286,7 +317,8 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
     for (uint32_t mode = 0; mode < 2 && ok; ++mode)
         for (uint32_t p = 0; p < 3 && ok; ++p) {
             const auto L = geo::build_lut(mode ? Nsv : 0, b, c.b_max, c.u_max, p);
-            ok = t->lut_pw[mode][p].upload(L.pilot_weight) && t->lut_w[mode][p].upload(L.weights);
+            ok = t->lut_pw[mode][p].upload(L.pilot_weight) && t->lut_w[mode][p].upload(L.weights) &&
+                 (N_eff_TX < 2 || pair_windows(L, t->N_occ, t->lut_pair_w[mode][p], t->lut_pair_p[mode][p]));
             t->lut_n[mode][p] = L.n;
             t->lut_nw[mode][p] = static_cast<uint32_t>(L.weights.size());
             // 16-B slots: the segment table behind both weight tables stays 16-B aligned in LDS
@@ -298,7 +330,7 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
     for (uint32_t mode = 0; mode < 2; ++mode)
         for (uint32_t p = 0; p < 3; ++p)
             luts[mode * 3 + p] = {t->lut_pw[mode][p].as<uint32_t>(), t->lut_w[mode][p].as<float>(), t->lut_n[mode][p],
-                                  t->lut_nw[mode][p]};
+                                  t->lut_nw[mode][p], t->lut_pair_w[mode][p].as<float4>(), t->lut_pair_p[mode][p].as<uint32_t>()};
     if (!ok || !t->luts.upload(luts)) {
         *err = DNRP_ENOMEM;
         return nullptr;

@@ -147,6 +147,7 @@ struct rx1_tables {  // per (u, b, N_eff_TX): STF/PCC phase
     uint32_t npp = 0;  // floats in taps_pp
     rx_plan_dev bplan;  // PCC phase back end
     dbuf lut_pw[2][3], lut_w[2][3], luts;
+    dbuf lut_pair_w[2][3], lut_pair_p[2][3];  // SFBC pair union windows of full symbols (rx_lut::pair_w)
     uint32_t lut_n[2][3] = {}, lut_nw[2][3] = {}, lut_T[2] = {};
     uint32_t wcap[2] = {};  // largest weight table of mode l / lr (rx_cells_kernel LDS slots)
 };

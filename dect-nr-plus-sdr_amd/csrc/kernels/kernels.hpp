@@ -130,6 +130,7 @@ struct rx_front_args {
     float2* zd;
     uint32_t zd_dops, zd_row;
     uint32_t fft_pass, fft_tw_lds;  // rx_fft_kernel layout (launch_rx_fft: symbols per pass, LDS twiddles)
+    uint32_t stf_chunk;             // rx_stf_ant_kernel: 0, or outputs per resampling chunk (launch_rx_stf)
 };
 bool rx_fft_wave_path(const rx_front_args& a);  // launch_rx_fft takes rx_fft_wave_kernel (snr_part supported)
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);
@@ -173,6 +174,11 @@ struct rx_lut {             // one Wiener LUT: [T][4][Nf] pilot | weight << 16, 
     const uint32_t* pw;
     const float* w;
     uint32_t n, nw;         // taps per weight vector, floats in w (n_vec n)
+    // SFBC pairs of a full PDC symbol (pair u on subcarriers 2u, 2u + 1, DC skipped) per LUT row and
+    // stream class c = (t & 3) ^ swap: the union window's first pilot (LUT units) and its 4 mean
+    // weights 0.5 (w_k0 + w_k1) (eq_compute's, zero-padded); null where a union window exceeds 4 taps
+    const float4* pair_w;   // [T][4][N_occ / 2]
+    const uint32_t* pair_p; // [T][4][N_occ / 2]
 };
 
 struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epoch)

@@ -84,6 +84,13 @@ __host__ __device__ inline uint32_t rx_stf_in(uint32_t n_stf, uint32_t Nd, uint3
 // arithmetic of each antenna is the one the single-workgroup form ran (same 256-thread loops and
 // block sums), so rx_stf_kernel's results are unchanged.
 __device__ __forceinline__ int64_t floordiv_rx(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+// float2 offset of the tap table in rx_stf_ant_kernel's chunked layout: behind sbuf + the span of one
+// chunk of outputs, and behind the two FFT buffers laid over sbuf
+__host__ __device__ inline uint32_t rx_stf_chunk_taps(uint32_t n_stf, uint32_t Nd, uint32_t C, uint32_t M, uint32_t L,
+                                                      uint32_t hl) {
+    const uint32_t a = n_stf + (C * M) / L + hl + 4 + M, b = 2 * Nd;
+    return a > b ? a : b;
+}
 // float2 slots of rx_stf_ant_kernel's compact area: the 9/10 input span of n_stf outputs (upper bound)
 __host__ __device__ inline uint32_t rx_stf_area(uint32_t n_stf) { return ((n_stf + 18) * 10) / 9 + 33 + 10 + 2; }
 
@@ -97,18 +104,28 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
     // compact layout (compiled-in taps, N a power of 4): one area holds the input span at its top and
     // the resampled STF from its bottom (a block's outputs stay below every window: 9 outputs per 10
     // inputs), and the FFT runs in place on its first N slots; otherwise sbuf | inbuf (FFT buffers) | taps
+    // chunked layout (A.stf_chunk > 0: N_b_DFT_os = 8192, where sbuf + the whole span exceed the LDS):
+    // the STF resampled in chunks of stf_chunk outputs through a small input buffer, the FFT buffers
+    // over sbuf once its samples are consumed
     const uint32_t lgN = 31u - __clz(Nd);
-    const bool compact = CT && (lgN & 1u) == 0 && A.STF_CP >= Nd + Nd / 32;  // the host sizes the LDS by the same test
+    const uint32_t C = A.stf_chunk;
+    const bool compact = CT && C == 0 && (lgN & 1u) == 0 && A.STF_CP >= Nd + Nd / 32;  // the host sizes the LDS by the same test
     float2* sbuf = smem;                                    // n_stf
-    float2* inbuf = sbuf + n_stf;                           // rx_stf_in(...)
-    float2* fa = inbuf;                                     // Nd
-    float2* fb = inbuf + Nd;                                // Nd
-    float* taps = reinterpret_cast<float*>(inbuf + rx_stf_in(n_stf, Nd, A.M, A.L, A.hl));
-    if (!CT) stage_copy<4>(taps, A.taps, (A.hl + 1) * A.L, threadIdx.x, blockDim.x);
+    float2* inbuf = sbuf + n_stf;                           // rx_stf_in(...) / the chunk's span
+    float2* fa = C ? smem : inbuf;                          // Nd
+    float2* fb = fa + Nd;                                   // Nd
+    float* taps = reinterpret_cast<float*>(smem + (C ? rx_stf_chunk_taps(n_stf, Nd, C, A.M, A.L, A.hl)
+                                                     : n_stf + rx_stf_in(n_stf, Nd, A.M, A.L, A.hl)));
+    if (!CT || C) stage_copy<4>(taps, A.taps, (A.hl + 1) * A.L, threadIdx.x, blockDim.x);
     const rx_pkt_in in = A.pin[pkt];
     const uint32_t P = n_stf / A.n_pattern;
     const float2* x = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in;
-    if (CT) {
+    if (C) {
+        __syncthreads();  // taps
+        for (uint32_t m0 = 0; m0 < n_stf; m0 += C)
+            resample_block<HL>(A, x, in.fine_peak, m0, min(C, n_stf - m0), inbuf, sbuf + m0, taps,
+                               static_cast<double>(m0) * in.inc0, in.inc0);
+    } else if (CT) {
         // compile-time 9/10 taps: the span staged once, then thread q one polyphase block of 9 outputs
         // from its 33-input window in registers (each tap an immediate, summed newest input first as
         // resample_block does), mixed with a phasor at the block start stepped by the increment
@@ -182,6 +199,22 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
             ys[w] = cscale(k >= N / 2 ? sbuf[r4pad(k - N / 2)] : sbuf[r4pad(A.off_lower + k)], A.amp_scale);
         }
         F = nullptr;
+    } else if (C) {  // fa overlaps the STF samples it is filled from: through registers
+        constexpr uint32_t MAXR = 8192 / 256;
+        float2 v[MAXR];
+#pragma unroll
+        for (uint32_t j = 0; j < MAXR; ++j) {
+            const uint32_t i = threadIdx.x + j * blockDim.x;
+            if (i < Nd) v[j] = sbuf[A.STF_CP + i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < MAXR; ++j) {
+            const uint32_t i = threadIdx.x + j * blockDim.x;
+            if (i < Nd) fa[i] = v[j];
+        }
+        __syncthreads();
+        F = fft_any<-1>(fa, fb, A.tw, A.plan);
     } else {
         for (uint32_t i = threadIdx.x; i < Nd; i += blockDim.x) fa[i] = sbuf[A.STF_CP + i];
         __syncthreads();
@@ -388,14 +421,20 @@ __global__ void __launch_bounds__(RX_THREADS) rx_fft_kernel(rx_front_args A) {
 
 static bool rx_fft_layout(rx_front_args& a);
 
-// LDS bytes of rx_stf_ant_kernel's launch (compact: the compiled-in taps' in-place layout)
-static size_t rx_stf_lds(const rx_front_args& a) {
+// LDS bytes of rx_stf_ant_kernel's launch (compact: the compiled-in taps' in-place layout; sets
+// a.stf_chunk where only the chunked layout fits)
+static size_t rx_stf_lds(rx_front_args& a) {
     const uint32_t Nd = a.plan.N, n_stf = a.STF_CP + Nd;
+    const size_t taps = size_t(a.hl + 1) * a.L * sizeof(float);
     uint32_t lgN = 0;
     while ((1u << lgN) < Nd) ++lgN;
+    a.stf_chunk = 0;
     const bool ct = a.stream && a.L == 9 && a.M == 10 && a.hl == 24;
     if (ct && lgN % 2 == 0 && a.STF_CP >= Nd + Nd / 32) return size_t(std::max(rx_stf_area(n_stf), n_stf)) * sizeof(float2);
-    return (n_stf + rx_stf_in(n_stf, Nd, a.M, a.L, a.hl)) * sizeof(float2) + (a.hl + 1) * a.L * sizeof(float);
+    const size_t whole = (n_stf + rx_stf_in(n_stf, Nd, a.M, a.L, a.hl)) * sizeof(float2) + taps;
+    if (whole <= 160 * 1024 || Nd > 8192) return whole;
+    a.stf_chunk = 2048;
+    return rx_stf_chunk_taps(n_stf, Nd, a.stf_chunk, a.M, a.L, a.hl) * sizeof(float2) + taps;
 }
 
 bool rx_front_fits(const rx_front_args& a_in) {  // every RX front-end launch of the geometry fits the LDS
@@ -403,7 +442,8 @@ bool rx_front_fits(const rx_front_args& a_in) {  // every RX front-end launch of
     return rx_stf_lds(a) <= 160 * 1024 && (rx_fft_wave_path(a) || rx_fft_layout(a));
 }
 
-hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st) {
+hipError_t launch_rx_stf(const rx_front_args& a_in, uint32_t n, hipStream_t st) {
+    rx_front_args a = a_in;
     const size_t lds = rx_stf_lds(a);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24)  // compiled-in taps (table taps: 0.50 vs 0.38 ms)

@@ -41,18 +41,20 @@ struct pilot_rows {
 // first units of a thread before the front end, so that they arrive during it)
 template <int NT>
 struct fused_unit {
-    static constexpr int NC = NT == 1 ? 1 : 4;
-    uint32_t jj, k0, k1, tab, bits;
-    uint32_t pw[NC];
+    uint32_t jj, k0, k1, tab;
 };
+// the loaded part of a unit: scrambling bits, and either its LUT words (pw, the general path) or, for
+// an SFBC pair of a full symbol with a 4-tap union window (rx_lut::pair_w), per stream the window's
+// first pilot (v[0..1]; its mean weights are loaded with the pilots)
 template <int NT>
 struct fused_pre {
-    uint32_t bits, pw[fused_unit<NT>::NC];
+    static constexpr int NV = NT == 1 ? 1 : 4;
+    uint32_t bits, v[NV];
 };
 
 // FIR taps of the Wiener interpolation handled per chunk: every pilot and weight load of a chunk is
 // issued before its FMAs (one memory round trip per chunk; nI + shift <= 4 at the high-SNR profile)
-constexpr uint32_t FUSED_TAPS = 4;
+constexpr uint32_t FUSED_TAPS = 2;
 
 template <int NRX, int NT>
 __global__ void __launch_bounds__(64 * NRX) __attribute__((amdgpu_waves_per_eu(NRX <= 4 ? 4 : 2))) rx_fused_kernel(rx_fused_args A) {
@@ -98,17 +100,27 @@ __global__ void __launch_bounds__(64 * NRX) __attribute__((amdgpu_waves_per_eu(N
             q.tab = static_cast<uint32_t>(A.pair_bits >> (8 * ((q.jj >> 1) % A.mod))) & 0xFFu;
         }
     };
+    // SFBC pairs of a full symbol from the precomputed union windows (host: every window <= 4 taps)
+    const bool pairtab = NT > 1 && ((info >> 13) & 1u) && LT.pair_w != nullptr;
+    const size_t prow = size_t(fsp->rel) * 4 * half;
     auto unit_load = [&](const fused_unit<NT>& q, fused_pre<NT>& p) {
         const uint32_t b0 = (q.jj * N_bps) >> 3, bl = ((q.jj + per_unit) * N_bps - 1) >> 3;
         p.bits = seq[b0] | (b0 + 1 <= bl ? uint32_t(seq[b0 + 1]) << 8 : 0u) | (b0 + 2 <= bl ? uint32_t(seq[b0 + 2]) << 16 : 0u);
         if constexpr (NT == 1) {
-            p.pw[0] = pwr[swap * Nf + q.k0];
+            p.v[0] = pwr[swap * Nf + q.k0];
         } else {
             const uint32_t tA = q.tab & 0xFu, tB = q.tab >> 4;
-            p.pw[0] = pwr[((tA & 3u) ^ swap) * Nf + q.k0];
-            p.pw[1] = pwr[((tA & 3u) ^ swap) * Nf + q.k1];
-            p.pw[2] = pwr[((tB & 3u) ^ swap) * Nf + q.k0];
-            p.pw[3] = pwr[((tB & 3u) ^ swap) * Nf + q.k1];
+            if (pairtab) {
+                const uint32_t u = (q.jj - j0) >> 1;
+#pragma unroll
+                for (int st = 0; st < 2; ++st)
+                    p.v[st] = LT.pair_p[prow + size_t(((st == 0 ? tA : tB) & 3u) ^ swap) * half + u];
+            } else {
+                p.v[0] = pwr[((tA & 3u) ^ swap) * Nf + q.k0];
+                p.v[1] = pwr[((tA & 3u) ^ swap) * Nf + q.k1];
+                p.v[2] = pwr[((tB & 3u) ^ swap) * Nf + q.k0];
+                p.v[3] = pwr[((tB & 3u) ^ swap) * Nf + q.k1];
+            }
         }
     };
     fused_pre<NT> P[UPT];  // the first UPT units of this thread, in flight during the front end
@@ -165,11 +177,26 @@ __global__ void __launch_bounds__(64 * NRX) __attribute__((amdgpu_waves_per_eu(N
         return zp[ant * ast + r + min(p >> 1, nd - 1)];
     };
     int16_t* __restrict__ llr = A.llr + size_t(row) * A.llr_stride;
-    auto equalise = [&](const fused_unit<NT>& q) {
+    // SFBC pair combining (rx_synced.cpp:1373-1391) of the pair's channels g[rx][stream], demap, store
+    auto sfbc_emit = [&](const fused_unit<NT>& q, const fused_pre<NT>& pre, const float2 (&g)[NRX][2]) {
+        float2 n0 = make_float2(0.f, 0.f), n1 = make_float2(0.f, 0.f);
+        float den = 0.f;
+#pragma unroll
+        for (int r = 0; r < NRX; ++r) {
+            const float2 h0 = g[r][0], h1 = g[r][1];
+            const float2 r0 = smem[r * region + q.k0], r1 = smem[r * region + q.k1];
+            n0 = cadd(n0, cadd(cmul(cconj(h0), r0), cmul(h1, cconj(r1))));
+            n1 = cadd(n1, cadd(cmul(make_float2(-h1.x, -h1.y), cconj(r0)), cmul(cconj(h0), r1)));
+            den += cnorm(h0) + cnorm(h1);
+        }
+        emit_cell(cscale(n0, 1.0f / den), q.jj, q.jj, N_bps, pre.bits, llr);
+        emit_cell(cscale(n1, 1.0f / den), q.jj + 1, q.jj, N_bps, pre.bits, llr);
+    };
+    auto equalise = [&](const fused_unit<NT>& q, const fused_pre<NT>& pre) {
         if constexpr (NT == 1) {
-            uint32_t p = q.pw[0] & 0xFFFFu;
+            uint32_t p = pre.v[0] & 0xFFFFu;
             if (!mode) p = 2 * p + (off & 1u);  // non-interlaced: latest DRS symbol only
-            const uint32_t wo = (q.pw[0] >> 16) * nI;
+            const uint32_t wo = (pre.v[0] >> 16) * nI;
             const pilot_rows pr = rows_of(0);
             float2 h[NRX];
 #pragma unroll
@@ -200,17 +227,56 @@ __global__ void __launch_bounds__(64 * NRX) __attribute__((amdgpu_waves_per_eu(N
                 num = cadd(num, cmulc(r0, h[r]));
                 den += cnorm(h[r]);
             }
-            emit_cell(cscale(num, 1.0f / den), q.jj, q.jj, N_bps, q.bits, llr);
+            emit_cell(cscale(num, 1.0f / den), q.jj, q.jj, N_bps, pre.bits, llr);
+        } else if (pairtab) {
+            // the pair's union windows precomputed: 4 taps per stream, one pass (eq_compute's sums)
+            const uint32_t tA = q.tab & 0xFu, tB = q.tab >> 4;
+            uint32_t base[2];
+            pilot_rows pr[2];
+            float4 w4[2];
+            const uint32_t u = (q.jj - j0) >> 1;
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                const uint32_t t = st == 0 ? tA : tB;
+                base[st] = mode ? pre.v[st] : 2 * pre.v[st] + ((off >> t) & 1u);
+                pr[st] = rows_of(t);
+                w4[st] = LT.pair_w[prow + size_t((t & 3u) ^ swap) * half + u];
+            }
+            float2 g[NRX][2];
+            float2 z[4][2][NRX];
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c)
+#pragma unroll
+                for (int st = 0; st < 2; ++st)
+#pragma unroll
+                    for (int r = 0; r < NRX; ++r) z[c][st][r] = pilot(pr[st], base[st] + c * step, r);
+#pragma unroll
+            for (int r = 0; r < NRX; ++r) g[r][0] = g[r][1] = make_float2(0.f, 0.f);
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c)
+#pragma unroll
+                for (int st = 0; st < 2; ++st) {
+                    const uint32_t p = base[st] + c * step;
+                    // past the pilot row: weight 0 (eq_compute's zero pad)
+                    const float wc = c == 0 ? w4[st].x : c == 1 ? w4[st].y : c == 2 ? w4[st].z : w4[st].w;
+                    const float wv = p < np2 ? wc : 0.f;
+#pragma unroll
+                    for (int r = 0; r < NRX; ++r) {
+                        g[r][st].x = fmaf(z[c][st][r].x, wv, g[r][st].x);
+                        g[r][st].y = fmaf(z[c][st][r].y, wv, g[r][st].y);
+                    }
+                }
+            sfbc_emit(q, pre, g);
         } else {
             const uint32_t tA = q.tab & 0xFu, tB = q.tab >> 4;
             uint32_t pos[4], wo[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const uint32_t t = c < 2 ? tA : tB;
-                uint32_t p = q.pw[c] & 0xFFFFu;
+                uint32_t p = pre.v[c] & 0xFFFFu;
                 if (!mode) p = 2 * p + ((off >> t) & 1u);
                 pos[c] = p;
-                wo[c] = (q.pw[c] >> 16) * nI;
+                wo[c] = (pre.v[c] >> 16) * nI;
             }
             // SFBC: a stream's pair channel is the mean of its interpolations at k0 and k1
             // (rx_synced.cpp:1365-1371), one pass over the union window with the mean weights (eq_compute)
@@ -256,18 +322,7 @@ __global__ void __launch_bounds__(64 * NRX) __attribute__((amdgpu_waves_per_eu(N
                             g[r][s].y = fmaf(z[c][s][r].y, wv[c][s], g[r][s].y);
                         }
             }
-            float2 n0 = make_float2(0.f, 0.f), n1 = make_float2(0.f, 0.f);
-            float den = 0.f;
-#pragma unroll
-            for (int r = 0; r < NRX; ++r) {  // SFBC pair combining (rx_synced.cpp:1373-1391)
-                const float2 h0 = g[r][0], h1 = g[r][1];
-                const float2 r0 = smem[r * region + q.k0], r1 = smem[r * region + q.k1];
-                n0 = cadd(n0, cadd(cmul(cconj(h0), r0), cmul(h1, cconj(r1))));
-                n1 = cadd(n1, cadd(cmul(make_float2(-h1.x, -h1.y), cconj(r0)), cmul(cconj(h0), r1)));
-                den += cnorm(h0) + cnorm(h1);
-            }
-            emit_cell(cscale(n0, 1.0f / den), q.jj, q.jj, N_bps, q.bits, llr);
-            emit_cell(cscale(n1, 1.0f / den), q.jj + 1, q.jj, N_bps, q.bits, llr);
+            sfbc_emit(q, pre, g);
         }
     };
 #pragma unroll
@@ -275,10 +330,7 @@ __global__ void __launch_bounds__(64 * NRX) __attribute__((amdgpu_waves_per_eu(N
         if (tid + g * NTH < units) {
             fused_unit<NT> q;
             unit_index(tid + g * NTH, q);
-            q.bits = P[g].bits;
-#pragma unroll
-            for (int c = 0; c < fused_unit<NT>::NC; ++c) q.pw[c] = P[g].pw[c];
-            equalise(q);
+            equalise(q, P[g]);
         }
     // units past the prefetched ones (narrow workgroups, long symbols): tables loaded here
     for (uint32_t u = tid + UPT * NTH; u < units; u += NTH) {
@@ -286,10 +338,7 @@ __global__ void __launch_bounds__(64 * NRX) __attribute__((amdgpu_waves_per_eu(N
         unit_index(u, q);
         fused_pre<NT> p;
         unit_load(q, p);
-        q.bits = p.bits;
-#pragma unroll
-        for (int c = 0; c < fused_unit<NT>::NC; ++c) q.pw[c] = p.pw[c];
-        equalise(q);
+        equalise(q, p);
     }
 }
 

@@ -42,6 +42,9 @@ PARITY_CASES = {
     # a u = 2 packet in a u_max = 8 / b_max = 16 context: N_b_DFT_os = 4096, the STF front end's
     # compact in-place layout over several rounds of polyphase blocks (rx_stf_ant_kernel)
     "u2_in_u8b16": ((2, 4, 1, 1, 0, 4), (8, 16, 1, 1, 10, 9), 1, (20.0, 30.0), 0),
+    # u = 1 at the same rate: N_b_DFT_os = 8192, the STF front end's chunked layout (rx_stf_ant_kernel)
+    # and the generic FFT front end with one symbol per pass, twiddles through the L1 (rx_fft_kernel)
+    "u1_in_u8b16": ((1, 16, 1, 1, 0, 4), (8, 16, 1, 1, 10, 9), 1, (20.0,), 0),
 }
 
 

@@ -119,3 +119,20 @@ def test_no_gpu_context_fails_loudly():
     with pytest.raises(dnrp.DnrpError) as e:
         dnrp.Phy(1, 1, 1)
     assert e.value.code == -5  # DNRP_EDEVICE: no silent CPU fallback
+
+
+@pytest.mark.parametrize("name", ["C2", "C3", "C4", "tm1_txdiv2", "mrc4_16qam", "subslot_tm5", "lm40_27_b12"])
+def test_symbol_cells_table(name):
+    """dnrp_query_table("symbol_cells"): per symbol the PCC / PDC / DRS cells of the packet geometry the
+    RX plans (and bench.py's byte counts) come from -- every occupied subcarrier of a DF symbol is one
+    of them (none in symbol 0, the STF), the PCC holds its 98 cells, the PDC cells carry G bits."""
+    psd, cf = F.case(name)
+    ps = dnrp.psdef(*psd)
+    sz = dnrp.compute_packet_sizes(ps, cf[0], cf[1], cf[3], cf[4], cf[5])
+    cells = dnrp.query_table("symbol_cells", psd[1], sz["N_TS"], sz["N_eff_TX"], sz["N_DF_symb"]).reshape(-1, 3)
+    assert cells.shape == (sz["N_DF_symb"] + 1, 3)
+    assert not cells[0].any()
+    assert (cells[1:].sum(1) <= sz["N_b_OCC"]).all()
+    assert cells[:, 0].sum() == 98
+    assert cells[:, 1].sum() * sz["N_bps"] * sz["N_SS"] == sz["G"]
+    assert cells[1, 2] > 0  # the first DF symbol carries DRS

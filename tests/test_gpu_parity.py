@@ -399,22 +399,6 @@ def test_rx_tm10_unsupported():
     assert e.value.code == -3
 
 
-def test_rx_large_fft_unsupported():
-    """A u = 1 packet at the u_max = 8 / b_max = 16 sample rate (N_b_DFT_os = 8192): its STF front end
-    needs more LDS than a CU has, so the PCC batch declines it (DNRP_EUNSUPPORTED) instead of failing a
-    launch; u = 2 (N_b_DFT_os = 4096) runs (PARITY_CASES u2_in_u8b16)."""
-    import dnrp
-    phy = dnrp.Phy(8, 16, 1, 1, 10, 9, max_batch=2)
-    ps = dnrp.psdef(1, 16, 1, 1, 0, 4)
-    S = phy.packet_sizes(ps)["N_samples_packet_os_rs"]
-    dev = torch.device("cuda:0")
-    iq = torch.zeros((1, 1, S, 2), dtype=torch.float32, device=dev)
-    pcc_llr = torch.zeros((1, 196), dtype=torch.int16, device=dev)
-    with pytest.raises(dnrp.DnrpError) as e:
-        phy.rx_pcc_batch([dnrp.SyncReport(0, 0.0, 0.0, 1, 16, 1)], iq, pcc_llr)
-    assert e.value.code == -3
-
-
 def test_rx_negative_fine_peak():
     """A sync report whose packet starts before the window (fine_peak_time < 0): the samples before
     the window read as zero history, never memory before the window row."""
