@@ -927,11 +927,12 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
     {
         // A/B switches, read once per PCC call so that its PDC call agrees with it:
         // DNRP_RX_SNR_FRONT=0 -> rx_snr gathers the DRS cells from Y (no front-end sums, no pilots,
-        // so no fused receiver); DNRP_RX_FUSED=0 -> the PDC phase through Y and rx_cells
+        // so no fused receiver); DNRP_RX_FUSED=1 -> the PDC phase through the fused receiver
+        // (rx_fused.hip) instead of Y and rx_cells: parity-tested, slower on MI355X
         const char* e = std::getenv("DNRP_RX_SNR_FRONT");
         ctx->rx_snr_front = !e || std::atoi(e);
         const char* f = std::getenv("DNRP_RX_FUSED");
-        ctx->rx_fused = ctx->rx_snr_front && (!f || std::atoi(f));
+        ctx->rx_fused = ctx->rx_snr_front && f && std::atoi(f);
         // zero-forced DRS pilots of every slot: at most one DRS symbol per 5 symbols (N_eff_TX <= 4)
         // plus the zero op
         ctx->zd_row = 14 * ctx->cfg.b_max;

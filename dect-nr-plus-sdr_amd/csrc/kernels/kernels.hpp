@@ -210,12 +210,15 @@ hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st);
 hipError_t launch_rx_cells_sm(const rx_cells_args& a, uint32_t n, hipStream_t st);
 
 // rx_cells_kernel's per-workgroup LDS staging (rx_back.hip, rx_eq.hpp).
-// The epoch's pilot buffer zfi: one row per (rx, ts) of 2 nd interlaced pilots plus ZFI_PAD zeros.
-// The pad puts the rows of different streams on different LDS banks (a wave's lanes alternate between
-// the streams of consecutive SFBC pairs) and lets a union window run past a row's last pilot.
+// The epoch's pilot buffer zfi: one row per (rx, ts) of 2 nd interlaced pilots plus ZFI_PAD zeros (a
+// union window may run past a row's last pilot). Rows start on the same bank (stride a multiple of 32
+// float2 = 64 dwords): a wave's lanes take consecutive SFBC pairs, whose streams alternate between
+// rows while their pilot positions advance by one per lane, so one read instruction of the wave hits
+// bank 2 p_lane + const whatever row each lane is in -- 32 distinct even banks per half-wave. (With
+// rows 2 nd + 8 slots apart, 912 dwords for b = 16, lanes 8 apart in different rows collided.)
 constexpr uint32_t ZFI_PAD = 8;
 constexpr uint32_t CELL_MAX_SEGS = 64;  // segments per epoch (host-checked, rx_plan_dev)
-__host__ __device__ constexpr uint32_t zfi_stride(uint32_t n_drs) { return 2 * n_drs + ZFI_PAD; }
+__host__ __device__ constexpr uint32_t zfi_stride(uint32_t n_drs) { return (2 * n_drs + ZFI_PAD + 31) / 32 * 32; }
 
 // An epoch segment with the packet's Wiener LUT resolved: the LUT row block of the segment's
 // processing-stage symbol and its weight table's slot in LDS

@@ -94,7 +94,7 @@ __host__ __device__ inline uint32_t rx_stf_chunk_taps(uint32_t n_stf, uint32_t N
 // float2 slots of rx_stf_ant_kernel's compact area: the 9/10 input span of n_stf outputs (upper bound)
 __host__ __device__ inline uint32_t rx_stf_area(uint32_t n_stf) { return ((n_stf + 18) * 10) / 9 + 33 + 10 + 2; }
 
-template <int HL, bool CT = false>
+template <int HL, bool CT = false, bool CHUNK = false>
 __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     __shared__ double red[16];
@@ -108,7 +108,8 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
     // the STF resampled in chunks of stf_chunk outputs through a small input buffer, the FFT buffers
     // over sbuf once its samples are consumed
     const uint32_t lgN = 31u - __clz(Nd);
-    const uint32_t C = A.stf_chunk;
+    const uint32_t C = CHUNK ? A.stf_chunk : 0u;  // a separate instantiation: its register-staged FFT
+                                                   // input would cost the other layouts occupancy
     const bool compact = CT && C == 0 && (lgN & 1u) == 0 && A.STF_CP >= Nd + Nd / 32;  // the host sizes the LDS by the same test
     float2* sbuf = smem;                                    // n_stf
     float2* inbuf = sbuf + n_stf;                           // rx_stf_in(...) / the chunk's span
@@ -199,7 +200,7 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
             ys[w] = cscale(k >= N / 2 ? sbuf[r4pad(k - N / 2)] : sbuf[r4pad(A.off_lower + k)], A.amp_scale);
         }
         F = nullptr;
-    } else if (C) {  // fa overlaps the STF samples it is filled from: through registers
+    } else if (CHUNK) {  // fa overlaps the STF samples it is filled from: through registers
         constexpr uint32_t MAXR = 8192 / 256;
         float2 v[MAXR];
 #pragma unroll
@@ -446,7 +447,9 @@ hipError_t launch_rx_stf(const rx_front_args& a_in, uint32_t n, hipStream_t st) 
     rx_front_args a = a_in;
     const size_t lds = rx_stf_lds(a);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24)  // compiled-in taps (table taps: 0.50 vs 0.38 ms)
+    if (a.stf_chunk)  // N_b_DFT_os = 8192: the chunked layout, run-time taps
+        hipLaunchKernelGGL((rx_stf_ant_kernel<-1, false, true>), dim3(n * a.N_RX), dim3(256), lds, st, a);
+    else if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24)  // compiled-in taps (table taps: 0.50 vs 0.38 ms)
         hipLaunchKernelGGL((rx_stf_ant_kernel<24, true>), dim3(n * a.N_RX), dim3(256), lds, st, a);
     else
         DNRP_HL_DISPATCH(rx_stf_ant_kernel, dim3(n * a.N_RX), dim3(256), lds, st, a);

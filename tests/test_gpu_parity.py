@@ -214,12 +214,21 @@ def test_rx_parity_stride(name, stride):
     test_rx_parity(name, stride)
 
 
-@pytest.mark.parametrize("name", ["C4", "C3", "tm5_u2b4", "mrc4_16qam", "lmode_C4", "tm1_txdiv2", "u2_in_u8b16"])
-def test_rx_parity_y_path(name, monkeypatch):
-    """DNRP_RX_FUSED=0: the PDC phase through the frequency-domain grid Y (rx_fft_wave_kernel over every
-    symbol, rx_snr, rx_cells) instead of the fused receiver (rx_fused.hip) -- same oracle and gates."""
-    monkeypatch.setenv("DNRP_RX_FUSED", "0")
+@pytest.mark.parametrize("name", ["C4", "C3", "tm5_u2b4", "mrc2_64qam", "mrc4_16qam", "lmode_C4", "lmode_txdiv2",
+                                  "tm1_txdiv2", "tm3_codebook3", "subslot_tm5", "u2_in_u8b16"])
+def test_rx_parity_fused(name, monkeypatch):
+    """DNRP_RX_FUSED=1: the PDC phase through the fused receiver (rx_fused.hip: the DRS symbols' front end
+    leaves zero-forced pilots, then one workgroup per (packet, symbol) transforms every antenna into LDS
+    and equalises from there, no Y round trip) instead of Y + rx_cells -- same oracle and gates.
+    Geometries outside the fused kernel (N_b_DFT_os != 1024) run the Y path either way."""
+    monkeypatch.setenv("DNRP_RX_FUSED", "1")
     test_rx_parity(name)
+
+
+@pytest.mark.parametrize("name,stride", [("C4", 1), ("tm5_u2b4", 3)])
+def test_rx_parity_fused_stride(name, stride, monkeypatch):
+    monkeypatch.setenv("DNRP_RX_FUSED", "1")
+    test_rx_parity(name, stride)
 
 
 @pytest.mark.parametrize("name", ["C4", "C3", "C2"])
