@@ -742,7 +742,10 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     tx_tables* t = get_tx(ctx, *psdef, &err);
     if (!t) return err;
     if (S < t->dm.N_packet_rs || pdc_stride < (t->q.G + 7) / 8) return DNRP_EINVAL;
-    if (t->q.N_b_OCC + 1 > 1024) return DNRP_EUNSUPPORTED;  // tx_kernel stages <= 4 code words per thread
+    // tx_kernel stages <= 4 code words per thread: N_b_DFT_os <= 1024 (the streaming and wave paths'
+    // 1024, the block path up to 1024; larger transforms, e.g. u < u_max at u_max = 8 / b_max = 16 or
+    // os_min >= 2 there, are not built for TX)
+    if (t->q.N_b_OCC + 1 > 1024 || t->dm.Nd > 1024) return DNRP_EUNSUPPORTED;
     auto* pk = static_cast<dev::tx_pkt*>(ctx->st_tx.get(sizeof(dev::tx_pkt) * n));
     if (!pk) return DNRP_ENOMEM;
     for (uint32_t i = 0; i < n; ++i) {

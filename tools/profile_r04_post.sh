@@ -1,0 +1,13 @@
+#!/bin/bash
+# copy the round-4 PMC summaries into profiles/r04 (C4 -> traffic.json / valu.json, others suffixed)
+set -e
+d=profiles/r04
+for tag in c4 c4sm fused; do
+  src=gpurun_out/prof_r04_$tag
+  suf=""; [ $tag != c4 ] && suf="_$tag"
+  cp $src/traffic.json $d/traffic$suf.json
+  cp $src/valu.json $d/valu$suf.json
+  cp $src/traffic.txt $d/traffic$suf.txt
+  cp $src/summary.txt $d/pmc_sq_summary$suf.txt
+  cp $(find $src/trace -name "*kernel_stats.csv" | head -1) $d/kernel_stats_profile_run$suf.csv
+done
