@@ -742,10 +742,7 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     tx_tables* t = get_tx(ctx, *psdef, &err);
     if (!t) return err;
     if (S < t->dm.N_packet_rs || pdc_stride < (t->q.G + 7) / 8) return DNRP_EINVAL;
-    // tx_kernel stages <= 4 code words per thread: N_b_DFT_os <= 1024 (the streaming and wave paths'
-    // 1024, the block path up to 1024; larger transforms, e.g. u < u_max at u_max = 8 / b_max = 16 or
-    // os_min >= 2 there, are not built for TX)
-    if (t->q.N_b_OCC + 1 > 1024 || t->dm.Nd > 1024) return DNRP_EUNSUPPORTED;
+    if (t->q.N_b_OCC + 1 > 1024) return DNRP_EUNSUPPORTED;
     auto* pk = static_cast<dev::tx_pkt*>(ctx->st_tx.get(sizeof(dev::tx_pkt) * n));
     if (!pk) return DNRP_ENOMEM;
     for (uint32_t i = 0; i < n; ++i) {
@@ -822,6 +819,16 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
         const uint32_t max_out = static_cast<uint32_t>((uint64_t(span + t->rs.hl) * t->rs.L + t->rs.M - 1) / t->rs.M) + t->rs.L;
         a.bufB_len = std::max((K + 1) * t->dm.Nd, max_out > t->dm.Nd + 256 ? max_out - t->dm.Nd - 256 : 0u);
     }
+    if (t->dm.Nd > 1024) {
+        // beyond the block path's registers (tx_kernel stages <= 4 bins per thread): the symbols go
+        // through a DECT-rate scratch (tx.hip tx_big_sym_kernel), e.g. u < u_max at b_max = 16
+        const uint64_t total = uint64_t(t->dm.STF_CP) + uint64_t(t->q.N_DF_symb) * t->dm.CP + uint64_t(t->q.N_DF_symb + 1) * t->dm.Nd;
+        a.big_len = static_cast<uint32_t>((total + 3) / 4 * 4);
+        if (!ctx->tx_big.ensure(sizeof(float) * 2 * a.big_len * uint64_t(n) * t->tm.N_TX)) return DNRP_ENOMEM;
+        HIPCHK(ctx->tx_big.wait_idle(st));
+        a.big = ctx->tx_big.as<float2>();
+        a.stage_bytes = 0;
+    }
     a.code = t->code.as<uint32_t>();
     a.pdc_off = t->pdc_off.as<uint32_t>();
     a.stf = t->stf.as<float2>();
@@ -872,6 +879,7 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     if (dev::launch_tx(a, n, st) != hipSuccess) return DNRP_EDEVICE;
     ctx->toc("tx", st);
     HIPCHK(ctx->tx_pk.mark_busy(st));
+    if (a.big) HIPCHK(ctx->tx_big.mark_busy(st));
     return DNRP_OK;
 }
 

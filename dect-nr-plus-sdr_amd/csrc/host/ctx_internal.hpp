@@ -201,6 +201,7 @@ struct dnrp_ctx {
     dbuf pcc_seq;
     // batch scratch
     dbuf tx_pk, rx_in, rx_st, Y, pdc_seq_ptrs, lut_d, nv_d, mimo_out;
+    dbuf tx_big;  // N_b_DFT_os > 1024: DECT-rate symbols [n][N_TX][big_len] (tx.hip tx_big_sym_kernel)
     dbuf stf_part;  // [max_batch][8] double2 cs | [max_batch][8] float rms | [max_batch][8][14 b_max] float2 cells
     dbuf snr_part;  // [slot][n_sym_total][N_RX][8] double2: front-end DRS SNR partial sums
     // zero-forced DRS pilots [slot][zd_dops][N_RX][4][zd_row] (rx_front_args::zd); op zd_dops - 1 of

@@ -62,6 +62,10 @@ struct tx_args {
     const uint32_t* code_bin;  // [N_DF+1][1024] cell code of every FFT bin (0: empty)
     uint32_t n_pieces, n_seg, piece_per_seg, stream;
     uint32_t pcc_syms;         // bit l: symbol l (< 32) carries PCC cells
+    // N_b_DFT_os > 1024 (beyond the block path's registers): every symbol's cyclic-prefixed DECT-rate
+    // samples through a scratch [packet][antenna][big_len] (tx_big_sym_kernel, tx_big_resample_kernel)
+    float2* big;
+    uint32_t big_len;
 };
 hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st);
 bool tx_stream_taps_match(const float* h, size_t n);  // compiled-in 10/9 taps == run-time taps

@@ -869,6 +869,92 @@ __global__ void __launch_bounds__(TX_THREADS) tx_kernel(tx_args A) {
     tx_resample<LR, MR, HLR>(w);
 }
 
+// ---- N_b_DFT_os > 1024: symbol-parallel through a DECT-rate scratch in HBM. An 8192-point
+// symbol's ping-pong buffers alone take 128 KiB of LDS, so the block path's runs (K symbols plus the
+// history symbol, resampled in LDS) do not fit; here workgroup (packet, antenna, symbol l) builds the
+// bins, runs the IFFT (twiddles from the L2) and stores the cyclic-prefixed, STF-covered symbol
+// into A.big, then one thread per hw-rate output runs the FIR over the scratch (tx_resample's run-time
+// tap form: inputs before the packet and past its flush samples are the zero history), the mixer and
+// the GI / slot-tail zeros (tx.cpp:679-714).
+constexpr uint32_t TX_BIG_THREADS = 512;
+
+__global__ void __launch_bounds__(TX_BIG_THREADS) tx_big_sym_kernel(tx_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const uint32_t l = blockIdx.x % (A.N_DF + 1), pa = blockIdx.x / (A.N_DF + 1);
+    tx_wg w{};
+    w.A = &A;
+    w.pkt = pa / A.N_TX;
+    w.ant = pa % A.N_TX;
+    w.P = A.pk[w.pkt];
+    w.Nd = A.plan.N;
+    w.N = A.N_occ;
+    w.Nf = w.N + 1;
+    w.hl = A.hl;
+    w.len0 = A.STF_CP + w.Nd;
+    w.lenD = A.CP + w.Nd;
+    float2* fa = smem;
+    float2* fb = smem + w.Nd;
+    w.qtab = fb + w.Nd;
+    w.pccs = w.qtab + 256;
+    w.wrow = w.pccs + 98;
+    w.dpdc = A.pdc_d + size_t(w.pkt) * A.pdc_stride;
+    w.cpdc = w.P.pdc_seq;
+    w.pdc_bytes = (A.G + 7) / 8;  // A.stage_bytes = 0: PDC bytes straight from HBM
+    const uint8_t* dpcc = A.pcc_d + size_t(w.pkt) * 25;
+    for (uint32_t i = threadIdx.x; i < (1u << A.N_bps); i += blockDim.x) w.qtab[i] = A.qam[i];
+    for (uint32_t j = threadIdx.x; j < 98; j += blockDim.x) {
+        const uint32_t bo = (2 * j) >> 3;
+        w.pccs[j] = A.qpsk[bits_of(dpcc[bo] ^ A.pcc_seq[bo], 0u, 2 * j, 2)];
+    }
+    for (uint32_t i = threadIdx.x; i < A.N_TS; i += blockDim.x) w.wrow[i] = A.W[(w.P.codebook * A.N_TX + w.ant) * A.N_TS + i];
+    __syncthreads();
+    for (uint32_t n = threadIdx.x; n < w.Nd; n += blockDim.x) fa[n] = w.bin(w.code(l, n), n, l);
+    __syncthreads();
+    float2* dst = A.big + size_t(pa) * A.big_len + w.bsym(l);
+    const uint32_t Nd = w.Nd;
+    fft_store<+1>(fa, fb, A.tw, A.plan, 1, [&](uint32_t, uint32_t n, float2 v) {
+        if (l == 0) {
+            for (uint32_t i = A.STF_CP + n;; i -= Nd) {  // the STF CP may exceed one FFT length
+                dst[i] = cscale(v, k_cover[min(i / A.pattern_len, 8u)]);
+                if (i < Nd) break;
+            }
+        } else {
+            dst[A.CP + n] = v;
+            if (n >= Nd - A.CP) dst[A.CP + n - Nd] = v;
+        }
+    });
+}
+
+__global__ void __launch_bounds__(256) tx_big_resample_kernel(tx_args A, uint32_t total) {
+    const uint32_t pa = blockIdx.y, m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= A.S) return;
+    float2* out = reinterpret_cast<float2*>(A.out) + size_t(pa) * A.S;
+    // outputs m with delay + m M < (total + hl) L: the packet and its flush samples
+    const uint64_t tb = uint64_t(total + A.hl) * A.L;
+    const uint32_t m_hi = tb > A.delay ? static_cast<uint32_t>(min<uint64_t>((tb - A.delay + A.M - 1) / A.M, A.n_keep)) : 0u;
+    if (m >= m_hi) {
+        out[m] = make_float2(0.f, 0.f);
+        return;
+    }
+    const tx_pkt& P = A.pk[pa / A.N_TX];
+    const float2* x = A.big + size_t(pa) * A.big_len;
+    const uint64_t t = A.delay + uint64_t(m) * A.M;
+    const int64_t p = static_cast<int64_t>(t / A.L);
+    const uint32_t ph = static_cast<uint32_t>(t % A.L);
+    float ar = 0.f, ai = 0.f;
+    for (uint32_t d = 0; d <= A.hl; ++d) {
+        const int64_t j = p - d;
+        if (j < 0 || j >= int64_t(total)) continue;  // zero history / flush: fma(0, h, a) == a
+        const float hv = A.taps[ph + d * A.L];
+        const float2 xv = x[j];
+        ar = fmaf(xv.x, hv, ar);
+        ai = fmaf(xv.y, hv, ai);
+    }
+    float2 y = make_float2(ar, ai);
+    if (P.do_mix) y = cmul(y, phasor(P.ph0 + static_cast<double>(m) * P.inc));
+    out[m] = y;
+}
+
 size_t tx_lds_bytes(const tx_args& a) {
     const bool wave = a.plan.N == 1024;
     return (size_t(a.lin_len) + (wave ? 0 : a.bufB_len + a.plan.N) + 256 + 98 + 8) * sizeof(float2) +
@@ -895,6 +981,16 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
             else DNRP_TXS(TXS_SM, false);
         }
 #undef DNRP_TXS
+        return hipGetLastError();
+    }
+    if (a.big) {
+        if (a.N_bps > 8 || a.stage_bytes || a.N_TS > 8) return hipErrorInvalidValue;
+        const uint32_t total = a.STF_CP + a.N_DF * a.CP + (a.N_DF + 1) * a.plan.N;
+        if (total > a.big_len) return hipErrorInvalidValue;
+        const size_t lds = (2 * size_t(a.plan.N) + 256 + 98 + 8) * sizeof(float2);
+        if (lds > 160 * 1024) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(tx_big_sym_kernel, dim3(n * a.N_TX * (a.N_DF + 1)), dim3(TX_BIG_THREADS), lds, st, a);
+        hipLaunchKernelGGL(tx_big_resample_kernel, dim3((a.S + 255) / 256, n * a.N_TX), dim3(256), 0, st, a, total);
         return hipGetLastError();
     }
     const bool wave = a.plan.N == 1024;

@@ -45,6 +45,9 @@ PARITY_CASES = {
     # u = 1 at the same rate: N_b_DFT_os = 8192, the STF front end's chunked layout (rx_stf_ant_kernel)
     # and the generic FFT front end with one symbol per pass, twiddles through the L1 (rx_fft_kernel)
     "u1_in_u8b16": ((1, 16, 1, 1, 0, 4), (8, 16, 1, 1, 10, 9), 1, (20.0,), 0),
+    # C4's packet at os_min = 2: N_b_DFT_os = 2048, 45-tap resamplers, TX through the DECT-rate scratch
+    # (tx_big_sym_kernel) and the RX generic FFT front end
+    "os2_C4": ((8, 16, 1, 1, 5, 8), (8, 16, 4, 2, 10, 9), 1, (30.0,), 0),
 }
 
 
