@@ -167,6 +167,17 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         for (const auto& w : geo::W_matrix(t->tm.N_TS, t->tm.N_TX, cb, &s)) W.push_back(make_float2(w.real(), w.imag()));
         t->wscale.push_back(s);
         t->wscale_opt.push_back(geo::W_scaling_optimal_DAC(t->tm.N_TS, t->tm.N_TX, cb));
+        // one nonzero entry in every antenna row (tx.hip TXS_TXDIV1)
+        bool oh = true;
+        for (uint32_t a = 0; a < t->tm.N_TX; ++a) {
+            uint32_t nzc = 0;
+            for (uint32_t ts = 0; ts < t->tm.N_TS; ++ts) {
+                const float2 w = W[(size_t(cb) * t->tm.N_TX + a) * t->tm.N_TS + ts];
+                nzc += (w.x != 0.f || w.y != 0.f) ? 1u : 0u;
+            }
+            oh = oh && nzc == 1;
+        }
+        t->w_onehot.push_back(oh ? 1 : 0);
     }
     t->pdc_off_h = m.pdc_sym_off;
     // transmit diversity TS pair (A | B << 4) per PCC/PDC cell into the code words (kernels.hpp CODE_*)
@@ -558,7 +569,7 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, con
         a.n_sym_op = plan->n_sym_op;
         // the zero-forced pilots next to the SNR sums (the fused PDC receiver's source), where the
         // plan's ops fit below the zero op
-        if (ctx->zd.p && plan->n_dops + 1 <= ctx->zd_dops) {
+        if (ctx->rx_fused && ctx->zd.p && plan->n_dops + 1 <= ctx->zd_dops) {
             a.zd = ctx->zd.as<float2>();
             a.zd_dops = ctx->zd_dops;
             a.zd_row = ctx->zd_row;
@@ -865,6 +876,9 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
             const char* mf_env = std::getenv("DNRP_TX_MFMA");
             a.mfma = (mf_env && std::atoi(mf_env)) ? 1u : 0u;
             a.code_bin = t->code_bin.as<uint32_t>();
+            a.onehot = t->tm.txdiv ? 1u : 0u;
+            for (uint32_t i = 0; i < n && a.onehot; ++i)
+                a.onehot = t->w_onehot[desc[i].codebook_index] ? 1u : 0u;
             a.pcc_syms = t->pcc_syms;
             a.n_pieces = static_cast<uint32_t>((int64_t(a.n_keep) - mfirst0 + 1279) / 1280);
             // enough wavefronts for ~8 rounds of 16 per CU; each extra segment costs one history FFT
@@ -944,16 +958,18 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         ctx->rx_snr_front = !e || std::atoi(e);
         const char* f = std::getenv("DNRP_RX_FUSED");
         ctx->rx_fused = ctx->rx_snr_front && f && std::atoi(f);
-        // zero-forced DRS pilots of every slot: at most one DRS symbol per 5 symbols (N_eff_TX <= 4)
-        // plus the zero op
+        // zero-forced DRS pilots of every slot (the fused receiver's only): at most one DRS symbol per
+        // 5 symbols (N_eff_TX <= 4) plus the zero op
         ctx->zd_row = 14 * ctx->cfg.b_max;
         ctx->zd_dops = std::min<uint32_t>(dev::RX_MAX_DOPS, (cap_max + 4) / 5 + 2) + 1;
         const size_t zbytes = size_t(n) * ctx->zd_dops * ctx->cfg.N_TX_max * 4 * ctx->zd_row * sizeof(float2);
-        if (!ctx->zd.ensure(zbytes)) return DNRP_ENOMEM;
-        const auto key = std::make_tuple(ctx->zd.p, ctx->zd_dops, ctx->zd_row, ctx->cfg.N_TX_max);
-        if (key != ctx->zd_key) {  // a new layout: the zero op of every slot (and all else) zeroed once
-            HIPCHK(hipMemsetAsync(ctx->zd.p, 0, ctx->zd.n, st));
-            ctx->zd_key = key;
+        if (ctx->rx_fused) {
+            if (!ctx->zd.ensure(zbytes)) return DNRP_ENOMEM;
+            const auto key = std::make_tuple(ctx->zd.p, ctx->zd_dops, ctx->zd_row, ctx->cfg.N_TX_max);
+            if (key != ctx->zd_key) {  // a new layout: the zero op of every slot (and all else) zeroed once
+                HIPCHK(hipMemsetAsync(ctx->zd.p, 0, ctx->zd.n, st));
+                ctx->zd_key = key;
+            }
         }
     }
     auto* pin = static_cast<dev::rx_pkt_in*>(ctx->st_rxin.get(sizeof(dev::rx_pkt_in) * n));

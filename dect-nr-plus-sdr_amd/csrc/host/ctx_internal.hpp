@@ -108,6 +108,7 @@ struct tx_tables {
     uint32_t pcc_syms = 0;  // bit l: symbol l carries PCC cells
     uint32_t npp = 0;  // floats in taps_pp
     std::vector<float> wscale, wscale_opt;  // per codebook: standard / optimal_scaling_DAC
+    std::vector<uint8_t> w_onehot;           // per codebook: one nonzero entry in every antenna row
     std::vector<uint32_t> pdc_off_h;  // host copy of maps.pdc_sym_off
 };
 

@@ -62,6 +62,7 @@ struct tx_args {
     const uint32_t* code_bin;  // [N_DF+1][1024] cell code of every FFT bin (0: empty)
     uint32_t n_pieces, n_seg, piece_per_seg, stream;
     uint32_t pcc_syms;         // bit l: symbol l (< 32) carries PCC cells
+    uint32_t onehot;           // transmit diversity with one nonzero W entry per antenna row (every packet)
     // N_b_DFT_os > 1024 (beyond the block path's registers): every symbol's cyclic-prefixed DECT-rate
     // samples through a scratch [packet][antenna][big_len] (tx_big_sym_kernel, tx_big_resample_kernel)
     float2* big;

@@ -422,7 +422,10 @@ constexpr uint32_t TXS_XB = 32;                       // FFT exchange / PDC byte
 constexpr uint32_t TXS_WROW = 12;                     // beamforming row (8) + descrambled PCC bytes (32 B)
 static_assert(TXS_XB + WFFT_XB <= TXS_CARRY + TXS_PIECE, "FFT exchange buffer must fit behind the carry");
 
-enum { TXS_SISO = 0, TXS_TXDIV = 1, TXS_SM = 2 };
+// TXS_TXDIV1: transmit diversity where every antenna's W row holds one nonzero entry (TM5 codebook 0:
+// W = I / 2): the antenna sends one stream of each SFBC pair, so a bin needs one PDC symbol and one
+// complex product, not two (the other product is an exact zero in TXS_TXDIV)
+enum { TXS_SISO = 0, TXS_TXDIV = 1, TXS_SM = 2, TXS_TXDIV1 = 3 };
 
 __device__ __forceinline__ uint32_t txs_sym(uint32_t r, uint32_t N_DF) {  // symbol of piece r (N_DF+1: none)
     return r <= 1 ? 0u : (r - 1 <= N_DF ? r - 1 : N_DF + 1);
@@ -440,6 +443,8 @@ struct txs_wave {
     uint32_t pkt, ant, lane;
     float2 *buf, *wrow, *qtab;
     float2 w0;  // unscaled W[ant][0]: the STF bins carry scale_stf alone (tx.cpp:864-871)
+    float2 wsel;  // TXS_TXDIV1: the antenna's one nonzero W entry, scale_df applied
+    uint32_t tsel;  // TXS_TXDIV1: its stream
     const uint8_t *dpdc, *cpdc;
     uint32_t pdc_bytes;
 
@@ -487,6 +492,20 @@ struct txs_wave {
     template <int MODE, bool Q8, bool PCC>
     __device__ float2 bin_df(uint32_t c, const uint8_t* sb, uint32_t ab, const uint8_t* pcb) const {
         const uint32_t ty = c & CODE_MASK, j = c & CODE_J_MASK, pr = (c >> CODE_PAIR_SHIFT) & 0xFFu;
+        if constexpr (MODE == TXS_TXDIV1) {
+            // the pair (tA, tB) of this cell: the antenna's stream is tA (x0 = symbol j) or tB (the
+            // flipped partner, symbol j ^ 1) or neither; DRS cells carry their stream in tA
+            const bool ua = (pr & 0xFu) == tsel, ub = (pr >> 4) == tsel;
+            const uint32_t js = ua ? j : (j ^ 1u);
+            float2 x = pdc_sym<Q8>(sb, ab, js);
+            if (PCC && ty == CODE_PCC) x = pcc_sym(pcb, js);
+            if (!ua) x = (j & 1u) ? make_float2(x.x, -x.y) : make_float2(-x.x, x.y);
+            float2 v = (ua || ub) ? cmul(wsel, x) : make_float2(0.f, 0.f);
+            const float2 d = ua ? cscale(wsel, (j & 8u) ? -1.f : 1.f) : make_float2(0.f, 0.f);
+            v = ty == CODE_DRS ? d : v;
+            v = (ty == CODE_PDC || ty == CODE_DRS || (PCC && ty == CODE_PCC)) ? v : make_float2(0.f, 0.f);
+            return v;
+        }
         float2 x0 = pdc_sym<Q8>(sb, ab, j);
         float2 v, wa_drs = make_float2(0.f, 0.f);
         if (MODE == TXS_SISO) {  // SISO (N_SS = 1): PCC and PDC alike
@@ -594,6 +613,12 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
         // the W row pre-scaled by the data-field scaling (tx.cpp:582-594, 864-871)
         if (lane < A.N_TS) T.wrow[lane] = cscale(A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS + lane], T.P.scale_df);
         T.w0 = A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS];
+        if constexpr (MODE == TXS_TXDIV1) {  // the row's nonzero entry (host-checked: exactly one)
+            T.tsel = 0;
+            for (uint32_t t = 0; t < A.N_TS; ++t)
+                if (nz(A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS + t])) T.tsel = t;
+            T.wsel = cscale(A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS + T.tsel], T.P.scale_df);
+        }
         if (lane < 32) pcb[lane] = lane < 25 ? static_cast<uint8_t>(A.pcc_d[size_t(T.pkt) * 25 + lane] ^ A.pcc_seq[lane]) : 0u;
     }
     __syncthreads();  // the only workgroup barrier: qtab / wrow visible
@@ -965,7 +990,7 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
     if (a.stream) {
         const uint64_t waves = uint64_t(n) * a.N_TX * a.n_seg;
         const dim3 g(static_cast<uint32_t>((waves + TXS_WPG - 1) / TXS_WPG)), b(64 * TXS_WPG);
-        const int mode = a.N_TS == 1 ? TXS_SISO : a.txdiv ? TXS_TXDIV : TXS_SM;
+        const int mode = a.N_TS == 1 ? TXS_SISO : a.txdiv ? (a.onehot ? TXS_TXDIV1 : TXS_TXDIV) : TXS_SM;
 #define DNRP_TXS(MODE, Q8)                                                                                       \
     do {                                                                                                         \
         if (a.mfma) hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8, true>), g, b, tx_stream_lds(), st, a, n);   \
@@ -974,10 +999,12 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
         if (a.N_bps == 8) {
             if (mode == TXS_SISO) DNRP_TXS(TXS_SISO, true);
             else if (mode == TXS_TXDIV) DNRP_TXS(TXS_TXDIV, true);
+            else if (mode == TXS_TXDIV1) DNRP_TXS(TXS_TXDIV1, true);
             else DNRP_TXS(TXS_SM, true);
         } else {
             if (mode == TXS_SISO) DNRP_TXS(TXS_SISO, false);
             else if (mode == TXS_TXDIV) DNRP_TXS(TXS_TXDIV, false);
+            else if (mode == TXS_TXDIV1) DNRP_TXS(TXS_TXDIV1, false);
             else DNRP_TXS(TXS_SM, false);
         }
 #undef DNRP_TXS
