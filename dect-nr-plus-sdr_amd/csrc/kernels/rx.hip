@@ -572,6 +572,61 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
     }
 }
 
+// The compile-time-tap path with SPW consecutive symbols of one (packet, antenna) per wave, one after
+// the other in the same LDS region: the per-wave start (packet tables, sync state, lane twiddles)
+// is paid once per SPW symbols
+#ifndef DNRP_RX_SPW
+#define DNRP_RX_SPW 2
+#endif
+template <int SPW>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) rx_fft_wave_ct_kernel(rx_front_args A) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    constexpr int LR = 9, MR = 10, HLR = 24;
+    const uint32_t nblk = (A.sym_count + SPW - 1) / SPW;
+    const uint32_t blk = blockIdx.x % nblk;
+    const uint32_t a = (blockIdx.x / nblk) % A.N_RX;
+    const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / (nblk * A.N_RX));
+    const uint32_t lane0 = threadIdx.x & 63u;
+    float2* R = smem;
+    const rx_pkt_in in = A.pin[pkt];
+    const rx_pkt_state S = A.st[pkt];
+    const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
+    const float2* src = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in + in.fine_peak;
+    const float2 w1_ = wfft_tw<-1>(A.tw, 4 * (lane0 & 15u)), wl_ = wfft_tw<-1>(A.tw, lane0);
+    const bool to_y = !A.no_y;
+#pragma unroll 1
+    for (int i = 0; i < SPW; ++i) {
+        const uint32_t li = blk * SPW + i;
+        if (li >= A.sym_count) break;
+        // lane index and twiddles opaque per symbol: lane-derived addresses are recomputed in the loop
+        // instead of being hoisted out of it (loop-invariant code motion would spill them)
+        uint32_t lane = threadIdx.x & 63u;
+        float2 w1 = w1_, wl = wl_;
+        asm volatile("" : "+v"(lane), "+v"(w1.x), "+v"(w1.y), "+v"(wl.x), "+v"(wl.y));
+        const uint32_t l = A.sym_list ? A.sym_list[li] : A.sym_first + li;
+        uint32_t so = 0xFFFFu;
+        if (A.snr_part && l < A.n_sym_op) {
+            const auto* sop = reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(reinterpret_cast<uintptr_t>(A.sym_op));
+            so = (sop[l >> 1] >> (16 * (l & 1u))) & 0xFFFFu;
+        }
+        const rx_span_t sp = rx_span<LR, MR, HLR>(A, l);
+        if (i) __builtin_amdgcn_wave_barrier();  // the previous symbol's reads of R are done
+        stage_span_lo<20>(R, src, sp.in0, sp.n_in, q_lo, q_hi, lane, 64);
+        __builtin_amdgcn_wave_barrier();
+        float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
+        const bool drs = so != 0xFFFFu;
+        rx_resample_ct<LR, MR, HLR>(A, in, S, sp, R, lane);
+        rx_fft_bins<true>(A, S, R, lane, [&](uint32_t k, float2 v) {
+            if (to_y) Yrow[k] = v;
+            if (drs) R[k] = v;
+        }, w1, wl);
+        if (drs) {
+            __builtin_amdgcn_wave_barrier();
+            rx_drs_partials(A, pkt, a, l, so, R, lane);
+        }
+    }
+}
+
 bool rx_stream_taps_match(const float* h, size_t n) {  // run-time RX taps == compiled-in taps, bitwise
     if (n != static_cast<size_t>(taps_rx_9_10::N)) return false;
     for (size_t i = 0; i < n; ++i)
@@ -624,8 +679,12 @@ hipError_t launch_rx_fft(const rx_front_args& a_in, uint32_t n, hipStream_t st) 
             // not 16) and no twiddle-load latency in the passes (PDC launch 5.44 -> 5.30 ms per C4
             // chunk, same box)
             const size_t lds1 = size_t(rxw_region(9, 10, W)) * sizeof(float2);
-            hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 1, true>), dim3(n * a.N_RX * a.sym_count), dim3(64),
-                               lds1, st, a);
+            if (DNRP_RX_SPW > 1)
+                hipLaunchKernelGGL((rx_fft_wave_ct_kernel<DNRP_RX_SPW>),
+                                   dim3(n * a.N_RX * ((a.sym_count + DNRP_RX_SPW - 1) / DNRP_RX_SPW)), dim3(64), lds1, st, a);
+            else
+                hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 1, true>), dim3(n * a.N_RX * a.sym_count), dim3(64),
+                                   lds1, st, a);
         } else {
             const size_t lds = (Nd + (a.npp + 1) / 2 + RXW_SYMS * size_t(rxw_region(9, 10, W))) * sizeof(float2);
             hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, false>), g, b, lds, st, a);
