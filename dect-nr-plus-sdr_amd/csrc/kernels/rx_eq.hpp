@@ -106,10 +106,24 @@ __device__ __forceinline__ void unit_stage_b(const rx_cells_args& A, const cell_
     }
     const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
     const uint32_t yoff = a.l * A.Nf_pad;
+    if constexpr (NT > 1) {
+        // the pair's two cells are neighbours except across DC: one 16-B load per antenna (8-B
+        // aligned: unaligned dwordx4, k0 + 1 <= N_b_OCC < Nf_pad stays in the row), the DC pair's
+        // second cell reloaded
 #pragma unroll
-    for (int r = 0; r < NRX; ++r) {
-        b.r0[r] = Yp[r * ast + yoff + a.k0];
-        if constexpr (NT > 1) b.r1[r] = Yp[r * ast + yoff + a.k1];
+        for (int r = 0; r < NRX; ++r) {
+            float4 v;
+            __builtin_memcpy(&v, Yp + r * ast + yoff + a.k0, 16);
+            b.r0[r] = make_float2(v.x, v.y);
+            b.r1[r] = make_float2(v.z, v.w);
+        }
+        if (a.k1 != a.k0 + 1) {
+#pragma unroll
+            for (int r = 0; r < NRX; ++r) b.r1[r] = Yp[r * ast + yoff + a.k1];
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < NRX; ++r) b.r0[r] = Yp[r * ast + yoff + a.k0];
     }
     // the unit's scrambling bits [jj N_bps, (jj + cells) N_bps) lie in at most 3 bytes
     // (loads clamped to the last byte and kept raw: nothing here waits on the loads in flight)
