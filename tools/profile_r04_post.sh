@@ -11,3 +11,8 @@ for tag in c4 c4sm fused; do
   cp $src/summary.txt $d/pmc_sq_summary$suf.txt
   cp $(find $src/trace -name "*kernel_stats.csv" | head -1) $d/kernel_stats_profile_run$suf.csv
 done
+# slots per launch of each summary (bench.py _pmc_chunk)
+cat > $d/pmc_meta.json <<'J'
+{"traffic.json": 16384, "valu.json": 16384, "traffic_fused.json": 16384, "valu_fused.json": 16384,
+ "traffic_c4sm.json": 4096, "valu_c4sm.json": 4096}
+J
