@@ -859,14 +859,18 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
     a.stream = 0;
     if (wave && t->code_bin.p && dev::tx_stream_taps_match(t->rs.h.data(), t->rs.h.size()) && a.L == 10 && a.M == 9 && a.hl == 22 && a.CP == 128 && a.STF_CP == 1280 &&
         a.pattern_len * 9 == a.STF_CP + 1024 && S % 2 == 0 && (reinterpret_cast<uintptr_t>(iq_out) & 15u) == 0) {
-        // every symbol's PDC bytes (SFBC partners included) within its 1024-byte staging window
+        // every symbol's PDC bytes (SFBC partners included) within its staging window: 1 KiB, spatial
+        // multiplexing 4 KiB (tx.hip TXS_SBW_SM: its first KiB prefetched, the rest loaded per symbol)
         const uint32_t bpc = t->tm.N_SS * t->q.N_bps;
-        bool fits = true;
-        for (uint32_t l = 1; l <= t->q.N_DF_symb && fits; ++l) {
+        const bool sm = t->tm.N_TS > 1 && !t->tm.txdiv;
+        uint64_t span = 0;
+        for (uint32_t l = 1; l <= t->q.N_DF_symb; ++l) {
             const uint64_t j0 = t->pdc_off_h[l] & ~1u, j1 = (uint64_t(t->pdc_off_h[l + 1]) + 1) & ~1ull;
             const uint64_t ab = ((j0 * bpc) >> 3) & ~15ull, hi = ((j1 * bpc + 7) >> 3) + 1;
-            fits = hi - ab <= 1024;
+            span = std::max(span, hi - ab);
         }
+        const bool fits = span <= (sm ? 4096u : 1024u);
+        a.sb_chunks = static_cast<uint32_t>((span + 1023) / 1024);
         const int qlo0 = -static_cast<int>((a.p_star + 8) / 9);
         const int64_t mfirst0 = int64_t(a.m_star) + 10 * qlo0;
         if (fits) {
@@ -876,7 +880,7 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
             const char* mf_env = std::getenv("DNRP_TX_MFMA");
             a.mfma = (mf_env && std::atoi(mf_env)) ? 1u : 0u;
             a.code_bin = t->code_bin.as<uint32_t>();
-            a.onehot = t->tm.txdiv ? 1u : 0u;
+            a.onehot = t->tm.N_TS > 1 ? 1u : 0u;  // transmit diversity or spatial multiplexing
             for (uint32_t i = 0; i < n && a.onehot; ++i)
                 a.onehot = t->w_onehot[desc[i].codebook_index] ? 1u : 0u;
             a.pcc_syms = t->pcc_syms;

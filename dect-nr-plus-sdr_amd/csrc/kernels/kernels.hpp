@@ -63,6 +63,7 @@ struct tx_args {
     uint32_t n_pieces, n_seg, piece_per_seg, stream;
     uint32_t pcc_syms;         // bit l: symbol l (< 32) carries PCC cells
     uint32_t onehot;           // transmit diversity with one nonzero W entry per antenna row (every packet)
+    uint32_t sb_chunks;        // spatial multiplexing: 1 KiB chunks of a symbol's PDC staging window (<= 4)
     // N_b_DFT_os > 1024 (beyond the block path's registers): every symbol's cyclic-prefixed DECT-rate
     // samples through a scratch [packet][antenna][big_len] (tx_big_sym_kernel, tx_big_resample_kernel)
     float2* big;

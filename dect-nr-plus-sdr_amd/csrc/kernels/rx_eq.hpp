@@ -307,9 +307,32 @@ __device__ __forceinline__ void emit_sym64(float2 x, uint32_t base, uint32_t b_f
         const uint32_t r = r0 + i;
         return static_cast<uint32_t>(bits >> (8 * (r >> 3) + 7 - (r & 7u))) & 1u;
     };
+    uint32_t w[4];  // the symbol's LLRs as int16 pairs
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k)
-        if (k < N_bps) llr[base + k] = q16(sbit(k) ? -L[k] : L[k]);
+    for (uint32_t k = 0; k < 8; k += 2) {
+        const int16_t v0 = q16(sbit(k) ? -L[k] : L[k]), v1 = q16(sbit(k + 1) ? -L[k + 1] : L[k + 1]);
+        w[k / 2] = static_cast<uint16_t>(v0) | (static_cast<uint32_t>(static_cast<uint16_t>(v1)) << 16);
+    }
+    // one store per symbol where the width allows (N_bps LLRs = 2 N_bps bytes at their natural
+    // alignment), else per LLR
+    int16_t* dst = llr + base;
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
+    if (N_bps == 8 && (ad & 15u) == 0) {
+        *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else if (N_bps == 4 && (ad & 7u) == 0) {
+        *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
+    } else if ((N_bps == 6 || N_bps == 2) && (ad & 3u) == 0) {
+        uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+        d32[0] = w[0];
+        if (N_bps == 6) {
+            d32[1] = w[1];
+            d32[2] = w[2];
+        }
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k)
+            if (k < N_bps) dst[k] = static_cast<int16_t>(k & 1u ? w[k / 2] >> 16 : w[k / 2] & 0xFFFFu);
+    }
 }
 
 template <int NRX, int NT>

@@ -425,7 +425,14 @@ static_assert(TXS_XB + WFFT_XB <= TXS_CARRY + TXS_PIECE, "FFT exchange buffer mu
 // TXS_TXDIV1: transmit diversity where every antenna's W row holds one nonzero entry (TM5 codebook 0:
 // W = I / 2): the antenna sends one stream of each SFBC pair, so a bin needs one PDC symbol and one
 // complex product, not two (the other product is an exact zero in TXS_TXDIV)
-enum { TXS_SISO = 0, TXS_TXDIV = 1, TXS_SM = 2, TXS_TXDIV1 = 3 };
+// TXS_SM1: spatial multiplexing with one nonzero W entry per antenna row (TM6 codebook 0): the antenna
+// sends one of the N_SS symbols of a cell, not a sum over all of them
+enum { TXS_SISO = 0, TXS_TXDIV = 1, TXS_SM = 2, TXS_TXDIV1 = 3, TXS_SM1 = 4 };
+// spatial multiplexing: N_SS streams of N_bps bits per cell put up to ~3 KB of PDC bytes into a symbol
+// (4 streams of 64-QAM: 2.6 KB); its staging window is 4 KiB, the first KiB prefetched with the other
+// modes' window, the rest loaded when the symbol starts (A.sb_chunks 1 KiB chunks, host-checked)
+constexpr uint32_t TXS_SBW_SM = 4096;
+static_assert(TXS_XB * 8 + TXS_SBW_SM <= (TXS_CARRY + TXS_PIECE) * 8, "staging window behind the carry");
 
 __device__ __forceinline__ uint32_t txs_sym(uint32_t r, uint32_t N_DF) {  // symbol of piece r (N_DF+1: none)
     return r <= 1 ? 0u : (r - 1 <= N_DF ? r - 1 : N_DF + 1);
@@ -481,30 +488,47 @@ struct txs_wave {
         const uint32_t q = (uint32_t(pcb[bo]) >> (6u - ((2 * j) & 7u))) & 3u;
         return make_float2((q & 2u) ? -0.70710678f : 0.70710678f, (q & 1u) ? -0.70710678f : 0.70710678f);
     }
-    template <bool Q8>
+    // SBW: bytes of the staging window (1 KiB; spatial multiplexing TXS_SM up to 4 KiB)
+    template <bool Q8, uint32_t SBW = 1024>
     __device__ float2 pdc_sym(const uint8_t* sb, uint32_t ab, uint32_t s) const {
-        if (Q8) return qtab[sb[(s - ab) & 1023u]];
-        const uint32_t lb = s * A->N_bps - 8 * ab, bo = (lb >> 3) & 1022u;
-        return qtab[bits_of(sb[bo], sb[bo + 1], lb, A->N_bps)];
+        if (Q8) return qtab[sb[(s - ab) & (SBW - 1)]];
+        // byte bo of the window and its successor (the host keeps both inside it; the masks only bound
+        // the LDS index)
+        const uint32_t lb = s * A->N_bps - 8 * ab, bo = (lb >> 3) & (SBW - 1);
+        return qtab[bits_of(sb[bo], sb[(bo + 1) & (SBW - 1)], lb, A->N_bps)];
     }
     // value of FFT bin n with cell code c in DF symbol l >= 1, scaled (tx.cpp:944-1116, 729-860, 862-871)
     // MODE: TXS_SISO (N_TS = 1), TXS_TXDIV (transmit diversity), TXS_SM (N_SS streams, PCC paired)
     template <int MODE, bool Q8, bool PCC>
     __device__ float2 bin_df(uint32_t c, const uint8_t* sb, uint32_t ab, const uint8_t* pcb) const {
         const uint32_t ty = c & CODE_MASK, j = c & CODE_J_MASK, pr = (c >> CODE_PAIR_SHIFT) & 0xFFu;
-        if constexpr (MODE == TXS_TXDIV1) {
+        if constexpr (MODE == TXS_TXDIV1 || MODE == TXS_SM1) {
             // the pair (tA, tB) of this cell: the antenna's stream is tA (x0 = symbol j) or tB (the
-            // flipped partner, symbol j ^ 1) or neither; DRS cells carry their stream in tA
+            // flipped partner, symbol j ^ 1) or neither; DRS cells carry their stream in tA. Sign flips
+            // and the choice of result as bit masks: no control flow (the compiler turns value selects
+            // around the table reads into exec-mask branches, which serialise the 16 bins' LDS reads).
+            // TXS_SM1: a PDC cell carries the antenna's stream symbol j N_SS + tsel, unflipped (the PCC
+            // stays transmit-diversity paired)
+            constexpr bool SM1 = MODE == TXS_SM1;
             const bool ua = (pr & 0xFu) == tsel, ub = (pr >> 4) == tsel;
-            const uint32_t js = ua ? j : (j ^ 1u);
-            float2 x = pdc_sym<Q8>(sb, ab, js);
-            if (PCC && ty == CODE_PCC) x = pcc_sym(pcb, js);
-            if (!ua) x = (j & 1u) ? make_float2(x.x, -x.y) : make_float2(-x.x, x.y);
-            float2 v = (ua || ub) ? cmul(wsel, x) : make_float2(0.f, 0.f);
-            const float2 d = ua ? cscale(wsel, (j & 8u) ? -1.f : 1.f) : make_float2(0.f, 0.f);
-            v = ty == CODE_DRS ? d : v;
-            v = (ty == CODE_PDC || ty == CODE_DRS || (PCC && ty == CODE_PCC)) ? v : make_float2(0.f, 0.f);
-            return v;
+            const bool pdc = ty == CODE_PDC;
+            const uint32_t jp = j ^ (ua ? 0u : 1u);
+            const uint32_t js = SM1 && pdc ? j * A->N_SS + tsel : jp;
+            float2 x = pdc_sym<Q8, SM1 ? TXS_SBW_SM : 1024u>(sb, ab, js);
+            if constexpr (PCC) {
+                const float2 px = pcc_sym(pcb, jp);
+                x = ty == CODE_PCC ? px : x;
+            }
+            const uint32_t nf = (ua || (SM1 && pdc)) ? 0u : 0x80000000u;  // the partner's flip (-re, +im) / (+re, -im)
+            const uint32_t fx = (j & 1u) ? 0u : nf, fy = (j & 1u) ? nf : 0u;
+            x = make_float2(__uint_as_float(__float_as_uint(x.x) ^ fx), __uint_as_float(__float_as_uint(x.y) ^ fy));
+            const float2 v = cmul(wsel, x);
+            const uint32_t ds = (j & 8u) ? 0x80000000u : 0u;  // DRS value +-1 times the W entry
+            const float2 d = make_float2(__uint_as_float(__float_as_uint(wsel.x) ^ ds), __uint_as_float(__float_as_uint(wsel.y) ^ ds));
+            const bool kv = (pdc && (SM1 || ua || ub)) || (PCC && ty == CODE_PCC && (ua || ub)), kd = ty == CODE_DRS && ua;
+            const uint32_t mv = 0u - static_cast<uint32_t>(kv), md = 0u - static_cast<uint32_t>(kd);
+            return make_float2(__uint_as_float((__float_as_uint(v.x) & mv) | (__float_as_uint(d.x) & md)),
+                               __uint_as_float((__float_as_uint(v.y) & mv) | (__float_as_uint(d.y) & md)));
         }
         float2 x0 = pdc_sym<Q8>(sb, ab, j);
         float2 v, wa_drs = make_float2(0.f, 0.f);
@@ -524,7 +548,7 @@ struct txs_wave {
             if (MODE == TXS_TXDIV) wa_drs = wrow[pr & 0xFu];
         } else {
             v = make_float2(0.f, 0.f);
-            for (uint32_t ss = 0; ss < A->N_SS; ++ss) v = cadd(v, cmul(wrow[ss], pdc_sym<Q8>(sb, ab, j * A->N_SS + ss)));
+            for (uint32_t ss = 0; ss < A->N_SS; ++ss) v = cadd(v, cmul(wrow[ss], pdc_sym<Q8, TXS_SBW_SM>(sb, ab, j * A->N_SS + ss)));
         }
         // DRS codes carry their stream in the pair field: in transmit diversity the pair's first W
         // entry above is the DRS weight (no second read)
@@ -613,7 +637,7 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
         // the W row pre-scaled by the data-field scaling (tx.cpp:582-594, 864-871)
         if (lane < A.N_TS) T.wrow[lane] = cscale(A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS + lane], T.P.scale_df);
         T.w0 = A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS];
-        if constexpr (MODE == TXS_TXDIV1) {  // the row's nonzero entry (host-checked: exactly one)
+        if constexpr (MODE == TXS_TXDIV1 || MODE == TXS_SM1) {  // the row's nonzero entry (host-checked: exactly one)
             T.tsel = 0;
             for (uint32_t t = 0; t < A.N_TS; ++t)
                 if (nz(A.W[(T.P.codebook * A.N_TX + T.ant) * A.N_TS + t])) T.tsel = t;
@@ -706,6 +730,14 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
             // stage this symbol's bytes, prefetch the next symbol's
             const uint32_t ab = (l >= 1) ? T.stage_base(l) : 0u;
             if (l >= 1) reinterpret_cast<uint4*>(sb)[lid] = make_uint4(pre.x ^ prc.x, pre.y ^ prc.y, pre.z ^ prc.z, pre.w ^ prc.w);
+            if constexpr (MODE == TXS_SM || MODE == TXS_SM1) {
+                if (l >= 1)
+                    for (uint32_t c = 1; c < A.sb_chunks; ++c) {  // the window's other KiBs, not prefetched
+                        uint4 d, e;
+                        T.chunk(ab + 1024 * c + 16 * lid, d, e);
+                        reinterpret_cast<uint4*>(sb)[64 * c + lid] = make_uint4(d.x ^ e.x, d.y ^ e.y, d.z ^ e.z, d.w ^ e.w);
+                    }
+            }
             __builtin_amdgcn_wave_barrier();
             if (l == 0) {
 #pragma unroll
@@ -715,7 +747,11 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
                 for (int m = 0; m < 16; ++m) v[m] = T.template bin_df<MODE, Q8, true>(cd[m], sb, ab, pcb);
             } else {
 #pragma unroll
-                for (int m = 0; m < 16; ++m) v[m] = T.template bin_df<MODE, Q8, false>(cd[m], sb, ab, pcb);
+                for (int m = 0; m < 16; ++m) {
+                    // two groups of 8 bins: the table reads of 8 bins in flight at a time (all 16 spill)
+                    if ((MODE == TXS_TXDIV1 || MODE == TXS_SM1) && m == 8) __builtin_amdgcn_sched_barrier(0);
+                    v[m] = T.template bin_df<MODE, Q8, false>(cd[m], sb, ab, pcb);
+                }
             }
             __builtin_amdgcn_wave_barrier();
             {
@@ -990,7 +1026,7 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
     if (a.stream) {
         const uint64_t waves = uint64_t(n) * a.N_TX * a.n_seg;
         const dim3 g(static_cast<uint32_t>((waves + TXS_WPG - 1) / TXS_WPG)), b(64 * TXS_WPG);
-        const int mode = a.N_TS == 1 ? TXS_SISO : a.txdiv ? (a.onehot ? TXS_TXDIV1 : TXS_TXDIV) : TXS_SM;
+        const int mode = a.N_TS == 1 ? TXS_SISO : a.txdiv ? (a.onehot ? TXS_TXDIV1 : TXS_TXDIV) : (a.onehot ? TXS_SM1 : TXS_SM);
 #define DNRP_TXS(MODE, Q8)                                                                                       \
     do {                                                                                                         \
         if (a.mfma) hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8, true>), g, b, tx_stream_lds(), st, a, n);   \
@@ -1000,11 +1036,13 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
             if (mode == TXS_SISO) DNRP_TXS(TXS_SISO, true);
             else if (mode == TXS_TXDIV) DNRP_TXS(TXS_TXDIV, true);
             else if (mode == TXS_TXDIV1) DNRP_TXS(TXS_TXDIV1, true);
+            else if (mode == TXS_SM1) DNRP_TXS(TXS_SM1, true);
             else DNRP_TXS(TXS_SM, true);
         } else {
             if (mode == TXS_SISO) DNRP_TXS(TXS_SISO, false);
             else if (mode == TXS_TXDIV) DNRP_TXS(TXS_TXDIV, false);
             else if (mode == TXS_TXDIV1) DNRP_TXS(TXS_TXDIV1, false);
+            else if (mode == TXS_SM1) DNRP_TXS(TXS_SM1, false);
             else DNRP_TXS(TXS_SM, false);
         }
 #undef DNRP_TXS

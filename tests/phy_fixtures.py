@@ -62,6 +62,13 @@ TX_ONLY_CASES = {
     "tm10_txdiv8": ((1, 2, 1, 2, 10, 4), (1, 2, 8, 1, 10, 9), 1, (), 0),
     "tm10_u8b16": ((8, 16, 1, 1, 10, 8), (8, 16, 8, 1, 10, 9), 1, (), 0),
     "tm11_sm8": ((1, 4, 1, 1, 11, 2), (1, 4, 8, 1, 10, 9), 1, (), 0),
+    # 4 spatial streams at mu8 b16 on the streaming TX kernel: 2.6 / 3.5 KB of PDC bytes per symbol,
+    # the 4 KiB staging window (tx.hip TXS_SBW_SM)
+    "tm6_u8b16_64qam": ((8, 16, 1, 1, 6, 6), (8, 16, 4, 1, 10, 9), 1, (), 0),
+    "tm6_u8b16_256qam": ((8, 16, 1, 1, 6, 8), (8, 16, 4, 1, 10, 9), 1, (), 0),
+    # the streaming kernel's multi-bit byte path (N_bps < 8: symbols straddle bytes), SISO and TM5
+    "u8b16_64qam": ((8, 16, 1, 1, 0, 6), (8, 16, 1, 1, 10, 9), 1, (), 0),
+    "tm5_u8b16_16qam": ((8, 16, 1, 1, 5, 4), (8, 16, 4, 1, 10, 9), 1, (), 0),
 }
 
 
