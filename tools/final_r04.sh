@@ -20,7 +20,7 @@ grep '^{"metric"' $out/bench_rocprof.log | tail -1 > $out/bench_c4_under_rocprof
 stats=$(find $out/trace -name "*kernel_stats.csv" | head -1)
 trace=$(find $out/trace -name "*kernel_trace.csv" | head -1)
 cp $stats $out/kernel_stats_c4_default_bench.csv
-python3 tools/trace_by_grid.py $trace --tail 16 > $out/kernel_by_grid_c4_default_serial_step.txt
+python3 tools/trace_by_grid.py $trace --tail 4 > $out/kernel_by_grid_c4_default_serial_step.txt
 python3 tools/trace_by_grid.py $trace > $out/kernel_by_grid_c4_default_all.txt
 rm -rf $out/trace
 head -20 $out/kernel_by_grid_c4_default_serial_step.txt
