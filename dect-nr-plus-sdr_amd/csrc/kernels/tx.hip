@@ -572,16 +572,28 @@ struct txs_wave {
 // descriptor's range (dropped by the hardware) and outputs >= n_keep are zero, so every call issues
 // the same stores -- the next piece's input waits stay counted (vmcnt(n)), not a drain of them.
 // inner (uniform): [m0, m0 + N) inside [0, n_keep), no per-element range work.
-template <int N>
+// SHIFT: output i staged at buf[i + head], so that every pair sits on a 16-B boundary (one b128 read,
+// conflict-free, instead of two b64 reads at a 16-B lane stride: 2-way conflicts)
+template <int N, bool SHIFT = false>
 __device__ __forceinline__ void txs_emit(const float2* buf, __amdgpu_buffer_rsrc_t orsrc, uint32_t head, uint32_t lid,
                                          int m0, int S, int n_keep) {
     constexpr int K = (N / 2 + 63) / 64;
     const bool inner = m0 >= 0 && m0 + N <= n_keep;
+    const uint32_t sh = SHIFT ? head : 0u;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t e = head + 2 * (lid + 64 * k);  // local output pair (e, e + 1)
-        const uint32_t ec = min(e, static_cast<uint32_t>(N - 2));
-        const float2 a = buf[ec], b = buf[ec + 1];
+        // clamped to the last pair of e's parity (N even), so that SHIFT keeps ec + sh even
+        const uint32_t ec = min(e, static_cast<uint32_t>(N - 2) - (SHIFT ? head : 0u));
+        float2 a, b;
+        if constexpr (SHIFT) {
+            const float4 p = *reinterpret_cast<const float4*>(buf + ec + sh);
+            a = make_float2(p.x, p.y);
+            b = make_float2(p.z, p.w);
+        } else {
+            a = buf[ec];
+            b = buf[ec + 1];
+        }
         const int m = m0 + static_cast<int>(e);
         mf_u4 v = {__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(b.x), __float_as_uint(b.y)};
         uint32_t off = static_cast<uint32_t>(m) * 8u;
@@ -595,7 +607,7 @@ __device__ __forceinline__ void txs_emit(const float2* buf, __amdgpu_buffer_rsrc
     }
     {  // odd m0: the first and last output alone (lanes 0, 1)
         const uint32_t e = lid == 0 ? 0u : static_cast<uint32_t>(N - 1);
-        const float2 a = buf[e];
+        const float2 a = buf[e + sh];
         const int m = m0 + static_cast<int>(e);
         const bool ok = head && lid < 2 && m >= 0 && m < S;
         const float2 ov = m < n_keep ? a : make_float2(0.f, 0.f);
@@ -863,9 +875,9 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
 #pragma unroll
-                for (int k = 0; k < LR; ++k) buf[LR * lid + k] = y[b][k];
+                for (int k = 0; k < LR; ++k) buf[(static_cast<uint32_t>(mfirst0) & 1u) + LR * lid + k] = y[b][k];
                 __builtin_amdgcn_wave_barrier();
-                txs_emit<640>(buf, orsrc, static_cast<uint32_t>(mfirst0) & 1u, lid, mfirst0 + static_cast<int>(1280 * r) + 640 * b,
+                txs_emit<640, true>(buf, orsrc, static_cast<uint32_t>(mfirst0) & 1u, lid, mfirst0 + static_cast<int>(1280 * r) + 640 * b,
                               static_cast<int>(A.S), static_cast<int>(A.n_keep));
                 __builtin_amdgcn_wave_barrier();
             }
