@@ -68,6 +68,29 @@ __device__ __forceinline__ void stage_span_lo(float2* dst, const float2* __restr
     });
 }
 
+// stage_span_lo for one wavefront whose whole span [q0, q0 + n] lies inside the valid range: two
+// samples per lane and load (16 B, 8-B aligned: the unaligned dwordx4 form), half the load
+// instructions of the float2 form and 16-B LDS writes; x[q0 + n] may be read, never written
+template <int U>
+__device__ __forceinline__ void stage_span_x2(float2* dst, const float2* __restrict__ x, int64_t q0, uint32_t n,
+                                              uint32_t lane) {
+    for (uint32_t base = 0; base < n; base += 128 * U) {
+        float4 v[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t i = base + 2 * lane + 128 * j;
+            v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i < n) __builtin_memcpy(&v[j], x + q0 + i, 16);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t i = base + 2 * lane + 128 * j;
+            if (i + 1 < n) *reinterpret_cast<float4*>(dst + i) = v[j];
+            else if (i < n) dst[i] = make_float2(v[j].x, v[j].y);
+        }
+    }
+}
+
 template <int U, class T>
 __device__ __forceinline__ void stage_copy(T* dst, const T* __restrict__ src, uint32_t n, uint32_t tid, uint32_t nt) {
     stage_gen<U>(dst, n, tid, nt, [&](uint32_t i) { return src[i]; });

@@ -616,7 +616,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) rx
         const rx_span_t sp = rx_span<LR, MR, HLR>(A, l);
         if (i) __builtin_amdgcn_wave_barrier();  // the previous symbol's reads of R are done
 #ifndef DNRP_FE_SKIP_LOAD
-        stage_span_lo<20>(R, src, sp.in0, sp.n_in, q_lo, q_hi, lane, 64);
+        if (sp.in0 >= q_lo && sp.in0 + sp.n_in < q_hi)  // the span and one sample past it inside the window
+            stage_span_x2<10>(R, src, sp.in0, sp.n_in, lane);
+        else
+            stage_span_lo<20>(R, src, sp.in0, sp.n_in, q_lo, q_hi, lane, 64);
 #endif
         __builtin_amdgcn_wave_barrier();
         float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
