@@ -214,7 +214,10 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
                     uint32_t k = 0xFFFFFFFFu;
                     if (nn <= N / 2) k = N / 2 + nn;
                     else if (nn >= t->dm.off_lower && nn < t->dm.off_lower + N / 2) k = nn - t->dm.off_lower;
-                    if (k != 0xFFFFFFFFu) cb[size_t(l) * 1024 + nn] = code[size_t(l) * Nf + k];
+                    // bin nn = lane + 64 m of the kernel's layout at [m / 4][lane][m % 4]: one 16-B load
+                    // per lane fetches the codes of four of its bins
+                    const uint32_t ln = nn & 63u, m = nn >> 6;
+                    if (k != 0xFFFFFFFFu) cb[size_t(l) * 1024 + ((m >> 2) * 64 + ln) * 4 + (m & 3u)] = code[size_t(l) * Nf + k];
                 }
             for (uint32_t l = 0; l <= t->q.N_DF_symb; ++l)
                 for (uint32_t k = 0; k < Nf; ++k)

@@ -59,7 +59,7 @@ struct tx_args {
     const tx_pkt* pk;
     // streaming kernel (tx_stream_kernel, N_b_DFT_os = 1024, L/M = 10/9, CP 128 / STF CP 1280):
     // one wavefront per (packet, antenna, segment of 1152-sample input pieces)
-    const uint32_t* code_bin;  // [N_DF+1][1024] cell code of every FFT bin (0: empty)
+    const uint32_t* code_bin;  // [N_DF+1][1024] cell code of every FFT bin (0: empty), bin lane + 64 m at [m / 4][lane][m % 4]
     uint32_t n_pieces, n_seg, piece_per_seg, stream;
     uint32_t pcc_syms;         // bit l: symbol l (< 32) carries PCC cells
     uint32_t onehot;           // transmit diversity with one nonzero W entry per antenna row (every packet)

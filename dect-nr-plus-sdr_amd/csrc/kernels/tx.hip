@@ -710,9 +710,15 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
     uint32_t cd[16];
     auto load_codes = [&](uint32_t rr, uint32_t ln) {
         const uint32_t ls = txs_sym(rr, A.N_DF);
-        const uint32_t* crow = A.code_bin + size_t(min(ls, A.N_DF)) * 1024;
+        const uint4* crow = reinterpret_cast<const uint4*>(A.code_bin + size_t(min(ls, A.N_DF)) * 1024);
 #pragma unroll
-        for (int m = 0; m < 16; ++m) cd[m] = crow[ln + 64 * m];
+        for (int j = 0; j < 4; ++j) {  // the codes of bins ln + 64 m, m = 4 j .. 4 j + 3, in one load
+            const uint4 c = crow[64 * j + ln];
+            cd[4 * j] = c.x;
+            cd[4 * j + 1] = c.y;
+            cd[4 * j + 2] = c.z;
+            cd[4 * j + 3] = c.w;
+        }
     };
     load_codes(r_start, lane);
     // the next piece's inputs (cell codes, PDC bytes of its symbol), issued once the FFT is done:
