@@ -109,15 +109,18 @@ __device__ __forceinline__ void unit_stage_b(const rx_cells_args& A, const cell_
     if constexpr (NT > 1) {
         // the pair's two cells are neighbours except across DC: one 16-B load per antenna (8-B
         // aligned: unaligned dwordx4, k0 + 1 <= N_b_OCC < Nf_pad stays in the row), the DC pair's
-        // second cell reloaded
+        // second cell reloaded. Nontemporal, so that it stays one dwordx4: a plain load with the DC
+        // reload behind it is sunk into an 8-B load plus two 4-B loads from a selected address (the
+        // cells are read once; nt loads bypass only the L1)
+        typedef float f4u __attribute__((ext_vector_type(4), aligned(8)));
+        const bool dc = a.k1 != a.k0 + 1;
 #pragma unroll
         for (int r = 0; r < NRX; ++r) {
-            float4 v;
-            __builtin_memcpy(&v, Yp + r * ast + yoff + a.k0, 16);
+            const f4u v = __builtin_nontemporal_load(reinterpret_cast<const f4u*>(Yp + r * ast + yoff + a.k0));
             b.r0[r] = make_float2(v.x, v.y);
             b.r1[r] = make_float2(v.z, v.w);
         }
-        if (a.k1 != a.k0 + 1) {
+        if (dc) {
 #pragma unroll
             for (int r = 0; r < NRX; ++r) b.r1[r] = Yp[r * ast + yoff + a.k1];
         }
