@@ -83,6 +83,13 @@ __device__ __forceinline__ void unit_stage_a(const rx_cells_args& A, const cell_
     a.l = A.cell_sym[a.jj];
 }
 
+// a pointer that came through LDS or a pointer table as a global one: the loads become global_load
+// instead of flat_load (a flat load also counts in lgkmcnt, so every LDS wait would wait for it)
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* as_global(const T* p) {
+    return reinterpret_cast<const __attribute__((address_space(1))) T*>(reinterpret_cast<uintptr_t>(p));
+}
+
 template <int NRX, int NT>
 __device__ __forceinline__ void unit_stage_b(const rx_cells_args& A, const cell_seg* sg, const uint32_t* pairs,
                                              const float2* __restrict__ Yp, const uint8_t* __restrict__ seq,
@@ -90,19 +97,21 @@ __device__ __forceinline__ void unit_stage_b(const rx_cells_args& A, const cell_
     const uint32_t Nf = A.N_occ + 1;
     const cell_seg& S = sg[a.si];
     const uint32_t swap = (S.info >> 1) & 3u;
+    const auto spw = as_global(S.pw);
+    const auto sq = as_global(seq);
     b.si = a.si;
     b.jj = a.jj;
     if constexpr (NT == 1) {
         b.tab = 0;
-        b.pw[0] = S.pw[swap * Nf + a.k0];
+        b.pw[0] = spw[swap * Nf + a.k0];
     } else {
         const uint32_t pr = pairs[(a.jj >> 1) % A.mod];
         const uint32_t tA = pr & 0xFu, tB = pr >> 4;
         b.tab = tA | tB << 4;
-        b.pw[0] = S.pw[((tA & 3u) ^ swap) * Nf + a.k0];
-        b.pw[1] = S.pw[((tA & 3u) ^ swap) * Nf + a.k1];
-        b.pw[2] = S.pw[((tB & 3u) ^ swap) * Nf + a.k0];
-        b.pw[3] = S.pw[((tB & 3u) ^ swap) * Nf + a.k1];
+        b.pw[0] = spw[((tA & 3u) ^ swap) * Nf + a.k0];
+        b.pw[1] = spw[((tA & 3u) ^ swap) * Nf + a.k1];
+        b.pw[2] = spw[((tB & 3u) ^ swap) * Nf + a.k0];
+        b.pw[3] = spw[((tB & 3u) ^ swap) * Nf + a.k1];
     }
     const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
     const uint32_t yoff = a.l * A.Nf_pad;
@@ -131,9 +140,9 @@ __device__ __forceinline__ void unit_stage_b(const rx_cells_args& A, const cell_
     // the unit's scrambling bits [jj N_bps, (jj + cells) N_bps) lie in at most 3 bytes
     // (loads clamped to the last byte and kept raw: nothing here waits on the loads in flight)
     const uint32_t b0 = (a.jj * A.N_bps) >> 3, bl = ((a.jj + (NT == 1 ? 1u : 2u)) * A.N_bps - 1) >> 3;
-    b.sb[0] = seq[b0];
-    b.sb[1] = seq[min(b0 + 1, bl)];
-    b.sb[2] = seq[min(b0 + 2, bl)];
+    b.sb[0] = sq[b0];
+    b.sb[1] = sq[min(b0 + 1, bl)];
+    b.sb[2] = sq[min(b0 + 2, bl)];
 }
 
 // demap + descramble + int16 of cell j (LLRs j*N_bps .. j*N_bps+N_bps-1); bits: the scrambling bytes
@@ -289,14 +298,14 @@ __device__ __forceinline__ void unit_stage_b_sm(const rx_cells_args& A, const ce
     b.si = a.si;
     b.jj = a.jj;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) b.pw[t] = S.pw[((static_cast<uint32_t>(t) & 3u) ^ swap) * Nf + a.k0];
+    for (int t = 0; t < NT; ++t) b.pw[t] = as_global(S.pw)[((static_cast<uint32_t>(t) & 3u) ^ swap) * Nf + a.k0];
     const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
     const uint32_t yoff = a.l * A.Nf_pad;
 #pragma unroll
     for (int r = 0; r < NRX; ++r) b.r0[r] = Yp[r * ast + yoff + a.k0];
     const uint32_t b0 = (a.jj * NT * A.N_bps) >> 3, bl = ((a.jj + 1) * NT * A.N_bps - 1) >> 3;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) b.sb[i] = seq[min(b0 + i, bl)];
+    for (int i = 0; i < 5; ++i) b.sb[i] = as_global(seq)[min(b0 + i, bl)];
 }
 
 // demap + descramble + int16 of one symbol: LLRs base .. base + N_bps - 1; bits: 5 scrambling bytes
