@@ -628,7 +628,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) rx
         rx_resample_ct<LR, MR, HLR>(A, in, S, sp, R, lane);
 #endif
         rx_fft_bins<true>(A, S, R, lane, [&](uint32_t k, float2 v) {
-            if (to_y) Yrow[k] = v;
+            // Y is written once and read by the next launch: nontemporal stores
+            typedef float f2v __attribute__((ext_vector_type(2)));
+            if (to_y) __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v*>(Yrow + k));
             if (drs) R[k] = v;
         }, w1, wl);
         if (drs) {

@@ -603,7 +603,8 @@ __device__ __forceinline__ void txs_emit(const float2* buf, __amdgpu_buffer_rsrc
             v = mf_u4{ka ? v.x : 0u, ka ? v.y : 0u, kb ? v.z : 0u, kb ? v.w : 0u};
             off = ok ? off : 0x80000000u;
         }
-        __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off, 0, 0);
+        // nontemporal (cache policy nt): the samples are written once and read by a later launch
+        __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off, 0, 2);
     }
     {  // odd m0: the first and last output alone (lanes 0, 1)
         const uint32_t e = lid == 0 ? 0u : static_cast<uint32_t>(N - 1);
