@@ -69,7 +69,7 @@ __device__ __forceinline__ void stage_span_lo(float2* dst, const float2* __restr
 }
 
 // stage_span_lo for one wavefront whose whole span [q0, q0 + n] lies inside the valid range: two
-// samples per lane and load (16 B, 8-B aligned: the unaligned dwordx4 form), half the load
+// samples per lane and load (16 B, 8-B aligned: the unaligned dwordx4 form, nontemporal), half the load
 // instructions of the float2 form and 16-B LDS writes; x[q0 + n] may be read, never written
 template <int U>
 __device__ __forceinline__ void stage_span_x2(float2* dst, const float2* __restrict__ x, int64_t q0, uint32_t n,
@@ -80,7 +80,12 @@ __device__ __forceinline__ void stage_span_x2(float2* dst, const float2* __restr
         for (int j = 0; j < U; ++j) {
             const uint32_t i = base + 2 * lane + 128 * j;
             v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (i < n) __builtin_memcpy(&v[j], x + q0 + i, 16);
+            // nontemporal: bypasses only the L1, the samples are not re-read by this wave
+            typedef float f4u __attribute__((ext_vector_type(4), aligned(8)));
+            if (i < n) {
+                const f4u t = __builtin_nontemporal_load(reinterpret_cast<const f4u*>(x + q0 + i));
+                v[j] = make_float4(t.x, t.y, t.z, t.w);
+            }
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {

@@ -409,7 +409,8 @@ __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, f
 #pragma unroll
         for (int j = 0; j < MR; ++j) {
             typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-            const u2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, static_cast<uint32_t>((ibn + j * 64) * 8), 0, 0);
+            // cache policy nt: the window row is streamed once by this wave
+            const u2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, static_cast<uint32_t>((ibn + j * 64) * 8), 0, 2);
             pre[j] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
         }
     }
