@@ -349,8 +349,8 @@ rx1_tables* get_rx1(dnrp_ctx* ctx, uint32_t u, uint32_t b, uint32_t N_eff_TX, in
         *err = DNRP_ENOMEM;
         return nullptr;
     }
-    // the STF front end of N_b_DFT_os = 8192 (a u = 1 packet at a u_max = 8 / b_max = 16 rate, or
-    // os_min 8) needs more than one CU's LDS: not supported
+    // a geometry is rejected only when neither the chunked STF layout (rx.hip rx_stf_lds, used from
+    // N_b_DFT_os = 8192) nor any rx_fft layout fits one CU's 160 KiB of LDS
     if (!dev::rx_front_fits(front_args(ctx, t.get(), nullptr, nullptr))) {
         *err = DNRP_EUNSUPPORTED;
         return nullptr;
@@ -416,6 +416,14 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
         static const uint32_t A_nonzero[9] = {0, 0, 2, 0, 12, 0, 0, 0, 0};  // beamforming_...mapping.hpp:110-119, N_TS = 1
         auto book = [&](uint32_t N, dbuf& W, dbuf& sc, uint32_t& ncb, uint32_t& A0) {
             if (N < 2) return true;
+            if (N != 2 && N != 4) {
+                // no single-stream codebook for 8 antennas (W_t::get_W(1, 8) is the SISO entry, and
+                // the reference's W_mat_single.at(tx) throws, estimator_mimo.cpp:160-200): no
+                // candidates, so rx_mimo_kernel reports 0xFFFFFFFF ("no recommendation")
+                ncb = 0;
+                A0 = 0;
+                return W.upload(std::vector<float2>{make_float2(0.f, 0.f)}) && sc.upload(std::vector<float>{0.f});
+            }
             ncb = geo::W_codebooks(1, N);
             A0 = A_nonzero[N];
             std::vector<float2> w;
@@ -593,11 +601,11 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
                 hipStream_t st, bool sm = false, bool cells = true) {
     const char* name = pdc ? "rx_pdc" : "rx_pcc";
     if (plan.n_dops > dev::RX_MAX_DOPS || (cells && !plan.cells_ok)) return DNRP_EUNSUPPORTED;
-    if (cells && sm) {  // the MMSE cells kernel's instantiations and its LDS staging (rx_back.hip)
+    if (cells) {  // the cells kernels' LDS staging (rx_back.hip): a geometry beyond one CU is unsupported
         const uint32_t R = ctx->cfg.N_TX_max, T = t->N_eff_TX;
-        if (!((R == 2 || R == 4 || R == 8) && (T == 2 || T == 4) && T <= R) ||
-            dev::cell_lds_bytes(R, T, t->N_occ / 4, t->wcap[0], t->wcap[1]) > 160 * 1024)
-            return DNRP_EUNSUPPORTED;
+        if (dev::cell_lds_bytes(R, T, t->N_occ / 4, t->wcap[0], t->wcap[1]) > 160 * 1024) return DNRP_EUNSUPPORTED;
+        // the MMSE cells kernel's instantiations
+        if (sm && !((R == 2 || R == 4 || R == 8) && (T == 2 || T == 4) && T <= R)) return DNRP_EUNSUPPORTED;
     }
     if (!ctx->lut_d.ensure(size_t(ctx->cfg.max_batch) * dev::RX_MAX_DOPS) ||
         !ctx->nv_d.ensure(size_t(ctx->cfg.max_batch) * dev::RX_MAX_DOPS * sizeof(float)))
@@ -838,7 +846,10 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
         // through a DECT-rate scratch (tx.hip tx_big_sym_kernel), e.g. u < u_max at b_max = 16
         const uint64_t total = uint64_t(t->dm.STF_CP) + uint64_t(t->q.N_DF_symb) * t->dm.CP + uint64_t(t->q.N_DF_symb + 1) * t->dm.Nd;
         a.big_len = static_cast<uint32_t>((total + 3) / 4 * 4);
-        if (!ctx->tx_big.ensure(sizeof(float) * 2 * a.big_len * uint64_t(n) * t->tm.N_TX)) return DNRP_ENOMEM;
+        // the scratch is capped at 4 GiB: larger batches run in passes of big_batch packets (tx.hip)
+        const uint64_t row_bytes = sizeof(float) * 2 * uint64_t(a.big_len) * t->tm.N_TX;
+        a.big_batch = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(n, (uint64_t(4) << 30) / row_bytes)));
+        if (!ctx->tx_big.ensure(row_bytes * a.big_batch)) return DNRP_ENOMEM;
         HIPCHK(ctx->tx_big.wait_idle(st));
         a.big = ctx->tx_big.as<float2>();
         a.stage_bytes = 0;
@@ -972,7 +983,8 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         const size_t zbytes = size_t(n) * ctx->zd_dops * ctx->cfg.N_TX_max * 4 * ctx->zd_row * sizeof(float2);
         if (ctx->rx_fused) {
             if (!ctx->zd.ensure(zbytes)) return DNRP_ENOMEM;
-            const auto key = std::make_tuple(ctx->zd.p, ctx->zd_dops, ctx->zd_row, ctx->cfg.N_TX_max);
+            // the size is part of the key: a reallocation can return the same base address
+            const auto key = std::make_tuple(ctx->zd.p, ctx->zd.n, ctx->zd_dops, ctx->zd_row, ctx->cfg.N_TX_max);
             if (key != ctx->zd_key) {  // a new layout: the zero op of every slot (and all else) zeroed once
                 HIPCHK(hipMemsetAsync(ctx->zd.p, 0, ctx->zd.n, st));
                 ctx->zd_key = key;

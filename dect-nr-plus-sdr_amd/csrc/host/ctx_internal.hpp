@@ -209,7 +209,7 @@ struct dnrp_ctx {
     // every slot stays zero (the fused receiver's op-less interlace slots), zd_key: layout it was zeroed for
     dbuf zd;
     uint32_t zd_dops = 0, zd_row = 0;
-    std::tuple<void*, uint32_t, uint32_t, uint32_t> zd_key{};
+    std::tuple<void*, size_t, uint32_t, uint32_t, uint32_t> zd_key{};
     // per PCC call: the DRS SNR sums (and pilots) come from the front end (DNRP_RX_SNR_FRONT, read
     // once per PCC call so that its PDC call agrees), and the PDC phase may take the fused receiver
     bool rx_snr_front = true, rx_fused = true;

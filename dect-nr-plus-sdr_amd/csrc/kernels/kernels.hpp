@@ -68,6 +68,7 @@ struct tx_args {
     // samples through a scratch [packet][antenna][big_len] (tx_big_sym_kernel, tx_big_resample_kernel)
     float2* big;
     uint32_t big_len;
+    uint32_t big_batch;  // packets per scratch pass (the scratch holds big_batch x N_TX rows)
 };
 hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st);
 bool tx_stream_taps_match(const float* h, size_t n);  // compiled-in 10/9 taps == run-time taps

@@ -9,6 +9,7 @@
 //                  (rx_synced.cpp:711-771) into the frequency-domain grid Y in HBM.
 // The back end (channel estimation, equalisation, demapping) is in rx_back.hip.
 #include "device_common.hpp"
+#include "experiments.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
 #include "rx_front.hpp"
@@ -593,11 +594,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) rx
     const int64_t q_hi = static_cast<int64_t>(A.S_in) - in.fine_peak, q_lo = in.fine_peak < 0 ? -in.fine_peak : 0;
     const float2* src = A.iq + (size_t(in.win) * A.N_RX + a) * A.S_in + in.fine_peak;
     const float2 w1_ = wfft_tw<-1>(A.tw, 4 * (lane0 & 15u)), wl_ = wfft_tw<-1>(A.tw, lane0);
-#ifdef DNRP_FE_SKIP_STORE  // phase-skip experiment builds
-    const bool to_y = false;
-#else
-    const bool to_y = !A.no_y;
-#endif
+    const bool to_y = !experiment(XS_FE_SKIP_STORE) && !A.no_y;
 #pragma unroll 1
     for (int i = 0; i < SPW; ++i) {
         const uint32_t li = blk * SPW + i;
@@ -615,18 +612,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) rx
         }
         const rx_span_t sp = rx_span<LR, MR, HLR>(A, l);
         if (i) __builtin_amdgcn_wave_barrier();  // the previous symbol's reads of R are done
-#ifndef DNRP_FE_SKIP_LOAD
-        if (sp.in0 >= q_lo && sp.in0 + sp.n_in < q_hi)  // the span and one sample past it inside the window
-            stage_span_x2<10>(R, src, sp.in0, sp.n_in, lane);
-        else
-            stage_span_lo<20>(R, src, sp.in0, sp.n_in, q_lo, q_hi, lane, 64);
-#endif
+        if constexpr (!experiment(XS_FE_SKIP_LOAD)) {
+            if (sp.in0 >= q_lo && sp.in0 + sp.n_in < q_hi)  // the span and one sample past it inside the window
+                stage_span_x2<10>(R, src, sp.in0, sp.n_in, lane);
+            else
+                stage_span_lo<20>(R, src, sp.in0, sp.n_in, q_lo, q_hi, lane, 64);
+        }
         __builtin_amdgcn_wave_barrier();
         float2* Yrow = A.Y + ((size_t(pkt) * A.N_RX + a) * A.n_sym_total + l) * A.Nf_pad;
         const bool drs = so != 0xFFFFu;
-#ifndef DNRP_FE_SKIP_FIR
-        rx_resample_ct<LR, MR, HLR>(A, in, S, sp, R, lane);
-#endif
+        if constexpr (!experiment(XS_FE_SKIP_FIR)) rx_resample_ct<LR, MR, HLR>(A, in, S, sp, R, lane);
         rx_fft_bins<true>(A, S, R, lane, [&](uint32_t k, float2 v) {
             // Y is written once and read by the next launch: nontemporal stores
             typedef float f2v __attribute__((ext_vector_type(2)));

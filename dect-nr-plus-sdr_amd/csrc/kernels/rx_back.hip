@@ -14,6 +14,7 @@
 //                   pdc_enc.cpp:339-344).
 // Y layout: [packet][N_RX][n_sym_total][Nf_pad] float2 (rx_fft_kernel).
 #include "device_common.hpp"
+#include "experiments.hpp"
 #include "kernels.hpp"
 #include "rx_eq.hpp"
 
@@ -205,14 +206,12 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
         }
         if (tid < 12) pairs[tid] = A.pair[tid];
     }
-#ifndef DNRP_CELLS_SKIP_PRO  // phase-skip experiment build: no pilot buffer
-    build_pilots<NRX, NT>(A, E, Yp, zfi, tid, CELL_THREADS);
-#endif
+    if constexpr (!experiment(XS_CELLS_SKIP_PRO)) build_pilots<NRX, NT>(A, E, Yp, zfi, tid, CELL_THREADS);
     __syncthreads();
-#ifdef DNRP_CELLS_SKIP_MAIN  // phase-skip experiment build: prologue only
-    if (tid < units) A.llr[size_t(row) * A.llr_stride + tid] = static_cast<int16_t>(zfi[tid].x);
-    return;
-#endif
+    if constexpr (experiment(XS_CELLS_SKIP_MAIN)) {
+        if (tid < units) A.llr[size_t(row) * A.llr_stride + tid] = static_cast<int16_t>(zfi[tid].x);
+        return;
+    }
     if (tid >= units) return;
     const uint8_t* __restrict__ seq = A.is_pdc ? A.pdc_seq[row] : A.pcc_seq;
     int16_t* __restrict__ llr = A.llr + size_t(row) * A.llr_stride;

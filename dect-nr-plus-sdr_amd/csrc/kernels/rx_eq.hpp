@@ -5,6 +5,7 @@
 #pragma once
 
 #include "device_common.hpp"
+#include "experiments.hpp"
 #include "kernels.hpp"
 
 namespace dnrp::dev {
@@ -197,8 +198,8 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
         const uint32_t t = c < 2 ? (b.tab & 0xFu) : (b.tab >> 4);
         uint32_t p = b.pw[c] & 0xFFFFu;
         if (!mode) p = 2 * p + ((off >> t) & 1u);  // non-interlaced: latest DRS symbol only
-        pos[c] = p + t * zst;
-        wo[c] = wbase + (b.pw[c] >> 16) * nI;
+        pos[c] = p + (experiment(XS_CELLS_ONE_ROW) ? 0u : t * zst);
+        wo[c] = wbase + (experiment(XS_CELLS_ONE_WROW) ? 0u : (b.pw[c] >> 16) * nI);
     }
     if constexpr (NT == 1) {
         float2 h[NRX];

@@ -9,6 +9,7 @@
 // hands every occupied bin, amplitude-scaled and STO-derotated, to a store functor.
 #pragma once
 
+#include "experiments.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
 #include "taps_gen.hpp"
@@ -91,12 +92,12 @@ __device__ __forceinline__ void rx_fft_bins(const rx_front_args& A, const rx_pkt
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = R[lane + 64 * m];
     __builtin_amdgcn_wave_barrier();
-#ifndef DNRP_FE_SKIP_FFT  // phase-skip experiment build: no transform
-    if constexpr (RT)
+    if constexpr (experiment(XS_FE_SKIP_FFT))
+        ;
+    else if constexpr (RT)
         wave_fft1024_rt<-1>(v, R, w1, wl, lane);
     else
         wave_fft1024<-1>(v, R, A.tw, lane);  // twiddles through the L1 (8 KB, every wave)
-#endif
     __builtin_amdgcn_wave_barrier();
     const uint32_t N = A.N_occ;
     const float2 s64 = phasor(64.0 * S.sto_inc);

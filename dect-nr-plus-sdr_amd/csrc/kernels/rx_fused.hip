@@ -15,6 +15,7 @@
 //     int16 demapping, descrambling and the LLR stores -- eq_compute's arithmetic (rx_eq.hpp) with the
 //     pilot buffer addressed in place instead of staged.
 #include "device_common.hpp"
+#include "experiments.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
 #include "rx_eq.hpp"
@@ -132,12 +133,9 @@ __global__ void __launch_bounds__(64 * NRX) __attribute__((amdgpu_waves_per_eu(N
     }
     // ---- front end: this wave's antenna into its LDS region
     float2* R = smem + a * region;
-#ifdef DNRP_FUSED_SKIP_FE  // phase-skip experiment build: no front end
-    if (true) {
+    if (experiment(XS_FUSED_SKIP_FE)) {
         for (uint32_t k = lane; k < Nf; k += 64) R[k] = make_float2(1.f, 0.f);
-    } else
-#endif
-    if ((info >> 12) & 1u) {  // bins already in Y (PCC-phase symbol, or a DRS symbol of this phase)
+    } else if ((info >> 12) & 1u) {  // bins already in Y (PCC-phase symbol, or a DRS symbol of this phase)
         const float2* Yrow = F.Y + ((size_t(pkt) * NRX + a) * F.n_sym_total + l) * F.Nf_pad;
         stage_copy<8>(R, Yrow, Nf, lane, 64);
     } else {
@@ -330,12 +328,12 @@ __global__ void __launch_bounds__(64 * NRX) __attribute__((amdgpu_waves_per_eu(N
             sfbc_emit(q, pre, g);
         }
     };
-#ifdef DNRP_FUSED_SKIP_EQ  // phase-skip experiment build: no equalisation (one LLR per unit stored)
+    if constexpr (experiment(XS_FUSED_SKIP_EQ)) {
 #pragma unroll
-    for (int g = 0; g < UPT; ++g)
-        if (tid + g * NTH < units) llr[(j0 + per_unit * (tid + g * NTH)) * N_bps] = static_cast<int16_t>(P[g].bits + smem[tid].x);
-    return;
-#endif
+        for (int g = 0; g < UPT; ++g)
+            if (tid + g * NTH < units) llr[(j0 + per_unit * (tid + g * NTH)) * N_bps] = static_cast<int16_t>(P[g].bits + smem[tid].x);
+        return;
+    }
 #pragma unroll
     for (int g = 0; g < UPT; ++g)
         if (tid + g * NTH < units) {

@@ -24,6 +24,7 @@
 #include <type_traits>
 
 #include "device_common.hpp"
+#include "experiments.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
 #include "taps_gen.hpp"
@@ -504,11 +505,8 @@ __global__ void __launch_bounds__(64) sync_steps_pipe_kernel(sync_args A, uint32
     const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
     const size_t orow = (static_cast<size_t>(w) * A.n_ant + a) * A.n_steps;
     const int64_t ib0 = static_cast<int64_t>(A.p_star) + MR * qa - HLR;
-#ifdef DNRP_SYNC_NOCLAMP  // A/B build: the whole window row in range
-    const int64_t in_end = A.S_win;
-#else
-    const int64_t in_end = min<int64_t>(A.S_win, max<int64_t>(0, ib0 + int64_t(NEW) * nch + CARRY));
-#endif
+    const int64_t in_end = experiment(XS_SYNC_NOCLAMP) ? int64_t(A.S_win)
+                                                       : min<int64_t>(A.S_win, max<int64_t>(0, ib0 + int64_t(NEW) * nch + CARRY));
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(x), 0, static_cast<int>(in_end * 8), 0x00020000);
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(A.P + orow, 0, static_cast<int>(A.n_steps * 4u), 0x00020000);
     const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(A.Cs + orow, 0, static_cast<int>(A.n_steps * 8u), 0x00020000);

@@ -16,6 +16,7 @@
 // and mixer_t::mix_phase_continuous (mixer.cpp:41-65). Only the packed d-bits are read and only
 // the final hw-rate IQ is written: HBM traffic = ceil(G/8) + 25 bytes in, N_TX * S * 8 bytes out.
 #include "device_common.hpp"
+#include "experiments.hpp"
 #include "kernels.hpp"
 #include "polyphase.hpp"
 #include "taps_gen.hpp"
@@ -491,7 +492,11 @@ struct txs_wave {
     // SBW: bytes of the staging window (1 KiB; spatial multiplexing TXS_SM up to 4 KiB)
     template <bool Q8, uint32_t SBW = 1024>
     __device__ float2 pdc_sym(const uint8_t* sb, uint32_t ab, uint32_t s) const {
-        if (Q8) return qtab[sb[(s - ab) & (SBW - 1)]];
+        if (Q8) {
+            const uint32_t v = sb[(s - ab) & (SBW - 1)];
+            if constexpr (experiment(XS_TX_NO_QTAB)) return make_float2(static_cast<float>(v), -static_cast<float>(v));
+            return qtab[v];
+        }
         // byte bo of the window and its successor (the host keeps both inside it; the masks only bound
         // the LDS index)
         const uint32_t lb = s * A->N_bps - 8 * ab, bo = (lb >> 3) & (SBW - 1);
@@ -1005,8 +1010,10 @@ __global__ void __launch_bounds__(TX_BIG_THREADS) tx_big_sym_kernel(tx_args A) {
     });
 }
 
+// grid: (packet, antenna) x output blocks folded into x (gridDim.y is capped at 65536 rows)
 __global__ void __launch_bounds__(256) tx_big_resample_kernel(tx_args A, uint32_t total) {
-    const uint32_t pa = blockIdx.y, m = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t nb = (A.S + 255) / 256;
+    const uint32_t pa = blockIdx.x / nb, m = (blockIdx.x % nb) * 256 + threadIdx.x;
     if (m >= A.S) return;
     float2* out = reinterpret_cast<float2*>(A.out) + size_t(pa) * A.S;
     // outputs m with delay + m M < (total + hl) L: the packet and its flush samples
@@ -1072,9 +1079,21 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
         const uint32_t total = a.STF_CP + a.N_DF * a.CP + (a.N_DF + 1) * a.plan.N;
         if (total > a.big_len) return hipErrorInvalidValue;
         const size_t lds = (2 * size_t(a.plan.N) + 256 + 98 + 8) * sizeof(float2);
-        if (lds > 160 * 1024) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(tx_big_sym_kernel, dim3(n * a.N_TX * (a.N_DF + 1)), dim3(TX_BIG_THREADS), lds, st, a);
-        hipLaunchKernelGGL(tx_big_resample_kernel, dim3((a.S + 255) / 256, n * a.N_TX), dim3(256), 0, st, a, total);
+        if (lds > 160 * 1024 || a.big_batch == 0) return hipErrorInvalidValue;
+        // passes of big_batch packets through the scratch (the host caps its size), each pass with
+        // the packet-indexed arguments offset to its first packet
+        for (uint32_t p0 = 0; p0 < n; p0 += a.big_batch) {
+            const uint32_t np = min(a.big_batch, n - p0);
+            tx_args b = a;
+            b.pk = a.pk + p0;
+            b.pcc_d = a.pcc_d + size_t(p0) * 25;
+            b.pdc_d = a.pdc_d + size_t(p0) * a.pdc_stride;
+            b.out = a.out + size_t(p0) * a.N_TX * a.S * 2;
+            const uint64_t gx = uint64_t((a.S + 255) / 256) * np * a.N_TX;
+            if (gx > 0x7FFFFFFFull) return hipErrorInvalidValue;
+            hipLaunchKernelGGL(tx_big_sym_kernel, dim3(np * a.N_TX * (a.N_DF + 1)), dim3(TX_BIG_THREADS), lds, st, b);
+            hipLaunchKernelGGL(tx_big_resample_kernel, dim3(static_cast<uint32_t>(gx)), dim3(256), 0, st, b, total);
+        }
         return hipGetLastError();
     }
     const bool wave = a.plan.N == 1024;

@@ -137,7 +137,7 @@ def rx(cf, ps, iq, fine_peak=0, cfo_rad=0.0, network_id=100, plcf_type=1, use_fl
     assert r == 0, r
     return dict(pcc_llr=pcc, pdc_llr=pdc, pcc_llr_f=pccf, pdc_llr_f=pdcf, rms=meta[:8].copy(),
                 cfo_fine=float(meta[8]), sto=float(meta[9]), snr_pcc=float(meta[10]), snr_pdc=float(meta[11]),
-                mimo_N_TS_other=int(meta[12]), mimo_idx=int(meta[13]), mimo_idx_reciprocal=int(meta[14]))
+                mimo_N_TS_other=int(meta[12]), mimo_idx=int(meta[13]) & 0xFFFFFFFF, mimo_idx_reciprocal=int(meta[14]) & 0xFFFFFFFF)
 
 
 def loopback_timed(cf, ps, n_packets, n_threads, seed=0xDEC7, sync_pre=0, sync_chunk=0, phases=False):

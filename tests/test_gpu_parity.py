@@ -174,6 +174,11 @@ def _check_rx(name, g_pcc, g_pdc, r1, r2, r):
 
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_rx_parity(name, stride=2):
+    _rx_parity(name, stride)
+
+
+def _rx_parity(name, stride=2):
+    """Runs one RX parity case; returns the context (its kernel timers, with DNRP_TIMING=1)."""
     import dnrp
     rng = np.random.default_rng(11)
     phy, ps, ops, ocf = _ctx(name, stride=stride)
@@ -204,6 +209,7 @@ def test_rx_parity(name, stride=2):
         if snrs[i] >= 20.0:  # uncoded hard decisions well above the demapping noise floor
             bits = np.unpackbits(pdc[i])[: sz["G"]]
             assert np.mean(bits != (g_pdc[i] > 0)) < 2e-2, (name, i)
+    return phy
 
 
 @pytest.mark.parametrize("name,stride", [("tm5_u2b4", 1), ("tm5_u2b4", 3), ("C4", 1), ("C4", 3), ("mrc2_64qam", 3),
@@ -221,14 +227,64 @@ def test_rx_parity_fused(name, monkeypatch):
     leaves zero-forced pilots, then one workgroup per (packet, symbol) transforms every antenna into LDS
     and equalises from there, no Y round trip) instead of Y + rx_cells -- same oracle and gates.
     Geometries outside the fused kernel (N_b_DFT_os != 1024) run the Y path either way."""
+    _rx_parity_fused(name, 2, monkeypatch)
+
+
+def _rx_parity_fused(name, stride, monkeypatch):
     monkeypatch.setenv("DNRP_RX_FUSED", "1")
-    test_rx_parity(name)
+    monkeypatch.setenv("DNRP_TIMING", "1")  # launch counts: the fused kernel ran exactly where it applies
+    phy = _rx_parity(name, stride)
+    ps = TX_CASES[name][0]
+    import dnrp
+    n_fused = phy.kernel_time_total("rx_fused")[1]
+    if phy.packet_sizes(dnrp.psdef(*ps))["N_b_DFT_os"] == 1024:
+        assert n_fused > 0, name
+    else:
+        assert n_fused == 0, name
 
 
 @pytest.mark.parametrize("name,stride", [("C4", 1), ("tm5_u2b4", 3)])
 def test_rx_parity_fused_stride(name, stride, monkeypatch):
+    _rx_parity_fused(name, stride, monkeypatch)
+
+
+def test_rx_largest_cells_geometry(monkeypatch):
+    """8 RX antennas x 4 transmit streams at b = 16 (TM5 into an N_TX_max = 8 context): the largest
+    N_RX / NT / b of the cells kernel's LDS staging (pilot rows of 8 x 4 streams, both weight tables).
+    Parity against the oracle where it fits one CU's LDS, else DNRP_EUNSUPPORTED before any launch
+    (never a device error)."""
+    import dnrp
+    name = "tm5_u8b16_rx8"
+    spec = ((8, 16, 1, 1, 5, 8), (8, 16, 8, 1, 10, 9), 1, (30.0,), 0)
+    monkeypatch.setitem(CASES, name, spec)
+    monkeypatch.setitem(TX_CASES, name, spec)
+    try:
+        _rx_parity(name)
+    except dnrp.DnrpError as e:
+        assert e.code == -3, str(e)  # DNRP_EUNSUPPORTED
+
+
+def test_rx_fused_growing_batch(monkeypatch):
+    """DNRP_RX_FUSED=1 with a small PCC/PDC batch and then a larger one in the same context: the pilot
+    buffer zd is reallocated (possibly at the same address) and its op-less interlace slot must be
+    zeroed again (ctx.cpp zd_key includes the size) -- both batches at parity."""
+    import dnrp
     monkeypatch.setenv("DNRP_RX_FUSED", "1")
-    test_rx_parity(name, stride)
+    rng = np.random.default_rng(23)
+    phy, ps, ops, ocf = _ctx("C4", max_batch=8)
+    sz = phy.packet_sizes(ps)
+    S, n_rx, dev = sz["N_samples_packet_os_rs"], phy.cfg.N_TX_max, torch.device("cuda:0")
+    for n in (2, 8):
+        windows, reports, nids, types, _, _ = _rx_windows(rng, "C4", phy, ps, ops, ocf, (30.0,) * n)
+        iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(n, n_rx, S, 2)).to(dev)
+        pcc_llr = torch.zeros((n, 196), dtype=torch.int16, device=dev)
+        pdc_llr = torch.zeros((n, sz["G"]), dtype=torch.int16, device=dev)
+        phy.rx_pcc_batch(reports, iq, pcc_llr)
+        phy.rx_pdc_batch([dnrp.PdcReq(ps, i, nids[i], types[i]) for i in range(n)], iq, pdc_llr)
+        phy.sync()
+        for i in (0, n - 1):
+            r = _oracle_rx(ocf, ops, windows[i], reports[i], nids[i], types[i])
+            _check_rx(("grow", n, i), pcc_llr[i].cpu().numpy(), pdc_llr[i].cpu().numpy(), None, None, r)
 
 
 @pytest.mark.parametrize("name", ["C4", "C3", "C2"])
@@ -436,10 +492,11 @@ def test_rx_negative_fine_peak():
     _check_rx("neg_peak", pcc_llr[1].cpu().numpy(), pdc_llr[0].cpu().numpy(), None, None, r)
 
 
-@pytest.mark.parametrize("name,n", [("C4", 4096), ("C3", 8192)])
+@pytest.mark.parametrize("name,n", [("C4", 4096), ("C3", 8192), ("C4", 16384)])
 def test_full_chunk_edges(name, n):
-    """A full bench chunk (C4: 4096 packets, C3: 8192, max_batch = chunk): TX and RX of the first,
-    middle and last packet compared with the oracle, chunk-boundary indexing included."""
+    """A full bench chunk (C4: 4096 packets, C3: 8192, and the bench's C4 chunk of 16384 packets, whose
+    window and Y offsets pass 2^32 float2 elements; max_batch = chunk): TX and RX of the first, middle
+    and last packet compared with the oracle (rx_synced.cpp:325-436), chunk-boundary indexing included."""
     import dnrp
     import math
     phy, ps, ops, ocf = _ctx(name, max_batch=n)
