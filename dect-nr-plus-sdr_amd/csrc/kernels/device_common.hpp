@@ -430,7 +430,14 @@ __device__ void fft_store(float2* x_, float2* y_, const float2* tw, const fft_pl
 // barrier. tw: forward twiddles exp(-2 pi i j / 1024) (LDS or global).
 constexpr uint32_t WFFT_XB = 1024 + 64;
 
-__device__ __forceinline__ uint32_t wfft_pad(uint32_t i) { return i + (i >> 4); }
+// exchange slot of element i: padded i + i / 16 (default: conflict-free b64 writes of pass 1 and 2,
+// 2-way ds_read_b64 conflicts in passes 2 and 3 -- slots 0 and 32 of a half-wave share a bank) or, with
+// DNRP_WFFT_SWZ, i ^ ((i >> 4) & 15): conflict-free for all four exchange patterns, but the XOR makes
+// the slot lane-dependent per instruction (address VALU instead of immediate offsets)
+#ifndef DNRP_WFFT_SWZ
+#define DNRP_WFFT_SWZ 0
+#endif
+__device__ __forceinline__ uint32_t wfft_pad(uint32_t i) { return DNRP_WFFT_SWZ ? (i ^ ((i >> 4) & 15u)) : i + (i >> 4); }
 
 template <int SIGN>
 __device__ __forceinline__ float2 wfft_tw(const float2* tw, uint32_t e) {

@@ -161,7 +161,7 @@ hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st) {
 // ===================================================================== cells
 constexpr uint32_t CELL_THREADS = 512;
 
-template <int NRX, int NT, bool SM = false>
+template <int NRX, int NT, bool SM = false, int NBPS = 0>
 __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     const uint32_t zst = zfi_stride(A.n_drs);
@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
         const bool m1 = u + CELL_THREADS < units, m2 = u + 2 * CELL_THREADS < units;
         if (m1) unit_stage_b<NRX, NT>(A, sg, pairs, Yp, seq, na, nb);
         if (m2) unit_stage_a(A, sg, nseg, si, u + 2 * CELL_THREADS, per_unit, na);
-        eq_compute<NRX, NT>(A, sg, zfi, wtab, zst, cur, llr);
+        eq_compute<NRX, NT, NBPS>(A, sg, zfi, wtab, zst, cur, llr);
         if (m1) cur = nb;
     }
 }
@@ -257,9 +257,13 @@ hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st) {
     const size_t lds = cell_lds_bytes(a.N_RX, a.NT, a.n_drs, a.wcap[0], a.wcap[1]);
     if (lds > 160 * 1024 || a.n_pkt != n) return hipErrorInvalidValue;
     const dim3 g((n + 7) / 8 * 8 * a.n_epochs), b(CELL_THREADS);
+    // 256-QAM (N_bps = 8, the bench's C3 / C4) with the demapper width compiled in
 #define DNRP_CELLS(R, T)                                                                 \
     if (a.N_RX == R && a.NT == T) {                                                      \
-        hipLaunchKernelGGL((rx_cells_kernel<R, T>), g, b, lds, st, a);                   \
+        if (a.N_bps == 8)                                                                \
+            hipLaunchKernelGGL((rx_cells_kernel<R, T, false, 8>), g, b, lds, st, a);     \
+        else                                                                             \
+            hipLaunchKernelGGL((rx_cells_kernel<R, T>), g, b, lds, st, a);               \
         return hipGetLastError();                                                        \
     }
     DNRP_CELLS(1, 1)

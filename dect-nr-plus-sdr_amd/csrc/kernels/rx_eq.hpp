@@ -10,6 +10,10 @@
 
 namespace dnrp::dev {
 
+#ifndef DNRP_CELLS_CH
+#define DNRP_CELLS_CH 3  // SFBC interpolation taps per chunk (eq_compute): 3 keeps rx_cells<4, 4> at 121 VGPRs (4: 131, one workgroup per CU)
+#endif
+
 __device__ __forceinline__ int16_t q16(float v) {
     const float r = rintf(v);
     return static_cast<int16_t>(fminf(32767.f, fmaxf(-32768.f, r)));
@@ -182,12 +186,14 @@ __device__ __forceinline__ void emit_cell(float2 x, uint32_t j, uint32_t j0, uin
 // Wiener interpolation (rx_synced.cpp:893-949), MRC (1204-1306) or SFBC combining (1335-1392),
 // demapping and the LLR store of one unit. zfi: the epoch's pilot rows [NRX][NT][zst]; wtab: the
 // weight-table slots.
-template <int NRX, int NT>
+// NBPS: bits per cell fixed at compile time (8: 256-QAM, the bench's C3 / C4), 0: A.N_bps at run time
+template <int NRX, int NT, int NBPS = 0>
 __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_seg* sg, const float2* zfi,
                                            const float* wtab, uint32_t zst, const unit_b<NRX, NT>& b,
                                            int16_t* __restrict__ llr) {
     constexpr int NC = unit_b<NRX, NT>::NC;
-    const uint32_t b0 = (b.jj * A.N_bps) >> 3, bl = ((b.jj + (NT == 1 ? 1u : 2u)) * A.N_bps - 1) >> 3;
+    const uint32_t N_bps = NBPS ? static_cast<uint32_t>(NBPS) : A.N_bps;
+    const uint32_t b0 = (b.jj * N_bps) >> 3, bl = ((b.jj + (NT == 1 ? 1u : 2u)) * N_bps - 1) >> 3;
     const uint32_t bits = b.sb[0] | (b0 + 1 <= bl ? b.sb[1] << 8 : 0u) | (b0 + 2 <= bl ? b.sb[2] << 16 : 0u);
     const uint32_t info = sg[b.si].info, wbase = sg[b.si].wbase;
     const uint32_t mode = info & 1u, off = (info >> 4) & 0xFFu, nI = info >> 12;
@@ -205,15 +211,27 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
         float2 h[NRX];
 #pragma unroll
         for (int a = 0; a < NRX; ++a) h[a] = make_float2(0.f, 0.f);
-        for (uint32_t i = 0; i < nI; ++i) {
-            const float wv = wtab[wo[0] + i];
-            const uint32_t p = pos[0] + i * step;
+        // taps in chunks of CH, the chunk's reads issued before its FMAs; taps past nI read the last
+        // one with weight 0 (exact zeros: the tap-ordered sums of the one-tap loop, bit for bit)
+        constexpr uint32_t CH = 4;
+        for (uint32_t i0 = 0; i0 < nI; i0 += CH) {
+            float wv[CH];
+            float2 z[CH][NRX];
 #pragma unroll
-            for (int a = 0; a < NRX; ++a) {
-                const float2 z = zfi[a * NT * zst + p];
-                h[a].x = fmaf(z.x, wv, h[a].x);
-                h[a].y = fmaf(z.y, wv, h[a].y);
+            for (uint32_t j = 0; j < CH; ++j) {
+                const uint32_t i = min(i0 + j, nI - 1);
+                const float w = wtab[wo[0] + i];
+                wv[j] = i0 + j < nI ? w : 0.f;
+#pragma unroll
+                for (int a = 0; a < NRX; ++a) z[j][a] = zfi[a * NT * zst + pos[0] + i * step];
             }
+#pragma unroll
+            for (uint32_t j = 0; j < CH; ++j)
+#pragma unroll
+                for (int a = 0; a < NRX; ++a) {
+                    h[a].x = fmaf(z[j][a].x, wv[j], h[a].x);
+                    h[a].y = fmaf(z[j][a].y, wv[j], h[a].y);
+                }
         }
         float2 num = make_float2(0.f, 0.f);
         float den = 0.f;
@@ -222,7 +240,7 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
             num = cadd(num, cmulc(b.r0[a], h[a]));
             den += cnorm(h[a]);
         }
-        emit_cell(cscale(num, 1.0f / den), b.jj, b.jj, A.N_bps, bits, llr);
+        emit_cell(cscale(num, 1.0f / den), b.jj, b.jj, N_bps, bits, llr);
     } else {
         // SFBC: a stream's pair channel is the mean of its interpolations at k0 and k1
         // (rx_synced.cpp:1365-1371). Both read the stream's pilot row with windows sh pilots apart
@@ -241,20 +259,34 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
         float2 g[NRX][2];
 #pragma unroll
         for (int a = 0; a < NRX; ++a) g[a][0] = g[a][1] = make_float2(0.f, 0.f);
-        for (uint32_t i = 0; i < ntap; ++i) {
+        // taps in chunks of CH, per stream every LDS read of a chunk (weights at clamped indices,
+        // pilots) issued before its FMAs: one LDS latency per chunk and stream instead of per tap,
+        // no exec-mask branches. Taps past a stream's union window carry weight 0 (their read stays
+        // in the row + ZFI_PAD) and add exact zeros, so the per-(antenna, stream) sums are the
+        // tap-ordered sums of the one-tap loop, bit for bit.
+        constexpr uint32_t CH = DNRP_CELLS_CH;
+        for (uint32_t i0 = 0; i0 < ntap; i0 += CH) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const float lo = i < nI ? wtab[wl[s] + i] : 0.f;
-                const float hi = i >= sh[s] && i - sh[s] < nI ? wtab[wh[s] + i - sh[s]] : 0.f;
-                const float wv = 0.5f * (lo + hi);
-                // past this stream's union window: weight 0, the read stays in the row + ZFI_PAD
-                const uint32_t p = base[s] + min(i, nI + sh[s]) * step;
+                __builtin_amdgcn_sched_barrier(0);  // one stream's chunk live at a time
+                float wv[CH];
+                float2 z[CH][NRX];
 #pragma unroll
-                for (int a = 0; a < NRX; ++a) {
-                    const float2 z = zfi[a * NT * zst + p];
-                    g[a][s].x = fmaf(z.x, wv, g[a][s].x);
-                    g[a][s].y = fmaf(z.y, wv, g[a][s].y);
+                for (uint32_t j = 0; j < CH; ++j) {
+                    const uint32_t i = i0 + j, ih = i - sh[s];  // ih wraps for i < sh
+                    const float lo = wtab[wl[s] + min(i, nI - 1)], hi = wtab[wh[s] + min(ih, nI - 1)];
+                    wv[j] = 0.5f * ((i < nI ? lo : 0.f) + (ih < nI ? hi : 0.f));
+                    const uint32_t p = base[s] + min(i, nI + sh[s]) * step;
+#pragma unroll
+                    for (int a = 0; a < NRX; ++a) z[j][a] = zfi[a * NT * zst + p];
                 }
+#pragma unroll
+                for (uint32_t j = 0; j < CH; ++j)
+#pragma unroll
+                    for (int a = 0; a < NRX; ++a) {
+                        g[a][s].x = fmaf(z[j][a].x, wv[j], g[a][s].x);
+                        g[a][s].y = fmaf(z[j][a].y, wv[j], g[a][s].y);
+                    }
             }
         }
         float2 n0 = make_float2(0.f, 0.f), n1 = make_float2(0.f, 0.f);
@@ -266,8 +298,8 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
             n1 = cadd(n1, cadd(cmul(make_float2(-h1.x, -h1.y), cconj(b.r0[a])), cmul(cconj(h0), b.r1[a])));
             den += cnorm(h0) + cnorm(h1);
         }
-        emit_cell(cscale(n0, 1.0f / den), b.jj, b.jj, A.N_bps, bits, llr);
-        emit_cell(cscale(n1, 1.0f / den), b.jj + 1, b.jj, A.N_bps, bits, llr);
+        emit_cell(cscale(n0, 1.0f / den), b.jj, b.jj, N_bps, bits, llr);
+        emit_cell(cscale(n1, 1.0f / den), b.jj + 1, b.jj, N_bps, bits, llr);
     }
 }
 

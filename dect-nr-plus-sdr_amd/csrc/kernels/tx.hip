@@ -40,6 +40,14 @@ constexpr bool cover_is_sign() {
 static_assert(cover_is_sign(), "cover sequence entries are +-1");
 __device__ __forceinline__ float cover_sign(uint32_t q) { return ((cover_neg_mask() >> q) & 1u) ? -1.f : 1.f; }
 
+// streaming TX, 256-QAM: constellation from the separable 16-level table (two conflict-free reads
+// and the index bit gathers) instead of the 256-entry table (one read, ~3 conflict cycles). A/B on
+// MI355X: TX 19.25-19.48 vs 18.83-18.98 ms per 16384-slot chunk -- the gathers' VALU (+5 % per
+// wave) cost more than the conflicts; off by default
+#ifndef DNRP_TX_QLEV
+#define DNRP_TX_QLEV 0
+#endif
+
 constexpr uint32_t TX_THREADS = 256;     // block-FFT path workgroup
 constexpr uint32_t TX_WAVE_MAX = 512;    // wave path: one wavefront per symbol slot, 64 (K + 1) threads
 constexpr uint32_t TX_MAX_SLOTS = 8;     // K + 1 (wave path)
@@ -450,6 +458,7 @@ struct txs_wave {
     tx_pkt P;
     uint32_t pkt, ant, lane;
     float2 *buf, *wrow, *qtab;
+    float* qlev;  // 256-QAM: level of the 4-bit index ((v >> 1) & 5) | ((v >> 4) & 10), the I part of qtab
     float2 w0;  // unscaled W[ant][0]: the STF bins carry scale_stf alone (tx.cpp:864-871)
     float2 wsel;  // TXS_TXDIV1: the antenna's one nonzero W entry, scale_df applied
     uint32_t tsel;  // TXS_TXDIV1: its stream
@@ -495,6 +504,13 @@ struct txs_wave {
         if (Q8) {
             const uint32_t v = sb[(s - ab) & (SBW - 1)];
             if constexpr (experiment(XS_TX_NO_QTAB)) return make_float2(static_cast<float>(v), -static_cast<float>(v));
+            if constexpr (DNRP_TX_QLEV) {
+                // 256-QAM is separable (36.211 7.1.5: I from bits 0, 2, 4, 6, Q from bits 1, 3, 5, 7, the
+                // same level function): two reads of the 16-level table, conflict-free (16 words on 16
+                // banks), instead of one 8-B read of the 256-entry table at a data-random index
+                const uint32_t iI = ((v >> 1) & 5u) | ((v >> 4) & 10u), iQ = (v & 5u) | ((v >> 3) & 10u);
+                return make_float2(qlev[iI], qlev[iQ]);
+            }
             return qtab[v];
         }
         // byte bo of the window and its successor (the host keeps both inside it; the masks only bound
@@ -630,11 +646,18 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
     static_assert(PD::W == TXS_CARRY + 1, "carry = window - 1");
     static_assert(taps_tx_10_9::L == LR && taps_tx_10_9::M == MR && taps_tx_10_9::HL == HLR, "generated taps");
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
-    float2* qtab = smem;  // [256] per workgroup
+    float2* qtab = smem;  // [256] per workgroup (256-QAM: the 16 levels in its first 8 slots)
     // wave index made provably uniform: everything derived from it (packet, segment, loop bounds,
     // pointers) stays in SGPRs and the piece loop is not divergent control flow
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    {
+    if constexpr (Q8 && DNRP_TX_QLEV) {
+        // level i = re of the table entry whose I bits (0, 2, 4, 6) give index i and Q bits are 0
+        if (threadIdx.x < 16) {
+            const uint32_t i = threadIdx.x;
+            const uint32_t v = ((i & 8u) << 4) | ((i & 2u) << 4) | ((i & 4u) << 1) | ((i & 1u) << 1);
+            reinterpret_cast<float*>(qtab)[i] = A.qam[v].x;
+        }
+    } else {
         const uint32_t nq = 1u << A.N_bps;
         for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) qtab[i] = A.qam[i];
     }
@@ -642,6 +665,7 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
     T.A = &A;
     T.lane = lane;
     T.qtab = qtab;
+    T.qlev = reinterpret_cast<float*>(qtab);
     T.buf = smem + 256 + wv * (TXS_BUF + TXS_WROW);
     T.wrow = T.buf + TXS_BUF;
     const uint32_t gw = blockIdx.x * TXS_WPG + wv;
@@ -884,10 +908,23 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
             __builtin_amdgcn_wave_barrier();
             if (lid < TXS_CARRY) creg = buf[TXS_PIECE + lid];
             __builtin_amdgcn_wave_barrier();
+            const uint32_t head = static_cast<uint32_t>(mfirst0) & 1u;  // packet-uniform
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
+                // the block's outputs as 16-B pairs at even slots (a lane's 10 outputs: 8 dwords x 10
+                // apart, conflict-free in every 8-lane group; 8-B stores at a 10-slot stride are 2-way)
+                static_assert(LR % 2 == 0, "pairs of outputs");
+                float2* dst = buf + head + LR * lid;
+                auto st4 = [&](int k) { *reinterpret_cast<float4*>(dst + k) = make_float4(y[b][k].x, y[b][k].y, y[b][k + 1].x, y[b][k + 1].y); };
+                if (head == 0) {
 #pragma unroll
-                for (int k = 0; k < LR; ++k) buf[(static_cast<uint32_t>(mfirst0) & 1u) + LR * lid + k] = y[b][k];
+                    for (int k = 0; k < LR; k += 2) st4(k);
+                } else {
+                    dst[0] = y[b][0];
+#pragma unroll
+                    for (int k = 1; k + 1 < LR; k += 2) st4(k);
+                    dst[LR - 1] = y[b][LR - 1];
+                }
                 __builtin_amdgcn_wave_barrier();
                 txs_emit<640, true>(buf, orsrc, static_cast<uint32_t>(mfirst0) & 1u, lid, mfirst0 + static_cast<int>(1280 * r) + 640 * b,
                               static_cast<int>(A.S), static_cast<int>(A.n_keep));

@@ -123,8 +123,11 @@ def found_reports(res, n_found):
     """All packets a sync batch found: res [n_win, max_reports] + n_found [n_win] -> the
     dnrp_sync_report array of the found packets in window order (window = its sync window)."""
     n_found = np.asarray(n_found).astype(np.int64)
+    if len(n_found) and (n_found == 1).all():  # one packet per window: a view, no record gather
+        return sync_reports(res[:, 0], np.arange(len(n_found)))
     win = np.repeat(np.arange(len(n_found)), n_found)
-    k = np.concatenate([np.arange(c) for c in n_found]) if len(n_found) else np.zeros(0, np.int64)
+    # report index within its window: position minus the window's first position (vectorised)
+    k = np.arange(len(win), dtype=np.int64) - np.repeat(np.cumsum(n_found) - n_found, n_found)
     return sync_reports(res[win, k], win)
 
 
@@ -453,7 +456,17 @@ class Phy:
         self._check_rx_windows(iq_in)
         _check_tensor(pdc_llr, "pdc_llr", torch.int16, 2, int(self.cfg.device))
         arr = reqs if isinstance(reqs, C.Array) else (PdcReq * m)(*reqs)
-        keys = {tuple(getattr(r.psdef, f) for f, _ in PsDef._fields_) for r in arr}
+        # distinct psdefs of the requests, vectorised over the array's memory (a Python loop over
+        # 16384 ctypes records takes ~50 ms per call)
+        nw = C.sizeof(PsDef) // 4  # PsDef: uint32 fields only
+        w = np.frombuffer(arr, dtype=np.uint32, count=m * C.sizeof(PdcReq) // 4).reshape(m, -1)[:, :nw] if m else None
+        if w is None:
+            keys = set()
+        elif (w == w[0]).all():
+            keys = {tuple(int(x) for x in w[0])}
+        else:
+            rows = np.unique(np.ascontiguousarray(w).view(np.dtype((np.void, 4 * nw))).ravel())
+            keys = {tuple(int(x) for x in np.frombuffer(r.tobytes(), np.uint32)) for r in rows}
         g_max = max((self.packet_sizes(PsDef(*k))["G"] for k in keys), default=0)
         if pdc_llr.shape[0] < m or pdc_llr.shape[1] < g_max:
             raise ValueError(f"pdc_llr shape {tuple(pdc_llr.shape)}, expected [>={m}, >={g_max}]")
