@@ -206,15 +206,44 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
         }
         if (tid < 12) pairs[tid] = A.pair[tid];
     }
-    if constexpr (!experiment(XS_CELLS_SKIP_PRO)) build_pilots<NRX, NT>(A, E, Yp, zfi, tid, CELL_THREADS);
+    if constexpr (!experiment(XS_CELLS_SKIP_PRO)) build_pilots<NRX, NT, SM>(A, E, Yp, zfi, tid, CELL_THREADS);
     __syncthreads();
     if constexpr (experiment(XS_CELLS_SKIP_MAIN)) {
         if (tid < units) A.llr[size_t(row) * A.llr_stride + tid] = static_cast<int16_t>(zfi[tid].x);
         return;
     }
-    if (tid >= units) return;
+    constexpr bool wave_mf = SM && DNRP_MMSE_MFMA && NT == 4;
+    if (!wave_mf && tid >= units) return;
     const uint8_t* __restrict__ seq = A.is_pdc ? A.pdc_seq[row] : A.pcc_seq;
     int16_t* __restrict__ llr = A.llr + size_t(row) * A.llr_stride;
+    if constexpr (wave_mf) {
+        // experiment: MFMA Gram (rx_eq.hpp gram_mfma) needs every lane of the wave, so the wave runs
+        // a uniform trip count over clamped units and stores only its real ones
+        const float nv = dc ? A.nv_d[size_t(pkt) * RX_MAX_DOPS + dc - 1] : 0.f;
+        const uint32_t wf = tid & ~63u;
+        if (wf >= units) return;
+        const uint32_t nit = (units - wf + CELL_THREADS - 1) / CELL_THREADS;
+        float2* scr = reinterpret_cast<float2*>(reinterpret_cast<char*>(smem) +
+                                                (cell_lds_bytes(NRX, NT, A.n_drs, A.wcap[0], A.wcap[1]) + 15) / 16 * 16) +
+                      (tid >> 6) * NRX * 4 * 24;
+        auto cl = [&](uint32_t x) { return min(x, units - 1); };
+        uint32_t si = 0;
+        unit_a na;
+        unit_sm<NRX, NT> cur;
+        uint32_t u = tid;
+        unit_stage_a(A, sg, nseg, si, cl(u), 1u, na);
+        unit_stage_b_sm<NRX, NT>(A, sg, Yp, seq, na, cur);
+        if (nit > 1) unit_stage_a(A, sg, nseg, si, cl(u + CELL_THREADS), 1u, na);
+        for (uint32_t it = 0; it < nit; ++it, u += CELL_THREADS) {
+            unit_sm<NRX, NT> nb;
+            const bool m1 = it + 1 < nit, m2 = it + 2 < nit;
+            if (m1) unit_stage_b_sm<NRX, NT>(A, sg, Yp, seq, na, nb);
+            if (m2) unit_stage_a(A, sg, nseg, si, cl(u + 2 * CELL_THREADS), 1u, na);
+            eq_mmse<NRX, NT, NBPS>(A, sg, zfi, wtab, zst, nv, cur, llr, scr, u < units);
+            if (m1) cur = nb;
+        }
+        return;
+    }
     if constexpr (SM) {  // spatial multiplexing: unit = one cell carrying NT symbols, MMSE (rx_eq.hpp)
         const float nv = dc ? A.nv_d[size_t(pkt) * RX_MAX_DOPS + dc - 1] : 0.f;
         uint32_t si = 0;
@@ -229,7 +258,7 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
             const bool m1 = u + CELL_THREADS < units, m2 = u + 2 * CELL_THREADS < units;
             if (m1) unit_stage_b_sm<NRX, NT>(A, sg, Yp, seq, na, nb);
             if (m2) unit_stage_a(A, sg, nseg, si, u + 2 * CELL_THREADS, 1u, na);
-            eq_mmse<NRX, NT>(A, sg, zfi, wtab, zst, nv, cur, llr);
+            eq_mmse<NRX, NT, NBPS>(A, sg, zfi, wtab, zst, nv, cur, llr);
             if (m1) cur = nb;
         }
         return;
@@ -280,12 +309,19 @@ hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st) {
 }
 
 hipError_t launch_rx_cells_sm(const rx_cells_args& a, uint32_t n, hipStream_t st) {
-    const size_t lds = cell_lds_bytes(a.N_RX, a.NT, a.n_drs, a.wcap[0], a.wcap[1]);
+    size_t lds = cell_lds_bytes(a.N_RX, a.NT, a.n_drs, a.wcap[0], a.wcap[1]);
+    if (DNRP_MMSE_MFMA && a.NT == 4) lds = (lds + 15) / 16 * 16 + CELL_THREADS / 64 * a.N_RX * 4 * 24 * sizeof(float2);
     if (lds > 160 * 1024 || a.n_pkt != n) return hipErrorInvalidValue;
     const dim3 g((n + 7) / 8 * 8 * a.n_epochs), b(CELL_THREADS);
+    // the demapper width compiled in for 64- and 256-QAM
 #define DNRP_CELLS_SM(R, T)                                                              \
     if (a.N_RX == R && a.NT == T) {                                                      \
-        hipLaunchKernelGGL((rx_cells_kernel<R, T, true>), g, b, lds, st, a);             \
+        if (a.N_bps == 6)                                                                \
+            hipLaunchKernelGGL((rx_cells_kernel<R, T, true, 6>), g, b, lds, st, a);      \
+        else if (a.N_bps == 8)                                                           \
+            hipLaunchKernelGGL((rx_cells_kernel<R, T, true, 8>), g, b, lds, st, a);      \
+        else                                                                             \
+            hipLaunchKernelGGL((rx_cells_kernel<R, T, true>), g, b, lds, st, a);         \
         return hipGetLastError();                                                        \
     }
     DNRP_CELLS_SM(2, 2)

@@ -10,6 +10,9 @@
 
 namespace dnrp::dev {
 
+#ifndef DNRP_MMSE_MFMA
+#define DNRP_MMSE_MFMA 0  // 4-stream MMSE Gram on v_mfma_f32_4x4x1_16b_f32 (A/B in DESIGN.md)
+#endif
 #ifndef DNRP_CELLS_CH
 #define DNRP_CELLS_CH 3  // SFBC interpolation taps per chunk (eq_compute): 3 keeps rx_cells<4, 4> at 121 VGPRs (4: 131, one workgroup per CU)
 #endif
@@ -341,22 +344,27 @@ __device__ __forceinline__ void unit_stage_b_sm(const rx_cells_args& A, const ce
     for (int i = 0; i < 5; ++i) b.sb[i] = as_global(seq)[min(b0 + i, bl)];
 }
 
-// demap + descramble + int16 of one symbol: LLRs base .. base + N_bps - 1; bits: 5 scrambling bytes
-// (byte k at bits 8k) from bit b_first & ~7 of the unit's first LLR
-__device__ __forceinline__ void emit_sym64(float2 x, uint32_t base, uint32_t b_first, uint32_t N_bps, uint64_t bits,
-                                           int16_t* __restrict__ llr) {
+// demap + descramble + int16 of one symbol: LLRs base .. base + N_bps - 1; sw: the symbol's
+// scrambling bits from the top (LLR k's bit at 31 - k). The flip is a sign XOR before the int16
+// rounding (q16 clamps asymmetrically, so it must see the flipped value); two LLRs per saturating
+// v_cvt_pk_i16_i32 after the clamp (a no-op saturation there: the values are in range already).
+__device__ __forceinline__ void emit_symw(float2 x, uint32_t base, uint32_t N_bps, uint32_t sw,
+                                          int16_t* __restrict__ llr) {
     float L[8];
     demap(x, N_bps, L);
-    const uint32_t r0 = base - (b_first & ~7u);
-    auto sbit = [&](uint32_t i) {
-        const uint32_t r = r0 + i;
-        return static_cast<uint32_t>(bits >> (8 * (r >> 3) + 7 - (r & 7u))) & 1u;
+    auto q = [&](uint32_t k) {
+        const float v = __uint_as_float(__float_as_uint(L[k]) ^ ((sw << k) & 0x80000000u));
+        return static_cast<int>(fminf(32767.f, fmaxf(-32768.f, rintf(v))));
     };
     uint32_t w[4];  // the symbol's LLRs as int16 pairs
 #pragma unroll
     for (uint32_t k = 0; k < 8; k += 2) {
-        const int16_t v0 = q16(sbit(k) ? -L[k] : L[k]), v1 = q16(sbit(k + 1) ? -L[k + 1] : L[k + 1]);
-        w[k / 2] = static_cast<uint16_t>(v0) | (static_cast<uint32_t>(static_cast<uint16_t>(v1)) << 16);
+        if (k >= N_bps) {
+            w[k / 2] = 0;
+            continue;
+        }
+        const auto pk = __builtin_amdgcn_cvt_pk_i16(q(k), q(k + 1));
+        w[k / 2] = static_cast<uint16_t>(pk[0]) | static_cast<uint32_t>(static_cast<uint16_t>(pk[1])) << 16;
     }
     // one store per symbol where the width allows (N_bps LLRs = 2 N_bps bytes at their natural
     // alignment), else per LLR
@@ -380,44 +388,112 @@ __device__ __forceinline__ void emit_sym64(float2 x, uint32_t base, uint32_t b_f
     }
 }
 
-template <int NRX, int NT>
+// Experiment (DNRP_MMSE_MFMA): the 4x4 Gram H^H H of the wave's 64 cells on the matrix pipe. The
+// 16-block 4x4x1 MFMA takes lane 4b+i's A/B value as row/column i of block b and returns G_b[i][j]
+// in lane 4b+j, component i. Per group of 16 cells: the group's H goes through the wave's LDS
+// scratch [NRX][4] rows of 16 cells so lane 4b+i holds H[a][i] of cell b, 4*NRX MFMAs (re: hr hr^T
+// + hi hi^T, im: hr hi^T - hi hr^T), G back through [4][4] rows of 16 cells to the cell's lane. A row
+// stride of 24 float2 puts the four rows one half-wave reads on disjoint bank quarters. Needs the
+// whole wave.
+template <int NRX>
+__device__ __forceinline__ void gram_mfma(const float2 (&h)[NRX][4], float2* scr, float nv, float (&gd)[4],
+                                          float2 (&go)[4][4]) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const uint32_t lane = threadIdx.x & 63u, c = lane & 15u, blk = lane >> 2, col = lane & 3u;
+    auto wsync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+        if ((lane >> 4) == g) {
+#pragma unroll
+            for (int a = 0; a < NRX; ++a)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) scr[(a * 4 + t) * 24 + c] = h[a][t];
+        }
+        wsync();
+        float2 hv[NRX];
+#pragma unroll
+        for (int a = 0; a < NRX; ++a) hv[a] = scr[(a * 4 + col) * 24 + blk];
+        wsync();
+        v4f gr = {0.f, 0.f, 0.f, 0.f}, gi = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < NRX; ++a) {
+            gr = __builtin_amdgcn_mfma_f32_4x4x1f32(hv[a].x, hv[a].x, gr, 0, 0, 0);
+            gr = __builtin_amdgcn_mfma_f32_4x4x1f32(hv[a].y, hv[a].y, gr, 0, 0, 0);
+            gi = __builtin_amdgcn_mfma_f32_4x4x1f32(hv[a].x, hv[a].y, gi, 0, 0, 0);
+            gi = __builtin_amdgcn_mfma_f32_4x4x1f32(-hv[a].y, hv[a].x, gi, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) scr[(i * 4 + col) * 24 + blk] = make_float2(gr[i], gi[i]);
+        wsync();
+        const bool mine = (lane >> 4) == g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float2 d = scr[(i * 4 + i) * 24 + c];
+            if (mine) gd[i] = nv + d.x;
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                const float2 v = scr[(i * 4 + j) * 24 + c];
+                if (mine) go[i][j] = v;
+            }
+        }
+        wsync();
+    }
+}
+
+template <int NRX, int NT, int NBPS = 0>
 __device__ __forceinline__ void eq_mmse(const rx_cells_args& A, const cell_seg* sg, const float2* zfi, const float* wtab,
-                                        uint32_t zst, float nv, const unit_sm<NRX, NT>& b, int16_t* __restrict__ llr) {
+                                        uint32_t zst, float nv, const unit_sm<NRX, NT>& b, int16_t* __restrict__ llr,
+                                        float2* scr = nullptr, bool act = true) {
+    const uint32_t N_bps = NBPS ? NBPS : A.N_bps;
     const uint32_t info = sg[b.si].info, wbase = sg[b.si].wbase;
     const uint32_t mode = info & 1u, off = (info >> 4) & 0xFFu, nI = info >> 12;
-    const uint32_t step = mode ? 1u : 2u;
-    // Wiener interpolation of every (rx, stream) at the cell (rx_synced.cpp:932-946)
+    const uint32_t sh = mode ? 0u : 1u;  // pilot step 1 (mode lr) or 2 (mode l, interlaced)
+    // Wiener interpolation of every (rx, stream) at the cell (rx_synced.cpp:932-946); the pilot
+    // buffer holds antenna pairs interleaved here (build_pilots<., ., true>): one 16-B read per pair
+    // and tap, the pairs zst * 2 cells apart
+    static_assert(NRX % 2 == 0, "MMSE: antenna pairs");
+    typedef float f4 __attribute__((ext_vector_type(4)));
     float2 h[NRX][NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         uint32_t p = b.pw[t] & 0xFFFFu;
         if (!mode) p = 2 * p + ((off >> t) & 1u);
-        const uint32_t pos = p + t * zst, wo = wbase + (b.pw[t] >> 16) * nI;
+        const float2* zr = zfi + (t * (NRX / 2) * zst + p) * 2;
+        const float* wb = wtab + wbase + (b.pw[t] >> 16) * nI;
+        const uint32_t zs = 2u << sh;
 #pragma unroll
         for (int a = 0; a < NRX; ++a) h[a][t] = make_float2(0.f, 0.f);
-        for (uint32_t i = 0; i < nI; ++i) {
-            const float wv = wtab[wo + i];
-            const uint32_t q = pos + i * step;
+#pragma unroll 4
+        for (uint32_t i = 0; i < nI; ++i, zr += zs) {
+            const float w = wb[i];
 #pragma unroll
-            for (int a = 0; a < NRX; ++a) {
-                const float2 z = zfi[a * NT * zst + q];
-                h[a][t].x = fmaf(z.x, wv, h[a][t].x);
-                h[a][t].y = fmaf(z.y, wv, h[a][t].y);
+            for (int q = 0; q < NRX / 2; ++q) {
+                const f4 z = *reinterpret_cast<const f4*>(zr + q * zst * 2);
+                h[2 * q][t].x = fmaf(z.x, w, h[2 * q][t].x);
+                h[2 * q][t].y = fmaf(z.y, w, h[2 * q][t].y);
+                h[2 * q + 1][t].x = fmaf(z.z, w, h[2 * q + 1][t].x);
+                h[2 * q + 1][t].y = fmaf(z.w, w, h[2 * q + 1][t].y);
             }
         }
     }
     // G = H^H H + nv I (diagonal gd, strictly lower go[i][j] = sum_a conj(h_ai) h_aj), z = H^H y
     float gd[NT];
     float2 go[NT][NT], zz[NT];
+    constexpr bool mf = DNRP_MMSE_MFMA && NT == 4;
+    if constexpr (mf) gram_mfma<NRX>(h, scr, nv, gd, go);
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-        gd[i] = nv;
         zz[i] = make_float2(0.f, 0.f);
 #pragma unroll
-        for (int a = 0; a < NRX; ++a) {
-            gd[i] += cnorm(h[a][i]);
-            zz[i] = cadd(zz[i], cmulc(b.r0[a], h[a][i]));
-        }
+        for (int a = 0; a < NRX; ++a) zz[i] = cadd(zz[i], cmulc(b.r0[a], h[a][i]));
+        if constexpr (mf) continue;
+        gd[i] = nv;
+#pragma unroll
+        for (int a = 0; a < NRX; ++a) gd[i] += cnorm(h[a][i]);
 #pragma unroll
         for (int j = 0; j < i; ++j) {
             go[i][j] = make_float2(0.f, 0.f);
@@ -461,10 +537,12 @@ __device__ __forceinline__ void eq_mmse(const rx_cells_args& A, const cell_seg* 
 #pragma unroll
         for (int q = 0; q <= m; ++q) w[m] = cadd(w[m], cmul(Mi[m][q], zz[q]));
     }
-    const uint32_t b_first = b.jj * NT * A.N_bps;
-    uint64_t bits = 0;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) bits |= static_cast<uint64_t>(b.sb[i] & 0xFFu) << (8 * i);
+    // the cell's scrambling bits big-endian from bit (b_first & ~7): bit r at 63 - r
+    const uint32_t b_first = b.jj * NT * N_bps;
+    const uint64_t be = static_cast<uint64_t>((b.sb[0] & 0xFFu) << 24 | (b.sb[1] & 0xFFu) << 16 | (b.sb[2] & 0xFFu) << 8 |
+                                              (b.sb[3] & 0xFFu))
+                            << 32 |
+                        static_cast<uint64_t>(b.sb[4] & 0xFFu) << 24;
 #pragma unroll
     for (int s = 0; s < NT; ++s) {
         float2 x = make_float2(0.f, 0.f);
@@ -475,7 +553,8 @@ __device__ __forceinline__ void eq_mmse(const rx_cells_args& A, const cell_seg* 
             ginv += cnorm(Mi[m][s]);
         }
         const float beta = 1.f - nv * ginv;
-        emit_sym64(cscale(x, 1.0f / beta), b_first + s * A.N_bps, b_first, A.N_bps, bits, llr);
+        const uint32_t sw = static_cast<uint32_t>((be << ((b_first & 7u) + s * N_bps)) >> 32);
+        if (act) emit_symw(cscale(x, __builtin_amdgcn_rcpf(beta)), b_first + s * N_bps, N_bps, sw, llr);
     }
 }
 
@@ -484,14 +563,21 @@ __device__ __forceinline__ void eq_mmse(const rx_cells_args& A, const cell_seg* 
 // source DRS op of every (ts, interlace slot), its parity and symbol are workgroup-uniform (scalar
 // loads); a thread loads the subcarrier indices of one pilot index for every (ts, slot) at once, then
 // the cells of every (rx, ts, slot): two memory round trips. Slots without a source read a valid
-// cell and store zero.
-template <int NRX, int NT>
+// cell and store zero. Layout [NRX][NT][zst], or for the MMSE path (AI) antenna pairs interleaved,
+// [NT][NRX / 2][zst][2]: one 16-B read per antenna pair and tap. (All NRX antennas of a pilot
+// contiguous, [NT][zst][NRX], puts the lanes' pilots 32 B apart and reads 8-16 B of each: 9
+// conflict cycles per LDS instruction, measured; padded to NRX + 1 cells per pilot it is conflict-
+// free but 25 % larger, one workgroup per CU instead of two: slower still.)
+template <int NRX, int NT, bool AI = false>
 __device__ __forceinline__ void build_pilots(const rx_cells_args& A, const rx_epoch* E, const float2* Yp, float2* zfi,
                                              uint32_t tid, uint32_t nthreads) {
     const uint32_t nd = A.n_drs, zst = zfi_stride(nd);
     const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
+    auto zi = [&](uint32_t a, uint32_t t, uint32_t idx) {
+        return AI ? ((t * (NRX / 2) + a / 2) * zst + idx) * 2 + (a & 1u) : (a * NT + t) * zst + idx;
+    };
     for (uint32_t e = tid; e < NRX * NT * ZFI_PAD; e += nthreads)
-        zfi[(e / ZFI_PAD) * zst + 2 * nd + e % ZFI_PAD] = make_float2(0.f, 0.f);
+        zfi[zi(e / ZFI_PAD / NT, e / ZFI_PAD % NT, 2 * nd + e % ZFI_PAD)] = make_float2(0.f, 0.f);
     // sources of all (ts, slot) first, then their DRS ops (two scalar round trips); a slot without a
     // source reads op 0 and is stored as zero
     uint32_t src[NT][2], kb[NT][2], yo[NT][2];
@@ -532,7 +618,7 @@ __device__ __forceinline__ void build_pilots(const rx_cells_args& A, const rx_ep
             for (int o = 0; o < 2; ++o)
 #pragma unroll
                 for (int a = 0; a < NRX; ++a)
-                    zfi[(a * NT + t) * zst + 2 * i + o] = ok[t][o] ? cscale(v[t][o][a], dv[t]) : make_float2(0.f, 0.f);
+                    zfi[zi(a, t, 2 * i + o)] = ok[t][o] ? cscale(v[t][o][a], dv[t]) : make_float2(0.f, 0.f);
     }
 }
 
