@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
         }
         if (tid < 12) pairs[tid] = A.pair[tid];
     }
-    if constexpr (!experiment(XS_CELLS_SKIP_PRO)) build_pilots<NRX, NT, SM>(A, E, Yp, zfi, tid, CELL_THREADS);
+    if constexpr (!experiment(XS_CELLS_SKIP_PRO)) build_pilots<NRX, NT, cells_ai(NRX, NT)>(A, E, Yp, zfi, tid, CELL_THREADS);
     __syncthreads();
     if constexpr (experiment(XS_CELLS_SKIP_MAIN)) {
         if (tid < units) A.llr[size_t(row) * A.llr_stride + tid] = static_cast<int16_t>(zfi[tid].x);

@@ -17,9 +17,25 @@ namespace dnrp::dev {
 #define DNRP_CELLS_CH 3  // SFBC interpolation taps per chunk (eq_compute): 3 keeps rx_cells<4, 4> at 121 VGPRs (4: 131, one workgroup per CU)
 #endif
 
+// the pilot-buffer layout of rx_cells_kernel<NRX, NT, SM>: antenna pairs interleaved for the MMSE
+// path and for SFBC with an even antenna count (build_pilots)
+__host__ __device__ constexpr bool cells_ai(int NRX, int NT) { return NT > 1 && NRX % 2 == 0; }
+
 __device__ __forceinline__ int16_t q16(float v) {
     const float r = rintf(v);
     return static_cast<int16_t>(fminf(32767.f, fmaxf(-32768.f, r)));
+}
+
+// two LLRs, each sign-flipped by the top bit of its scrambling word (a sign XOR before the int16
+// rounding: q16 clamps asymmetrically, so it must see the flipped value), as one int16 pair: the
+// saturating v_cvt_pk_i16_i32 packs them (no-op saturation, the values are clamped already)
+__device__ __forceinline__ uint32_t q16_pair(float a, uint32_t fa, float b, uint32_t fb) {
+    auto q = [](float v, uint32_t f) {
+        const float x = __uint_as_float(__float_as_uint(v) ^ (f & 0x80000000u));
+        return static_cast<int>(fminf(32767.f, fmaxf(-32768.f, rintf(x))));
+    };
+    const auto pk = __builtin_amdgcn_cvt_pk_i16(q(a, fa), q(b, fb));
+    return static_cast<uint16_t>(pk[0]) | static_cast<uint32_t>(static_cast<uint16_t>(pk[1])) << 16;
 }
 
 // srsRAN demod_soft restatement: LTE max-log per axis with int16 scale constants
@@ -161,14 +177,11 @@ __device__ __forceinline__ void emit_cell(float2 x, uint32_t j, uint32_t j0, uin
     demap(x, N_bps, L);
     const uint32_t base = j * N_bps, r0 = base - ((j0 * N_bps) & ~7u);  // bit offset in `bits`
     auto sbit = [&](uint32_t i) { const uint32_t r = r0 + i; return (bits >> (8 * (r >> 3) + 7 - (r & 7u))) & 1u; };
-    if (N_bps == 8) {  // one 16-B store
+    if (N_bps == 8) {  // one 16-B store; the cell's scrambling byte is byte r0 / 8 of `bits`
+        const uint32_t sw = (bits >> r0) << 24;  // LLR b's bit at 31 - b
         uint32_t w[4];
 #pragma unroll
-        for (int b = 0; b < 8; b += 2) {
-            const float v0 = sbit(b) ? -L[b] : L[b];
-            const float v1 = sbit(b + 1) ? -L[b + 1] : L[b + 1];
-            w[b / 2] = static_cast<uint16_t>(q16(v0)) | (static_cast<uint32_t>(static_cast<uint16_t>(q16(v1))) << 16);
-        }
+        for (int b = 0; b < 8; b += 2) w[b / 2] = q16_pair(L[b], sw << b, L[b + 1], sw << (b + 1));
         int16_t* dst = llr + base;
         if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
             *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
@@ -201,13 +214,18 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
     const uint32_t info = sg[b.si].info, wbase = sg[b.si].wbase;
     const uint32_t mode = info & 1u, off = (info >> 4) & 0xFFu, nI = info >> 12;
     const uint32_t step = mode ? 1u : 2u;
+    // SFBC with an even antenna count reads the antenna-pair-interleaved pilot buffer (AI, see
+    // build_pilots): positions in float2 of the stream's first pair row, pilot steps of 2 float2
+    constexpr bool AI = cells_ai(NRX, NT);
+    constexpr uint32_t PS = AI ? 2u : 1u;
     uint32_t pos[NC], wo[NC];  // pilot start (LDS float2 index) and weight offset (LDS float index)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const uint32_t t = c < 2 ? (b.tab & 0xFu) : (b.tab >> 4);
         uint32_t p = b.pw[c] & 0xFFFFu;
         if (!mode) p = 2 * p + ((off >> t) & 1u);  // non-interlaced: latest DRS symbol only
-        pos[c] = p + (experiment(XS_CELLS_ONE_ROW) ? 0u : t * zst);
+        pos[c] = AI ? ((experiment(XS_CELLS_ONE_ROW) ? 0u : t * (NRX / 2) * zst) + p) * 2
+                    : p + (experiment(XS_CELLS_ONE_ROW) ? 0u : t * zst);
         wo[c] = wbase + (experiment(XS_CELLS_ONE_WROW) ? 0u : (b.pw[c] >> 16) * nI);
     }
     if constexpr (NT == 1) {
@@ -254,11 +272,12 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
         for (int s = 0; s < 2; ++s) {
             const bool up = pos[2 * s + 1] >= pos[2 * s];
             base[s] = up ? pos[2 * s] : pos[2 * s + 1];
-            sh[s] = (up ? pos[2 * s + 1] - pos[2 * s] : pos[2 * s] - pos[2 * s + 1]) / step;
+            sh[s] = (up ? pos[2 * s + 1] - pos[2 * s] : pos[2 * s] - pos[2 * s + 1]) / (PS * step);
             wl[s] = up ? wo[2 * s] : wo[2 * s + 1];
             wh[s] = up ? wo[2 * s + 1] : wo[2 * s];
         }
         const uint32_t ntap = nI + max(sh[0], sh[1]);
+        const uint32_t psh = (AI ? 1u : 0u) + (mode ? 0u : 1u);  // log2(PS * step): a shift, not v_mul_lo
         float2 g[NRX][2];
 #pragma unroll
         for (int a = 0; a < NRX; ++a) g[a][0] = g[a][1] = make_float2(0.f, 0.f);
@@ -279,9 +298,19 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
                     const uint32_t i = i0 + j, ih = i - sh[s];  // ih wraps for i < sh
                     const float lo = wtab[wl[s] + min(i, nI - 1)], hi = wtab[wh[s] + min(ih, nI - 1)];
                     wv[j] = 0.5f * ((i < nI ? lo : 0.f) + (ih < nI ? hi : 0.f));
-                    const uint32_t p = base[s] + min(i, nI + sh[s]) * step;
+                    const uint32_t p = base[s] + (min(i, nI + sh[s]) << psh);
+                    if constexpr (AI) {
+                        typedef float f4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-                    for (int a = 0; a < NRX; ++a) z[j][a] = zfi[a * NT * zst + p];
+                        for (int q = 0; q < NRX / 2; ++q) {
+                            const f4 v = *reinterpret_cast<const f4*>(zfi + p + q * zst * 2);
+                            z[j][2 * q] = make_float2(v.x, v.y);
+                            z[j][2 * q + 1] = make_float2(v.z, v.w);
+                        }
+                    } else {
+#pragma unroll
+                        for (int a = 0; a < NRX; ++a) z[j][a] = zfi[a * NT * zst + p];
+                    }
                 }
 #pragma unroll
                 for (uint32_t j = 0; j < CH; ++j)
@@ -345,27 +374,14 @@ __device__ __forceinline__ void unit_stage_b_sm(const rx_cells_args& A, const ce
 }
 
 // demap + descramble + int16 of one symbol: LLRs base .. base + N_bps - 1; sw: the symbol's
-// scrambling bits from the top (LLR k's bit at 31 - k). The flip is a sign XOR before the int16
-// rounding (q16 clamps asymmetrically, so it must see the flipped value); two LLRs per saturating
-// v_cvt_pk_i16_i32 after the clamp (a no-op saturation there: the values are in range already).
+// scrambling bits from the top (LLR k's bit at 31 - k)
 __device__ __forceinline__ void emit_symw(float2 x, uint32_t base, uint32_t N_bps, uint32_t sw,
                                           int16_t* __restrict__ llr) {
     float L[8];
     demap(x, N_bps, L);
-    auto q = [&](uint32_t k) {
-        const float v = __uint_as_float(__float_as_uint(L[k]) ^ ((sw << k) & 0x80000000u));
-        return static_cast<int>(fminf(32767.f, fmaxf(-32768.f, rintf(v))));
-    };
     uint32_t w[4];  // the symbol's LLRs as int16 pairs
 #pragma unroll
-    for (uint32_t k = 0; k < 8; k += 2) {
-        if (k >= N_bps) {
-            w[k / 2] = 0;
-            continue;
-        }
-        const auto pk = __builtin_amdgcn_cvt_pk_i16(q(k), q(k + 1));
-        w[k / 2] = static_cast<uint16_t>(pk[0]) | static_cast<uint32_t>(static_cast<uint16_t>(pk[1])) << 16;
-    }
+    for (uint32_t k = 0; k < 8; k += 2) w[k / 2] = k < N_bps ? q16_pair(L[k], sw << k, L[k + 1], sw << (k + 1)) : 0u;
     // one store per symbol where the width allows (N_bps LLRs = 2 N_bps bytes at their natural
     // alignment), else per LLR
     int16_t* dst = llr + base;
