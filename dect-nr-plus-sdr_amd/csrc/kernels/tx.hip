@@ -522,6 +522,7 @@ struct txs_wave {
     // MODE: TXS_SISO (N_TS = 1), TXS_TXDIV (transmit diversity), TXS_SM (N_SS streams, PCC paired)
     template <int MODE, bool Q8, bool PCC>
     __device__ float2 bin_df(uint32_t c, const uint8_t* sb, uint32_t ab, const uint8_t* pcb) const {
+        if constexpr (experiment(XS_TX_TRIVIAL_BINS)) return make_float2(__uint_as_float(c), 0.f);
         const uint32_t ty = c & CODE_MASK, j = c & CODE_J_MASK, pr = (c >> CODE_PAIR_SHIFT) & 0xFFu;
         if constexpr (MODE == TXS_TXDIV1 || MODE == TXS_SM1) {
             // the pair (tA, tB) of this cell: the antenna's stream is tA (x0 = symbol j) or tB (the

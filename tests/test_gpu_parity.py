@@ -404,6 +404,9 @@ SM_CASES = {
     "tm6_u8b16_256qam": ((8, 16, 1, 1, 6, 8), (8, 16, 4, 1, 10, 9), (40.0,)),
     "tm2_sm2_u2b2": ((2, 2, 1, 2, 2, 6), (2, 2, 2, 1, 10, 9), (15.0, 30.0)),
     "tm4_cl_sm2_u1b4": ((1, 4, 1, 2, 4, 3), (1, 4, 2, 1, 10, 9), (25.0,)),
+    # 8 RX antennas: rx_cells_kernel<8, 4, true> and <8, 2, true>
+    "tm6_u2b4_8rx_16qam": ((2, 4, 1, 2, 6, 4), (2, 4, 8, 1, 10, 9), (25.0,)),
+    "tm2_sm2_u2b2_8rx": ((2, 2, 1, 2, 2, 6), (2, 2, 8, 1, 10, 9), (20.0,)),
 }
 
 
