@@ -29,7 +29,8 @@ enum xs_bit : unsigned {
     XS_CELLS_ONE_ROW = 1u << 9,
     XS_CELLS_ONE_WROW = 1u << 10,
     XS_TX_NO_QTAB = 1u << 11,
-    XS_TX_TRIVIAL_BINS = 1u << 12,  // TX: a DF bin's value is its code (no mapping; timing / ISA only)
+    XS_TX_TRIVIAL_BINS = 1u << 12,
+    XS_CELLS_ONE_PILOT = 1u << 13,  // rx_cells: every unit reads its windows from pilot 0 (conflict attribution)  // TX: a DF bin's value is its code (no mapping; timing / ISA only)
 };
 
 __host__ __device__ constexpr bool experiment(unsigned bit) { return (DNRP_EXPERIMENTS & bit) != 0u; }

@@ -224,6 +224,7 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
         const uint32_t t = c < 2 ? (b.tab & 0xFu) : (b.tab >> 4);
         uint32_t p = b.pw[c] & 0xFFFFu;
         if (!mode) p = 2 * p + ((off >> t) & 1u);  // non-interlaced: latest DRS symbol only
+        if (experiment(XS_CELLS_ONE_PILOT)) p = 0;
         pos[c] = AI ? ((experiment(XS_CELLS_ONE_ROW) ? 0u : t * (NRX / 2) * zst) + p) * 2
                     : p + (experiment(XS_CELLS_ONE_ROW) ? 0u : t * zst);
         wo[c] = wbase + (experiment(XS_CELLS_ONE_WROW) ? 0u : (b.pw[c] >> 16) * nI);
