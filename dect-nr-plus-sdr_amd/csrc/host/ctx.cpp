@@ -232,6 +232,37 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
                 *err = DNRP_ENOMEM;
                 return nullptr;
             }
+            // one-hot W rows: every bin's code resolved per antenna stream ts (tx.hip bin_oh), so the
+            // kernel maps a bin without the pair tests (tx.hip bin_df TXS_TXDIV1 / TXS_SM1 restated)
+            const uint32_t NTS = t->tm.N_TS;
+            bool oh_ok = NTS > 1;
+            std::vector<uint32_t> oh(oh_ok ? size_t(NTS) * cb.size() : 0u, 0u);
+            for (uint32_t ts = 0; ts < NTS && oh_ok; ++ts)
+                for (size_t i = 0; i < cb.size(); ++i) {
+                    const uint32_t c = cb[i], ty = c & dev::CODE_MASK, j = c & dev::CODE_J_MASK;
+                    const uint32_t pr = (c >> dev::CODE_PAIR_SHIFT) & 0xFFu;
+                    const bool ua = (pr & 0xFu) == ts, ub = (pr >> 4) == ts;
+                    uint32_t o = 0;
+                    if (ty == dev::CODE_DRS) {
+                        if (ua) o = dev::CODE_DRS | ((j & 8u) ? dev::OH_NEG : 0u);
+                    } else if (ty == dev::CODE_PDC && !t->tm.txdiv) {  // spatial multiplexing: the stream's symbol
+                        const uint64_t js = uint64_t(j) * t->tm.N_SS + ts;
+                        if (js > dev::CODE_J_MASK) oh_ok = false;
+                        o = dev::CODE_PDC | static_cast<uint32_t>(js & dev::CODE_J_MASK);
+                    } else if ((ty == dev::CODE_PDC || ty == dev::CODE_PCC) && (ua || ub)) {
+                        // SFBC: stream A maps symbol j, stream B the partner j ^ 1 with (-re, +im) for
+                        // even j, (+re, -im) for odd j (transmit_diversity_precoding.cpp:37-75)
+                        const uint32_t flip = ua ? 0u : ((j & 1u) ? dev::OH_FY : dev::OH_FX);
+                        o = ty | (j ^ (ua ? 0u : 1u)) | flip;
+                    } else if (ty == dev::CODE_STF) {
+                        o = c;
+                    }
+                    oh[size_t(ts) * cb.size() + i] = o;
+                }
+            if (oh_ok && !t->code_oh.upload(oh)) {
+                *err = DNRP_ENOMEM;
+                return nullptr;
+            }
         }
     }
     if (!t->code.upload(code) || !t->stf.upload(stf) || !t->pdc_off.upload(m.pdc_sym_off) || !t->W.upload(W) || !t->taps.upload(t->rs.h) || !t->taps_pp.upload(taps_polyphase(t->rs, &t->npp)) ||
@@ -894,9 +925,10 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
             const char* mf_env = std::getenv("DNRP_TX_MFMA");
             a.mfma = (mf_env && std::atoi(mf_env)) ? 1u : 0u;
             a.code_bin = t->code_bin.as<uint32_t>();
-            a.onehot = t->tm.N_TS > 1 ? 1u : 0u;  // transmit diversity or spatial multiplexing
+            a.onehot = t->tm.N_TS > 1 && t->code_oh.p ? 1u : 0u;  // transmit diversity or spatial multiplexing
             for (uint32_t i = 0; i < n && a.onehot; ++i)
                 a.onehot = t->w_onehot[desc[i].codebook_index] ? 1u : 0u;
+            a.code_oh = t->code_oh.as<uint32_t>();
             a.pcc_syms = t->pcc_syms;
             a.n_pieces = static_cast<uint32_t>((int64_t(a.n_keep) - mfirst0 + 1279) / 1280);
             // enough wavefronts for ~8 rounds of 16 per CU; each extra segment costs one history FFT

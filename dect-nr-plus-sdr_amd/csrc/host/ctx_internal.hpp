@@ -105,6 +105,7 @@ struct tx_tables {
     geo::resampler_t rs;
     dbuf code, stf, W, taps, taps_pp, tw, qam, qpsk, pdc_off;
     dbuf code_bin;  // [N_DF+1][1024] code per FFT bin, bin lane + 64 m at [m / 4][lane][m % 4] (streaming TX kernel, N_b_DFT_os = 1024)
+    dbuf code_oh;   // [N_TS][N_DF+1][1024] one-hot W codes per antenna stream (kernels.hpp OH_*; empty: not built)
     uint32_t pcc_syms = 0;  // bit l: symbol l carries PCC cells
     uint32_t npp = 0;  // floats in taps_pp
     std::vector<float> wscale, wscale_opt;  // per codebook: standard / optimal_scaling_DAC

@@ -21,6 +21,13 @@ enum : uint32_t {
     CODE_DRS = 3u << 29,
     CODE_STF = 4u << 29,
     CODE_MASK = 7u << 29,
+    // one-hot W rows (tx.hip TXS_TXDIV1 / TXS_SM1): the code of a bin as seen by the antenna whose
+    // nonzero W entry is stream ts (host-built per ts, ctx.cpp). Type PCC / PDC / DRS only where that
+    // stream carries the cell (else 0); bits 0..19: the symbol index to map (SFBC partner or spatial
+    // stream resolved), OH_FX / OH_FY: sign of its re / im part flipped, OH_NEG: DRS value -1
+    OH_FX = 1u << 20,
+    OH_FY = 1u << 21,
+    OH_NEG = 1u << 22,
 };
 
 // ---------------------------------------------------------------- TX
@@ -63,6 +70,7 @@ struct tx_args {
     uint32_t n_pieces, n_seg, piece_per_seg, stream;
     uint32_t pcc_syms;         // bit l: symbol l (< 32) carries PCC cells
     uint32_t onehot;           // transmit diversity with one nonzero W entry per antenna row (every packet)
+    const uint32_t* code_oh;   // onehot: [N_TS][N_DF+1][1024] per-stream codes (code_bin layout), see OH_*
     uint32_t sb_chunks;        // spatial multiplexing: 1 KiB chunks of a symbol's PDC staging window (<= 4)
     // N_b_DFT_os > 1024 (beyond the block path's registers): every symbol's cyclic-prefixed DECT-rate
     // samples through a scratch [packet][antenna][big_len] (tx_big_sym_kernel, tx_big_resample_kernel)

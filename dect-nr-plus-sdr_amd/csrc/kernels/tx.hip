@@ -579,6 +579,29 @@ struct txs_wave {
         v = (ty == CODE_PDC || ty == CODE_DRS || (PCC && ty == CODE_PCC)) ? v : make_float2(0.f, 0.f);
         return v;  // wrow carries scale_df (one multiply per W entry instead of two per bin)
     }
+    // TXS_TXDIV1 / TXS_SM1 from the antenna stream's own code table (ctx.cpp, kernels.hpp OH_*):
+    // the pair tests, the partner index and its flips were resolved on the host, so a bin is one
+    // table read, the flips as sign XORs, one complex product and the type select (bin_df's
+    // TXS_TXDIV1 branch, bit for bit)
+    template <bool Q8, bool PCC, uint32_t SBW>
+    __device__ float2 bin_oh(uint32_t c, const uint8_t* sb, uint32_t ab, const uint8_t* pcb) const {
+        if constexpr (experiment(XS_TX_TRIVIAL_BINS)) return make_float2(__uint_as_float(c), 0.f);
+        const uint32_t ty = c & CODE_MASK, js = c & CODE_J_MASK;
+        float2 x = pdc_sym<Q8, SBW>(sb, ab, js);
+        if constexpr (PCC) {
+            const float2 px = pcc_sym(pcb, js);
+            x = ty == CODE_PCC ? px : x;
+        }
+        x = make_float2(__uint_as_float(__float_as_uint(x.x) ^ ((c << 11) & 0x80000000u)),
+                        __uint_as_float(__float_as_uint(x.y) ^ ((c << 10) & 0x80000000u)));
+        const float2 v = cmul(wsel, x);
+        const uint32_t ds = (c << 9) & 0x80000000u;  // OH_NEG
+        const float2 d = make_float2(__uint_as_float(__float_as_uint(wsel.x) ^ ds), __uint_as_float(__float_as_uint(wsel.y) ^ ds));
+        const bool kv = ty == CODE_PDC || (PCC && ty == CODE_PCC), kd = ty == CODE_DRS;
+        const uint32_t mv = 0u - static_cast<uint32_t>(kv), md = 0u - static_cast<uint32_t>(kd);
+        return make_float2(__uint_as_float((__float_as_uint(v.x) & mv) | (__float_as_uint(d.x) & md)),
+                           __uint_as_float((__float_as_uint(v.y) & mv) | (__float_as_uint(d.y) & md)));
+    }
     // STF bin n (stf.cpp:185-285 values, STF scaling)
     __device__ float2 bin_stf(uint32_t c, uint32_t n) const {
         const uint32_t N = A->N_occ;
@@ -739,9 +762,12 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
     // cell codes of the piece's 16 bins per lane, loaded one piece ahead: issued before the piece's
     // output stores, so waiting for them never waits for those stores (vmcnt retires in order)
     uint32_t cd[16];
+    // one-hot W rows: the antenna stream's own code table (bin_oh)
+    constexpr bool OH = MODE == TXS_TXDIV1 || MODE == TXS_SM1;
+    const uint32_t* ctab = OH ? A.code_oh + size_t(T.tsel) * (A.N_DF + 1) * 1024 : A.code_bin;
     auto load_codes = [&](uint32_t rr, uint32_t ln) {
         const uint32_t ls = txs_sym(rr, A.N_DF);
-        const uint4* crow = reinterpret_cast<const uint4*>(A.code_bin + size_t(min(ls, A.N_DF)) * 1024);
+        const uint4* crow = reinterpret_cast<const uint4*>(ctab + size_t(min(ls, A.N_DF)) * 1024);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {  // the codes of bins ln + 64 m, m = 4 j .. 4 j + 3, in one load
             const uint4 c = crow[64 * j + ln];
@@ -793,13 +819,17 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
                 for (int m = 0; m < 16; ++m) v[m] = T.bin_stf(cd[m], lid + 64 * m);
             } else if ((l < 32) && ((A.pcc_syms >> l) & 1u)) {
 #pragma unroll
-                for (int m = 0; m < 16; ++m) v[m] = T.template bin_df<MODE, Q8, true>(cd[m], sb, ab, pcb);
+                for (int m = 0; m < 16; ++m) {
+                    if constexpr (OH) v[m] = T.template bin_oh<Q8, true, MODE == TXS_SM1 ? TXS_SBW_SM : 1024u>(cd[m], sb, ab, pcb);
+                    else v[m] = T.template bin_df<MODE, Q8, true>(cd[m], sb, ab, pcb);
+                }
             } else {
 #pragma unroll
                 for (int m = 0; m < 16; ++m) {
                     // two groups of 8 bins: the table reads of 8 bins in flight at a time (all 16 spill)
-                    if ((MODE == TXS_TXDIV1 || MODE == TXS_SM1) && m == 8) __builtin_amdgcn_sched_barrier(0);
-                    v[m] = T.template bin_df<MODE, Q8, false>(cd[m], sb, ab, pcb);
+                    if (OH && m == 8) __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (OH) v[m] = T.template bin_oh<Q8, false, MODE == TXS_SM1 ? TXS_SBW_SM : 1024u>(cd[m], sb, ab, pcb);
+                    else v[m] = T.template bin_df<MODE, Q8, false>(cd[m], sb, ab, pcb);
                 }
             }
             __builtin_amdgcn_wave_barrier();
