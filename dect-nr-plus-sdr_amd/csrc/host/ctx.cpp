@@ -244,7 +244,7 @@ tx_tables* get_tx(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
                     const bool ua = (pr & 0xFu) == ts, ub = (pr >> 4) == ts;
                     uint32_t o = 0;
                     if (ty == dev::CODE_DRS) {
-                        if (ua) o = dev::CODE_DRS | ((j & 8u) ? dev::OH_NEG : 0u);
+                        if (ua) o = dev::CODE_DRS | ((j & 8u) ? dev::OH_FX : 0u);
                     } else if (ty == dev::CODE_PDC && !t->tm.txdiv) {  // spatial multiplexing: the stream's symbol
                         const uint64_t js = uint64_t(j) * t->tm.N_SS + ts;
                         if (js > dev::CODE_J_MASK) oh_ok = false;

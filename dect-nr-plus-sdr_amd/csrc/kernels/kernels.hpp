@@ -24,10 +24,10 @@ enum : uint32_t {
     // one-hot W rows (tx.hip TXS_TXDIV1 / TXS_SM1): the code of a bin as seen by the antenna whose
     // nonzero W entry is stream ts (host-built per ts, ctx.cpp). Type PCC / PDC / DRS only where that
     // stream carries the cell (else 0); bits 0..19: the symbol index to map (SFBC partner or spatial
-    // stream resolved), OH_FX / OH_FY: sign of its re / im part flipped, OH_NEG: DRS value -1
+    // stream resolved), OH_FX / OH_FY: sign of its re / im part flipped (DRS: the point (1, 0), OH_FX
+    // for the value -1)
     OH_FX = 1u << 20,
     OH_FY = 1u << 21,
-    OH_NEG = 1u << 22,
 };
 
 // ---------------------------------------------------------------- TX
