@@ -81,7 +81,7 @@ __device__ __forceinline__ void rx_resample_ct(const rx_front_args& A, const rx_
 // wave FFT of R[0..1024) (R also serves as the exchange buffer, >= WFFT_XB float2) and the occupied
 // bins: FFT bin n -> subcarrier index k (n <= N/2: k = n + N/2; upper half: k = n - off_lower),
 // amplitude sqrt(N_b_OCC)/N_b_DFT_os, STO derotation exp(j sto_inc (k - N/2)) by two running
-// phasors stepped by 64 bins. put(k, value) for every k in [0, N_b_OCC]; R is free again when
+// phasors stepped by 64 bins (the amplitude folded into them). put(k, value) for every k in [0, N_b_OCC]; R is free again when
 // put is called (all exchange reads have completed).
 // RT: wave_fft1024_rt with the lane's two twiddles w1 = W^(4 (lane & 15)), wl = W^lane loaded by the
 // caller (e.g. before its input staging) instead of 27 twiddle loads inside the passes
@@ -101,9 +101,11 @@ __device__ __forceinline__ void rx_fft_bins(const rx_front_args& A, const rx_pkt
     __builtin_amdgcn_wave_barrier();
     const uint32_t N = A.N_occ;
     const float2 s64 = phasor(64.0 * S.sto_inc);
-    float2 pa = phasor(S.sto_inc * static_cast<double>(lane));
-    float2 pb = phasor(S.sto_inc * (static_cast<double>(lane) - static_cast<double>(A.off_lower) -
-                                    static_cast<double>(N / 2)));
+    // the amplitude folded into the two derotation phasors: one complex product per bin (A/B per
+    // 16384-slot PDC launch: 19.05 / 18.97 -> 18.82 / 18.55 ms)
+    float2 pa = cscale(phasor(S.sto_inc * static_cast<double>(lane)), A.amp_scale);
+    float2 pb = cscale(phasor(S.sto_inc * (static_cast<double>(lane) - static_cast<double>(A.off_lower) -
+                                           static_cast<double>(N / 2))), A.amp_scale);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         const uint32_t n = lane + 64 * m;
@@ -115,7 +117,7 @@ __device__ __forceinline__ void rx_fft_bins(const rx_front_args& A, const rx_pkt
             k = n - A.off_lower;
             rot = pb;
         }
-        if (k != 0xFFFFFFFFu) put(k, cmul(cscale(v[m], A.amp_scale), rot));
+        if (k != 0xFFFFFFFFu) put(k, cmul(v[m], rot));
         pa = cmul(pa, s64);
         pb = cmul(pb, s64);
     }
