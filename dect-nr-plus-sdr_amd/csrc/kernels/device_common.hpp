@@ -2,6 +2,8 @@
 // (radix 4/2/3, autosort, one workgroup per transform), block reductions.
 #pragma once
 
+#include "experiments.hpp"
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -432,12 +434,9 @@ constexpr uint32_t WFFT_XB = 1024 + 64;
 
 // exchange slot of element i: padded i + i / 16 (default: conflict-free b64 writes of pass 1 and 2,
 // 2-way ds_read_b64 conflicts in passes 2 and 3 -- slots 0 and 32 of a half-wave share a bank) or, with
-// DNRP_WFFT_SWZ, i ^ ((i >> 4) & 15): conflict-free for all four exchange patterns, but the XOR makes
+// XS_WFFT_SWZ (experiments.hpp), i ^ ((i >> 4) & 15): conflict-free for all four exchange patterns, but the XOR makes
 // the slot lane-dependent per instruction (address VALU instead of immediate offsets)
-#ifndef DNRP_WFFT_SWZ
-#define DNRP_WFFT_SWZ 0
-#endif
-__device__ __forceinline__ uint32_t wfft_pad(uint32_t i) { return DNRP_WFFT_SWZ ? (i ^ ((i >> 4) & 15u)) : i + (i >> 4); }
+__device__ __forceinline__ uint32_t wfft_pad(uint32_t i) { return experiment(XS_WFFT_SWZ) ? (i ^ ((i >> 4) & 15u)) : i + (i >> 4); }
 
 template <int SIGN>
 __device__ __forceinline__ float2 wfft_tw(const float2* tw, uint32_t e) {

@@ -579,9 +579,6 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
 #ifndef DNRP_RX_SPW
 #define DNRP_RX_SPW 2
 #endif
-#ifndef DNRP_FE_PREFETCH
-#define DNRP_FE_PREFETCH 0  // A/B on MI355X, per 16384-slot PDC launch: 19.08 / 19.23 ms with, 18.77 / 18.71 without
-#endif
 template <int SPW>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) rx_fft_wave_ct_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -627,7 +624,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) rx
         // the symbol, so no wait of this symbol is on them; the next symbol's span loads then hit L2 /
         // the Infinity Cache instead of HBM
         float pf0 = 0.f, pf1 = 0.f;
-        if (DNRP_FE_PREFETCH && i + 1 < SPW && li + 1 < A.sym_count) {
+        if (experiment(XS_FE_PREFETCH) && i + 1 < SPW && li + 1 < A.sym_count) {
             const rx_span_t sn = rx_span<LR, MR, HLR>(A, A.sym_list ? A.sym_list[li + 1] : l + 1);
             const int64_t lo = max<int64_t>(sn.in0, q_lo), hi = min<int64_t>(sn.in0 + sn.n_in, q_hi) - 1;
             if (hi >= lo) {

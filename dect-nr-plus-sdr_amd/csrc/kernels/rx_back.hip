@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
         if (tid < units) A.llr[size_t(row) * A.llr_stride + tid] = static_cast<int16_t>(zfi[tid].x);
         return;
     }
-    constexpr bool wave_mf = SM && DNRP_MMSE_MFMA && NT == 4;
+    constexpr bool wave_mf = SM && experiment(XS_MMSE_MFMA) && NT == 4;
     if (!wave_mf && tid >= units) return;
     const uint8_t* __restrict__ seq = A.is_pdc ? A.pdc_seq[row] : A.pcc_seq;
     int16_t* __restrict__ llr = A.llr + size_t(row) * A.llr_stride;
@@ -310,7 +310,7 @@ hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st) {
 
 hipError_t launch_rx_cells_sm(const rx_cells_args& a, uint32_t n, hipStream_t st) {
     size_t lds = cell_lds_bytes(a.N_RX, a.NT, a.n_drs, a.wcap[0], a.wcap[1]);
-    if (DNRP_MMSE_MFMA && a.NT == 4) lds = (lds + 15) / 16 * 16 + CELL_THREADS / 64 * a.N_RX * 4 * 24 * sizeof(float2);
+    if (experiment(XS_MMSE_MFMA) && a.NT == 4) lds = (lds + 15) / 16 * 16 + CELL_THREADS / 64 * a.N_RX * 4 * 24 * sizeof(float2);
     if (lds > 160 * 1024 || a.n_pkt != n) return hipErrorInvalidValue;
     const dim3 g((n + 7) / 8 * 8 * a.n_epochs), b(CELL_THREADS);
     // the demapper width compiled in for 64- and 256-QAM

@@ -10,9 +10,6 @@
 
 namespace dnrp::dev {
 
-#ifndef DNRP_MMSE_MFMA
-#define DNRP_MMSE_MFMA 0  // 4-stream MMSE Gram on v_mfma_f32_4x4x1_16b_f32 (A/B in DESIGN.md)
-#endif
 #ifndef DNRP_CELLS_CH
 #define DNRP_CELLS_CH 3  // SFBC interpolation taps per chunk (eq_compute): 3 keeps rx_cells<4, 4> at 121 VGPRs (4: 131, one workgroup per CU)
 #endif
@@ -405,7 +402,7 @@ __device__ __forceinline__ void emit_symw(float2 x, uint32_t base, uint32_t N_bp
     }
 }
 
-// Experiment (DNRP_MMSE_MFMA): the 4x4 Gram H^H H of the wave's 64 cells on the matrix pipe. The
+// Experiment (XS_MMSE_MFMA): the 4x4 Gram H^H H of the wave's 64 cells on the matrix pipe. The
 // 16-block 4x4x1 MFMA takes lane 4b+i's A/B value as row/column i of block b and returns G_b[i][j]
 // in lane 4b+j, component i. Per group of 16 cells: the group's H goes through the wave's LDS
 // scratch [NRX][4] rows of 16 cells so lane 4b+i holds H[a][i] of cell b, 4*NRX MFMAs (re: hr hr^T
@@ -500,7 +497,7 @@ __device__ __forceinline__ void eq_mmse(const rx_cells_args& A, const cell_seg* 
     // G = H^H H + nv I (diagonal gd, strictly lower go[i][j] = sum_a conj(h_ai) h_aj), z = H^H y
     float gd[NT];
     float2 go[NT][NT], zz[NT];
-    constexpr bool mf = DNRP_MMSE_MFMA && NT == 4;
+    constexpr bool mf = experiment(XS_MMSE_MFMA) && NT == 4;
     if constexpr (mf) gram_mfma<NRX>(h, scr, nv, gd, go);
 #pragma unroll
     for (int i = 0; i < NT; ++i) {

@@ -44,9 +44,6 @@ __device__ __forceinline__ float cover_sign(uint32_t q) { return ((cover_neg_mas
 // and the index bit gathers) instead of the 256-entry table (one read, ~3 conflict cycles). A/B on
 // MI355X: TX 19.25-19.48 vs 18.83-18.98 ms per 16384-slot chunk -- the gathers' VALU (+5 % per
 // wave) cost more than the conflicts; off by default
-#ifndef DNRP_TX_QLEV
-#define DNRP_TX_QLEV 0
-#endif
 
 constexpr uint32_t TX_THREADS = 256;     // block-FFT path workgroup
 constexpr uint32_t TX_WAVE_MAX = 512;    // wave path: one wavefront per symbol slot, 64 (K + 1) threads
@@ -504,7 +501,7 @@ struct txs_wave {
         if (Q8) {
             const uint32_t v = sb[(s - ab) & (SBW - 1)];
             if constexpr (experiment(XS_TX_NO_QTAB)) return make_float2(static_cast<float>(v), -static_cast<float>(v));
-            if constexpr (DNRP_TX_QLEV) {
+            if constexpr (experiment(XS_TX_QLEV)) {
                 // 256-QAM is separable (36.211 7.1.5: I from bits 0, 2, 4, 6, Q from bits 1, 3, 5, 7, the
                 // same level function): two reads of the 16-level table, conflict-free (16 words on 16
                 // banks), instead of one 8-B read of the 256-entry table at a data-random index
@@ -671,7 +668,7 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
     // wave index made provably uniform: everything derived from it (packet, segment, loop bounds,
     // pointers) stays in SGPRs and the piece loop is not divergent control flow
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    if constexpr (Q8 && DNRP_TX_QLEV) {
+    if constexpr (Q8 && experiment(XS_TX_QLEV)) {
         // level i = re of the table entry whose I bits (0, 2, 4, 6) give index i and Q bits are 0
         if (threadIdx.x < 16) {
             const uint32_t i = threadIdx.x;
