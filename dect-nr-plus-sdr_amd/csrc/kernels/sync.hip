@@ -260,7 +260,10 @@ __global__ void __launch_bounds__(64 * WPG) sync_steps_wave_kernel(sync_args A) 
 // resampled, so every wave keeps its own loads in flight instead of waiting on a staging pass.
 // Per wave LDS: the chunk's input window (carry W - M + M * 64) and a 1024-sample output ring
 // holding the pattern lookback; no workgroup barrier anywhere.
-constexpr uint32_t SS_RING = 1024;
+#ifndef DNRP_SS_RING
+#define DNRP_SS_RING 1024  // power of two >= 64 * 9 + step + pattern + 9 (host-checked)
+#endif
+constexpr uint32_t SS_RING = DNRP_SS_RING;
 constexpr uint32_t SS_WPG = 4;
 
 template <int LR, int MR, int HLR>
