@@ -458,12 +458,14 @@ __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, f
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            if (!corr) u[j] = make_float2(0.f, 0.f);
             pw = fmaf(v[j].x, v[j].x, fmaf(v[j].y, v[j].y, pw));
             cc.x = fmaf(u[j].x, v[j].x, fmaf(u[j].y, v[j].y, cc.x));
             cc.y = fmaf(u[j].y, v[j].x, fmaf(-u[j].x, v[j].y, cc.y));
         }
     }
+    // a step before the first full lag has no correlation term: dropped once here, not per sample
+    // (the sums of zero products were +0, as the select gives)
+    if (!corr) cc = make_float2(0.f, 0.f);
     if (!live) {
         pw = 0.f;
         cc = make_float2(0.f, 0.f);
