@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace dnrp::dev {
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
@@ -515,6 +517,76 @@ __device__ void fft_r4_inplace(float2* x_, const float2* tw, uint32_t log2N) {
         }
         __syncthreads();
     }
+}
+
+// fft_r4_inplace<SIGN, true> for a compile-time size (sync_fine's 4096 points): the same butterflies
+// and twiddles in the same order, so bit-identical results. The passes unrolled, so each butterfly's
+// four padded slots are one base address plus immediate offsets (Q constant; for Q = 16 the second
+// half of a 64-slot group lies one pad slot further), and two butterflies per thread and trip (j and
+// j + nt) with both butterflies' slot and twiddle loads issued before either is computed: one memory
+// latency per pass instead of two at NB = 2 nt. Twiddles through a buffer resource (32-bit offsets).
+template <uint32_t S, uint32_t LOG2N, class F>
+__device__ __forceinline__ void r4_passes(F& pass) {  // pass(integral_constant<S>) for S = 0, 2, .. < LOG2N
+    if constexpr (S < LOG2N) {
+        pass(std::integral_constant<uint32_t, S>{});
+        r4_passes<S + 2, LOG2N>(pass);
+    }
+}
+
+template <int SIGN, uint32_t LOG2N>
+__device__ void fft_r4_inplace_ct(float2* x_, const float2* tw) {
+    constexpr uint32_t NB = 1u << (LOG2N - 2);
+    const uint32_t nt = blockDim.x;
+    const __amdgpu_buffer_rsrc_t twr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(tw), 0, static_cast<int>((1u << LOG2N) * 8u), 0x00020000);
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    auto pass = [&](auto sc) {
+        constexpr uint32_t s = decltype(sc)::value, Q = 1u << s, tsh = LOG2N - s - 2;
+        static_assert(Q >= 32 || 4 * Q <= 32 || Q == 16, "pad offsets");
+        // padded slot of i0 + r Q relative to r4pad(i0), i0 = 4 Q m + k with k < Q
+        auto off = [](int r) -> uint32_t {
+            if constexpr (Q >= 32) return r * Q + r * (Q / 32);
+            else if constexpr (Q == 16) return r * Q + (r >= 2 ? 1u : 0u);
+            else return r * Q;
+        };
+        for (uint32_t j0 = threadIdx.x; j0 < NB; j0 += 2 * nt) {
+            const bool two = j0 + nt < NB;
+            float2 a[2][4], w[2][3];
+            float2* p[2];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const uint32_t j = b && two ? j0 + nt : j0;
+                const uint32_t k = j & (Q - 1u);
+                p[b] = x_ + r4pad(((j >> s) << (s + 2)) + k);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) a[b][r] = p[b][off(r)];
+                if constexpr (s > 0) {
+                    const uint32_t e8 = (k << tsh) * 8u;
+#pragma unroll
+                    for (int r = 0; r < 3; ++r) {
+                        const u2 v = __builtin_amdgcn_raw_buffer_load_b64(twr, (r + 1) * e8, 0, 0);
+                        w[b][r] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+                    }
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                if constexpr (s > 0) {
+#pragma unroll
+                    for (int r = 0; r < 3; ++r) a[b][r + 1] = cmul(a[b][r + 1], SIGN > 0 ? cconj(w[b][r]) : w[b][r]);
+                }
+                dft4<SIGN>(a[b][0], a[b][1], a[b][2], a[b][3]);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) p[0][off(r)] = a[0][r];
+            if (two) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) p[1][off(r)] = a[1][r];
+            }
+        }
+        __syncthreads();
+    };
+    r4_passes<0, LOG2N>(pass);
 }
 
 // base-4 digit reversal of the log2N / 2 digits of i (fft_r4_inplace's input position)

@@ -1345,7 +1345,10 @@ __global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args 
     auto fft = [&](auto sign, float2* a, float2* b) -> const float2* {
         constexpr int SG = decltype(sign)::value;
         if (ip) {
-            fft_r4_inplace<SG, true>(a, A.tw_fft, A.log2_fft);
+            if (A.log2_fft == 12)  // C3 / C4
+                fft_r4_inplace_ct<SG, 12>(a, A.tw_fft);
+            else
+                fft_r4_inplace<SG, true>(a, A.tw_fft, A.log2_fft);
             return a;
         }
         return fft_pow2<SG>(a, b, A.tw_fft, A.log2_fft);
@@ -1382,8 +1385,8 @@ __global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args 
     const float2* S = fft(std::integral_constant<int, -1>{}, xb, yb);
     for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) Sb[i] = S[ox(i)];
     __syncthreads();  // S's buffer is overwritten below; each thread re-reads only its own Sb[i]
-    float xm[4];
-    uint32_t xi[4];
+    // per template: its peak metric and index in the header's upper half (s_val / s_idx 8 + k; the
+    // wave maxima use 0..7), written by thread 0, the only reader: no registers held across the FFTs
     for (uint32_t k = 0; k < A.n_templates; ++k) {
         const float2* T = A.tmpl_f + static_cast<size_t>(k) * nf;
         for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) xb[ix(i)] = cmul(Sb[i], T[i]);
@@ -1416,11 +1419,15 @@ __global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args 
                 bv = s_val[v];
                 bi = s_idx[v];
             }
-        xm[k] = sqrtf(bv);
-        xi[k] = bi;
+        if (threadIdx.x == 0) {
+            s_val[8 + k] = sqrtf(bv);
+            s_idx[8 + k] = bi;
+        }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
+        const float* xm = s_val + 8;
+        const uint32_t* xi = s_idx + 8;
         uint32_t kbest = 0;
         float msum_max = 0.f;
         for (uint32_t k = 0; k < A.n_templates; ++k)
