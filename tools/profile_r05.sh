@@ -4,5 +4,5 @@
 # -> gpurun_out/prof_r05_<tag>/
 set -e
 bash tools/profile_r03.sh r05_c4 --batch 16384
-bash tools/profile_r03.sh r05_c4sm --workload C4SM
+bash tools/profile_r03.sh r05_c4sm --workload C4SM --batch 8192
 DNRP_RX_FUSED=1 bash tools/profile_r03.sh r05_fused --batch 16384

@@ -14,5 +14,5 @@ done
 # slots per launch of each summary (bench.py _pmc_chunk)
 cat > $d/pmc_meta.json <<'J'
 {"traffic.json": 16384, "valu.json": 16384, "traffic_fused.json": 16384, "valu_fused.json": 16384,
- "traffic_c4sm.json": 4096, "valu_c4sm.json": 4096}
+ "traffic_c4sm.json": 8192, "valu_c4sm.json": 8192}
 J
