@@ -106,6 +106,21 @@ __device__ __forceinline__ void rx_fft_bins(const rx_front_args& A, const rx_pkt
     float2 pa = cscale(phasor(S.sto_inc * static_cast<double>(lane)), A.amp_scale);
     float2 pb = cscale(phasor(S.sto_inc * (static_cast<double>(lane) - static_cast<double>(A.off_lower) -
                                            static_cast<double>(N / 2))), A.amp_scale);
+    if (N == 896 && A.off_lower == 576) {  // beta = 16 at N_b_DFT_os = 1024 (C3 / C4): the bin map is static
+        // rows m <= 6 lower half (k = n + 448), row 7 only n = 448 (k = 896), row 8 empty, rows >= 9
+        // upper half (k = n - 576): no per-bin range tests or phasor selects, and pa stepped only
+        // while it is used; pb still stepped from row 0, so every product is the generic path's
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const uint32_t n = lane + 64 * m;
+            if (m <= 6) put(n + 448, cmul(v[m], pa));
+            else if (m == 7 && lane == 0) put(896u, cmul(v[m], pa));
+            else if (m >= 9) put(n - 576, cmul(v[m], pb));
+            if (m < 7) pa = cmul(pa, s64);
+            if (m < 15) pb = cmul(pb, s64);
+        }
+        return;
+    }
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         const uint32_t n = lane + 64 * m;
