@@ -877,9 +877,12 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
         // through a DECT-rate scratch (tx.hip tx_big_sym_kernel), e.g. u < u_max at b_max = 16
         const uint64_t total = uint64_t(t->dm.STF_CP) + uint64_t(t->q.N_DF_symb) * t->dm.CP + uint64_t(t->q.N_DF_symb + 1) * t->dm.Nd;
         a.big_len = static_cast<uint32_t>((total + 3) / 4 * 4);
-        // the scratch is capped at 4 GiB: larger batches run in passes of big_batch packets (tx.hip)
+        // the scratch is capped at 4 GiB: larger batches run in passes of big_batch packets (tx.hip);
+        // DNRP_TX_BIG_CAP (bytes, read per call) lowers the cap so a test can force several passes
         const uint64_t row_bytes = sizeof(float) * 2 * uint64_t(a.big_len) * t->tm.N_TX;
-        a.big_batch = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(n, (uint64_t(4) << 30) / row_bytes)));
+        uint64_t cap = uint64_t(4) << 30;
+        if (const char* e = std::getenv("DNRP_TX_BIG_CAP")) cap = std::min<uint64_t>(cap, std::strtoull(e, nullptr, 10));
+        a.big_batch = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(n, cap / row_bytes)));
         if (!ctx->tx_big.ensure(row_bytes * a.big_batch)) return DNRP_ENOMEM;
         HIPCHK(ctx->tx_big.wait_idle(st));
         a.big = ctx->tx_big.as<float2>();
@@ -1084,8 +1087,10 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
 int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const float* iq_in, uint32_t n_windows,
                       uint32_t S_in, int16_t* pdc_llr, uint32_t llr_stride, dnrp_pdc_report* rep, void* stream) {
     if (!ctx || (m > 0 && (!req || !iq_in || !pdc_llr))) return DNRP_EINVAL;
-    if (!ctx->rx_valid) return DNRP_ESTATE;
+    // no packet continues with its PDC: nothing to enqueue, whatever the PCC call before (an empty
+    // chunk enqueues no job either, worker_sync.cpp:170-190)
     if (m == 0) return DNRP_OK;
+    if (!ctx->rx_valid) return DNRP_ESTATE;
     // the PDC symbols are read from the PCC call's windows (the state it kept points into them)
     if (iq_in != ctx->rx_iq || n_windows != ctx->rx_n_windows) return DNRP_ESTATE;
     if (m > ctx->rx_n || S_in != ctx->rx_S_in) return DNRP_EINVAL;

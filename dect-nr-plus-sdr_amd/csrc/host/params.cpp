@@ -3,6 +3,7 @@
 // Every value comes from csrc/params.hpp, the constants the host code and kernels actually use;
 // the names are the reference's own macro / field names so tests/test_oracle_pins.py can compare
 // them one by one with the values the reference headers compile to.
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -10,6 +11,7 @@
 #include "../params.hpp"
 #include "dnrp.h"
 #include "geometry.hpp"
+#include "kernels.hpp"
 
 namespace {
 
@@ -180,6 +182,18 @@ int dnrp_query_table(const char* name, const uint32_t* arg, uint32_t n_arg, floa
         } else if (n == "W_codebooks") {  // (N_TS, N_TX)
             if (n_arg != 2) return DNRP_EINVAL;
             v.push_back(static_cast<float>(geo::W_codebooks(a(0), a(1))));
+        } else if (n == "cells_lds_bytes") {  // (u_max, b_max, b, N_RX, N_eff_TX): rx_cells_kernel's LDS
+            // staging for the geometry (ctx.cpp launch_back: above 160 KiB -> DNRP_EUNSUPPORTED); the
+            // weight-table slots as get_rx1 sizes them from the Wiener LUTs of both modes
+            if (n_arg != 5 || a(2) == 0 || a(2) > a(1) || a(4) == 0 || a(4) > 8) return DNRP_EINVAL;
+            const uint32_t Nsv = a(4) <= 2 ? 5 : 10;
+            uint32_t wcap[2] = {};
+            for (uint32_t mode = 0; mode < 2; ++mode)
+                for (uint32_t p = 0; p < 3; ++p) {
+                    const auto L = geo::build_lut(mode ? Nsv : 0, a(2), a(1), a(0), p);
+                    wcap[mode] = std::max(wcap[mode], (static_cast<uint32_t>(L.weights.size()) + 3u) & ~3u);
+                }
+            v.push_back(static_cast<float>(dnrp::dev::cell_lds_bytes(a(3), a(4), 56 * a(2) / 4, wcap[0], wcap[1])));
         } else if (n == "stf") {  // (b, N_eff_TX): transmit-stream vector [N_b_OCC + 1] re/im, scale 1
             if (n_arg != 2 || !(a(0) == 1 || a(0) == 2 || a(0) == 4 || a(0) == 8 || a(0) == 12 || a(0) == 16) ||
                 !(a(1) == 1 || a(1) == 2 || a(1) == 4 || a(1) == 8))

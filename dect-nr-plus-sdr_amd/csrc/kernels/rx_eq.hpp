@@ -569,7 +569,7 @@ __device__ __forceinline__ void eq_mmse(const rx_cells_args& A, const cell_seg* 
         }
         const float beta = 1.f - nv * ginv;
         const uint32_t sw = static_cast<uint32_t>((be << ((b_first & 7u) + s * N_bps)) >> 32);
-        if (act) emit_symw(cscale(x, __builtin_amdgcn_rcpf(beta)), b_first + s * N_bps, N_bps, sw, llr);
+        if (act) emit_symw(cscale(x, 1.0f / beta), b_first + s * N_bps, N_bps, sw, llr);
     }
 }
 

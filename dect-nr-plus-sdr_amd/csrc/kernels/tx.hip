@@ -1143,7 +1143,12 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
         const size_t lds = (2 * size_t(a.plan.N) + 256 + 98 + 8) * sizeof(float2);
         if (lds > 160 * 1024 || a.big_batch == 0) return hipErrorInvalidValue;
         // passes of big_batch packets through the scratch (the host caps its size), each pass with
-        // the packet-indexed arguments offset to its first packet
+        // the packet-indexed arguments offset to its first packet; the largest pass's grids checked
+        // before the first launch, so a call either runs every pass or none
+        const uint64_t np_max = min(a.big_batch, n);
+        if (uint64_t((a.S + 255) / 256) * np_max * a.N_TX > 0x7FFFFFFFull ||
+            np_max * a.N_TX * (a.N_DF + 1) > 0x7FFFFFFFull)
+            return hipErrorInvalidValue;
         for (uint32_t p0 = 0; p0 < n; p0 += a.big_batch) {
             const uint32_t np = min(a.big_batch, n - p0);
             tx_args b = a;
@@ -1152,7 +1157,6 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
             b.pdc_d = a.pdc_d + size_t(p0) * a.pdc_stride;
             b.out = a.out + size_t(p0) * a.N_TX * a.S * 2;
             const uint64_t gx = uint64_t((a.S + 255) / 256) * np * a.N_TX;
-            if (gx > 0x7FFFFFFFull) return hipErrorInvalidValue;
             hipLaunchKernelGGL(tx_big_sym_kernel, dim3(np * a.N_TX * (a.N_DF + 1)), dim3(TX_BIG_THREADS), lds, st, b);
             hipLaunchKernelGGL(tx_big_resample_kernel, dim3(static_cast<uint32_t>(gx)), dim3(256), 0, st, b, total);
         }

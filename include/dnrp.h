@@ -375,7 +375,9 @@ const char* dnrp_param_name(uint32_t index);
  *   "stf" (b, N_eff_TX)          stf_t transmit-stream vector [N_b_OCC + 1] re/im, scale 1 (stf.cpp:185-285)
  *   "drs_values" (b, t)          the N_b_OCC/4 DRS values of transmit stream t (drs.cpp:227-254)
  *   "txdiv_pairs" (N_TS)         Y_i_t::index_N_TS_x rows A0 B0 A1 B1 ... (transmit_diversity_precoding.cpp:48-75)
- *   "stf_cover_sequence" ()      stf_t::cover_sequence (stf.hpp:146-151) */
+ *   "stf_cover_sequence" ()      stf_t::cover_sequence (stf.hpp:146-151)
+ *   "cells_lds_bytes" (u_max, b_max, b, N_RX, N_eff_TX)   LDS bytes of the PDC equaliser's staging for
+ *                                the geometry; above 160 KiB dnrp_rx_*_batch return DNRP_EUNSUPPORTED */
 int dnrp_query_table(const char* name, const uint32_t* arg, uint32_t n_arg, float* out, uint32_t cap);
 
 /* Kernel timing (only when the environment has DNRP_TIMING=1 at dnrp_ctx_create): HIP events

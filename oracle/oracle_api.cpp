@@ -347,8 +347,9 @@ int oracle_rx(const uint32_t* cfg, const uint32_t* psdef, uint32_t N_RX, const f
         meta[11] = o.snr_pdc_db;
         meta[12] = static_cast<float>(o.mimo_N_TS_other);
         // 0xFFFFFFFF (no recommendation) as -1: exact in a float
-        meta[13] = o.mimo_idx == 0xFFFFFFFFu ? -1.f : static_cast<float>(o.mimo_idx);
-        meta[14] = o.mimo_idx_reciprocal == 0xFFFFFFFFu ? -1.f : static_cast<float>(o.mimo_idx_reciprocal);
+        // MIMO_REF_UNDEFINED (the reference asserts / throws) -> -2
+        meta[13] = o.mimo_idx == MIMO_REF_UNDEFINED ? -2.f : static_cast<float>(o.mimo_idx);
+        meta[14] = o.mimo_idx_reciprocal == MIMO_REF_UNDEFINED ? -2.f : static_cast<float>(o.mimo_idx_reciprocal);
         return 0;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "oracle_rx: %s\n", e.what());

@@ -605,10 +605,12 @@ struct rx_state_t {
         const uint32_t NTS = N_eff_TX;
         // stage[rx][tx][c]: float, as the reference's cf_t stages
         auto pick = [&](uint32_t N_TX_virt, uint32_t N_RX_virt, auto&& H) -> uint32_t {
-            // no single-stream codebook for 8 antennas: W_t::get_W(1, 8) is the SISO entry and the
-            // reference's W_mat_single.at(tx) throws for tx >= 1 (estimator_mimo.cpp:160-200); the
-            // defined counterpart here (and in the product) is "no recommendation", 0xFFFFFFFF
-            if (N_TX_virt != 2 && N_TX_virt != 4) return 0xFFFFFFFFu;
+            // no single-stream codebook for 8 antennas: estimator_mimo.cpp:180 asserts and
+            // W_mat_single.at(tx) throws for tx >= 1 (estimator_mimo.cpp:160-200) -- the reference
+            // defines no result. The oracle flags the case (MIMO_REF_UNDEFINED) instead of inventing
+            // one; the product's own defined answer ("no recommendation", 0xFFFFFFFF) is tested as a
+            // documented divergence, not as parity (tests/test_gpu_parity.py _check_rx)
+            if (N_TX_virt != 2 && N_TX_virt != 4) return MIMO_REF_UNDEFINED;
             static const uint32_t A_nonzero[9] = {0, 0, 2, 0, 12, 0, 0, 0, 0};  // N_TS_N_TX_codebook_index_nonzero[1][.]
             const uint32_t n_cb = W_codebook_max(1, N_TX_virt) + 1;
             float power_outer = -1.0e6f;

@@ -9,6 +9,9 @@
 
 namespace orc {
 
+// mimo_report_t index where the reference defines no result (estimator_mimo.cpp:180 asserts)
+constexpr uint32_t MIMO_REF_UNDEFINED = 0xFFFFFFFEu;
+
 struct cfg_t {  // worker_pool_config_t subset: radio device class maxima + resampling
     uint32_t u_max = 8, b_max = 16, os_min = 1, L = 10, M = 9;
     bool chestim_mode_lr = true;  // phy.json chestim_mode_lr_default
@@ -37,7 +40,7 @@ struct rx_out_t {
     std::vector<float> pcc_llr_f, pdc_llr_f; // pre-quantisation values, descrambled
     std::vector<float> rms;
     float cfo_fine_rad = 0, sto_fractional = 0, snr_pcc_db = 0, snr_pdc_db = 0;
-    uint32_t mimo_N_TS_other = 0, mimo_idx = 0, mimo_idx_reciprocal = 0;  // mimo_report_t
+    uint32_t mimo_N_TS_other = 0, mimo_idx = 0, mimo_idx_reciprocal = 0;  // mimo_report_t (MIMO_REF_UNDEFINED: none)
 };
 
 struct dims_t {

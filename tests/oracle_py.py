@@ -11,6 +11,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # ORACLE_LIB: another build of the same sources (bench.py's cpu_baseline builds one -march=native)
+# mimo_report_t index where the reference defines no result (oracle_dsp.hpp MIMO_REF_UNDEFINED)
+MIMO_REF_UNDEFINED = 0xFFFFFFFE
 LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(ROOT, "oracle", "liboracle.so")
 
 _lib = None

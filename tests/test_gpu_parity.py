@@ -3,7 +3,8 @@
 Tolerances:
   * TX IQ: relative L2 error per packet and antenna <= 1e-4 (float IQ), GI/tail exactly zero.
   * RX: int16 LLRs |delta| <= 1 LSB against the double-precision oracle (pre-quantisation float
-    values agree to ~1e-5 relative; the +-1 covers rounding-boundary flips), SNR reports within
+    values agree to ~1e-5 relative; the +-1 covers rounding-boundary flips), with |mean delta| <= 0.01
+    LSB and at most 1 % of the LLRs of a packet differing (tests/llr_gate.py), SNR reports within
     0.05 dB, STO within 1e-3 samples, RMS within 1e-4 relative, MIMO report exact.
 
 Configurations (CASES): the bench configurations C2/C3/C4 plus every mode the reference RX
@@ -18,6 +19,7 @@ subslot packets (PacketLengthType 0).
 import numpy as np
 import pytest
 
+import llr_gate
 import oracle_py as O
 import phy_fixtures as F
 
@@ -102,6 +104,16 @@ def test_tx_parity_matrix_blocks(name, monkeypatch):
     test_tx_parity(name)
 
 
+@pytest.mark.parametrize("name", ["os2_C4", "u2_in_u8b16", "u1_in_u8b16"])
+def test_tx_big_passes(name, monkeypatch):
+    """N_b_DFT_os > 1024 (tx_big_sym_kernel + tx_big_resample_kernel through the DECT-rate scratch):
+    DNRP_TX_BIG_CAP=1 shrinks the scratch cap so every packet runs in a pass of its own (big_batch = 1
+    < n), with the packet-indexed arguments offset per pass -- first, middle and last packet at
+    parity with the oracle."""
+    monkeypatch.setenv("DNRP_TX_BIG_CAP", "1")
+    test_tx_parity(name)
+
+
 @pytest.mark.parametrize("name,cb", [("tm5_u2b4", 3), ("tm2_sm2", 1), ("C4", 0)])
 def test_tx_optimal_scaling_dac(name, cb):
     """tx_meta_t::optimal_scaling_DAC (tx.cpp:582-592): W_t::scaling_factor_optimal_DAC instead of
@@ -156,10 +168,9 @@ def _oracle_rx(ocf, ops, win, rep, nid, pt):
 
 
 def _check_rx(name, g_pcc, g_pdc, r1, r2, r):
-    d_pcc = np.abs(g_pcc.astype(np.int32) - r["pcc_llr"].astype(np.int32))
-    d_pdc = np.abs(g_pdc[: len(r["pdc_llr"])].astype(np.int32) - r["pdc_llr"].astype(np.int32))
-    assert d_pcc.max() <= 1, (name, d_pcc.max(), np.argmax(d_pcc))
-    assert d_pdc.max() <= 1, (name, d_pdc.max(), np.argmax(d_pdc), np.mean(d_pdc))
+    # max |delta| <= 1, |mean delta| and the fraction of nonzero deltas bounded (tests/llr_gate.py)
+    llr_gate.check((name, "pcc"), g_pcc, r["pcc_llr"])
+    llr_gate.check((name, "pdc"), g_pdc[: len(r["pdc_llr"])], r["pdc_llr"])
     if r1 is not None:
         assert abs(r1.snr_dB - r["snr_pcc"]) < 0.05, (name, r1.snr_dB, r["snr_pcc"])
         assert abs(r1.sto_fractional - r["sto"]) < 1e-3, (name, r1.sto_fractional, r["sto"])
@@ -167,9 +178,13 @@ def _check_rx(name, g_pcc, g_pdc, r1, r2, r):
             assert abs(r1.rms[a] - r["rms"][a]) <= 1e-4 * max(1.0, r["rms"][a]), (name, a)
     if r2 is not None:
         assert abs(r2.snr_dB - r["snr_pdc"]) < 0.05, (name, r2.snr_dB, r["snr_pdc"])
-        # mimo_report_t (estimator_mimo.cpp): codebook recommendations exact
-        assert (r2.mimo_N_TS_other, r2.tm_3_7_beamforming_idx, r2.tm_3_7_beamforming_reciprocal_idx) == \
-            (r["mimo_N_TS_other"], r["mimo_idx"], r["mimo_idx_reciprocal"]), name
+        # mimo_report_t (estimator_mimo.cpp): codebook recommendations exact; where the reference has
+        # no result (8 antennas: estimator_mimo.cpp:180 asserts, the oracle flags MIMO_REF_UNDEFINED)
+        # the product's defined "no recommendation" 0xFFFFFFFF is checked as a documented divergence
+        assert r2.mimo_N_TS_other == r["mimo_N_TS_other"], name
+        for g, o in ((r2.tm_3_7_beamforming_idx, r["mimo_idx"]),
+                     (r2.tm_3_7_beamforming_reciprocal_idx, r["mimo_idx_reciprocal"])):
+            assert g == (0xFFFFFFFF if o == O.MIMO_REF_UNDEFINED else o), (name, g, o)
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
@@ -251,17 +266,21 @@ def test_rx_parity_fused_stride(name, stride, monkeypatch):
 def test_rx_largest_cells_geometry(monkeypatch):
     """8 RX antennas x 4 transmit streams at b = 16 (TM5 into an N_TX_max = 8 context): the largest
     N_RX / NT / b of the cells kernel's LDS staging (pilot rows of 8 x 4 streams, both weight tables).
-    Parity against the oracle where it fits one CU's LDS, else DNRP_EUNSUPPORTED before any launch
-    (never a device error)."""
+    The host states the staging size ("cells_lds_bytes"); the one outcome it implies is asserted:
+    parity against the oracle when it fits one CU's 160 KiB, else DNRP_EUNSUPPORTED before any
+    launch (never a device error)."""
     import dnrp
     name = "tm5_u8b16_rx8"
     spec = ((8, 16, 1, 1, 5, 8), (8, 16, 8, 1, 10, 9), 1, (30.0,), 0)
     monkeypatch.setitem(CASES, name, spec)
     monkeypatch.setitem(TX_CASES, name, spec)
-    try:
+    lds = int(dnrp.query_table("cells_lds_bytes", 8, 16, 16, 8, 4)[0])
+    if lds <= 160 * 1024:
         _rx_parity(name)
-    except dnrp.DnrpError as e:
-        assert e.code == -3, str(e)  # DNRP_EUNSUPPORTED
+    else:
+        with pytest.raises(dnrp.DnrpError) as e:
+            _rx_parity(name)
+        assert e.value.code == -3, str(e.value)  # DNRP_EUNSUPPORTED
 
 
 def test_rx_fused_growing_batch(monkeypatch):
@@ -370,6 +389,41 @@ def test_rx_pdc_request_errors():
     with pytest.raises(dnrp.DnrpError) as e:
         phy.rx_pdc_batch([dnrp.PdcReq(ps, 0, 100, 1)], other, pdc_llr)
     assert e.value.code == -7
+
+
+def test_rx_empty_chunk_then_parity():
+    """A chunk of noise only: sync finds no packet, the PCC batch is empty (n = 0) and so is the PDC
+    batch (m = 0) -- both return OK (no job without a packet, worker_sync.cpp:170-190), also when
+    the empty PDC batch follows an empty PCC batch; then a normal batch in the same context is at
+    parity."""
+    import dnrp
+    rng = np.random.default_rng(31)
+    phy, ps, ops, ocf = _ctx("C2")
+    sz = phy.packet_sizes(ps)
+    S = sz["N_samples_packet_os_rs"]
+    dev = torch.device("cuda:0")
+    noise = (rng.normal(size=(4, 1, S)) + 1j * rng.normal(size=(4, 1, S))).astype(np.complex64) * 0.01
+    iq0 = torch.from_numpy(noise.view(np.float32).reshape(4, 1, S, 2)).to(dev)
+    sc = dnrp.SyncCfg(1, 1, 1, S * 7 // 8, 1)
+    res, cnt = phy.rx_sync_batch(sc, iq0, 4, S, S, S)
+    phy.sync()
+    assert int(np.asarray(cnt[:4]).sum()) == 0
+    reps = dnrp.found_reports(res, cnt[:4])
+    assert len(reps) == 0
+    pcc_llr = torch.zeros((4, 196), dtype=torch.int16, device=dev)
+    pdc_llr = torch.zeros((4, sz["G"]), dtype=torch.int16, device=dev)
+    for _ in range(2):
+        phy.rx_pcc_batch(reps, iq0, pcc_llr)
+        phy.rx_pdc_batch([], iq0, pdc_llr)
+    phy.sync()
+    windows, reports, nids, types, _, _ = _rx_windows(rng, "C2", phy, ps, ops, ocf, (20.0, 30.0))
+    iq = torch.from_numpy(np.stack(windows).view(np.float32).reshape(2, 1, S, 2)).to(dev)
+    phy.rx_pcc_batch(reports, iq, pcc_llr)
+    phy.rx_pdc_batch([dnrp.PdcReq(ps, i, nids[i], types[i]) for i in range(2)], iq, pdc_llr)
+    phy.sync()
+    for i in range(2):
+        r = _oracle_rx(ocf, ops, windows[i], reports[i], nids[i], types[i])
+        _check_rx(("after_empty", i), pcc_llr[i].cpu().numpy(), pdc_llr[i].cpu().numpy(), None, None, r)
 
 
 def test_rx_window_index_checked_by_c_abi():

@@ -13,6 +13,7 @@ dnrp_rx_sync_stream) against numpy / the oracle.
 import numpy as np
 import pytest
 
+import llr_gate
 import oracle_py as O
 import phy_fixtures as F
 
@@ -138,6 +139,6 @@ def test_sync_stream_c2():
     ocf = O.cfg(cfgt[0], cfgt[1], os_min=cfgt[3], L=cfgt[4], M=cfgt[5])
     for i, m in enumerate(made):
         r = O.rx(ocf, O.psdef(*psd), wins[i], pre, float(got[i]["cfo_fractional_rad"]), m[2], m[3])
-        assert np.abs(pcc[i].cpu().numpy().astype(int) - r["pcc_llr"]).max() <= 1, i
-        assert np.abs(pdc[i].cpu().numpy().astype(int) - r["pdc_llr"]).max() <= 1, i
+        llr_gate.check(("ring", i, "pcc"), pcc[i].cpu().numpy(), r["pcc_llr"])
+        llr_gate.check(("ring", i, "pdc"), pdc[i].cpu().numpy(), r["pdc_llr"])
         assert np.array_equal(np.unpackbits(m[1])[: sz["G"]], (pdc[i].cpu().numpy() > 0).astype(np.uint8)), i

@@ -17,6 +17,7 @@ physical_resources.hpp:44); the wave-kernel fallback of the step sums (DNRP_SYNC
 import numpy as np
 import pytest
 
+import llr_gate
 import oracle_py as O
 import phy_fixtures as F
 
@@ -175,8 +176,8 @@ def test_sync_two_packets_per_window(rounds, monkeypatch):
     for i in range(6):
         r = O.rx(ocf, ops, windows[int(reps["window"][i])], int(reps["fine_peak_time"][i]),
                  float(reps["cfo_fractional_rad"][i]), meta[i][2], meta[i][3])
-        assert np.abs(pcc_llr[i].cpu().numpy().astype(int) - r["pcc_llr"]).max() <= 1, i
-        assert np.abs(pdc_llr[i].cpu().numpy().astype(int) - r["pdc_llr"]).max() <= 1, i
+        llr_gate.check(("two_per_window", i, "pcc"), pcc_llr[i].cpu().numpy(), r["pcc_llr"])
+        llr_gate.check(("two_per_window", i, "pdc"), pdc_llr[i].cpu().numpy(), r["pdc_llr"])
         assert np.array_equal(np.unpackbits(meta[i][1])[:G], (r["pdc_llr"] > 0).astype(np.uint8)), i
 
 
@@ -221,8 +222,7 @@ def test_sync_then_demodulate(name):
         fine, cfo_g = int(res[i, 0]["fine_peak_time"]), float(res[i, 0]["cfo_fractional_rad"])
         assert o["fine_64"] == fine and abs(o["cfo_frac"] - cfo_g) < 2e-6, (name, i, o["fine_64"], fine)
         r = O.rx(ocf, O.psdef(*psd), win, fine, cfo_g, metas[i][2], metas[i][3])
-        d_pdc = np.abs(g_pdc[i].astype(np.int32) - r["pdc_llr"].astype(np.int32))
-        d_pcc = np.abs(g_pcc[i].astype(np.int32) - r["pcc_llr"].astype(np.int32))
-        assert d_pcc.max() <= 1 and d_pdc.max() <= 1, (name, i, d_pcc.max(), d_pdc.max())
+        llr_gate.check((name, i, "pcc"), g_pcc[i], r["pcc_llr"])
+        llr_gate.check((name, i, "pdc"), g_pdc[i], r["pdc_llr"])
         bits = np.unpackbits(metas[i][1])[: sz["G"]]
         assert np.mean((g_pdc[i] > 0).astype(np.uint8) != bits) < 2e-2, name
