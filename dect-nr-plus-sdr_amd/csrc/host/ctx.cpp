@@ -1011,6 +1011,8 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         ctx->rx_snr_front = !e || std::atoi(e);
         const char* f = std::getenv("DNRP_RX_FUSED");
         ctx->rx_fused = ctx->rx_snr_front && f && std::atoi(f);
+        const char* gr = std::getenv("DNRP_RX_GROUP");
+        ctx->rx_group = gr ? static_cast<uint32_t>(std::atoi(gr)) : 0u;
         // zero-forced DRS pilots of every slot (the fused receiver's only): at most one DRS symbol per
         // 5 symbols (N_eff_TX <= 4) plus the zero op
         ctx->zd_row = 14 * ctx->cfg.b_max;
@@ -1196,15 +1198,46 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
         } else {
             fa.zd = nullptr;  // no reader
             fa.sym_first = t->pcc_max + 1;
-            if (t2->q.N_DF_symb > t->pcc_max) {
+            const uint32_t G = ctx->rx_group;
+            if (G && ng > G && t2->q.N_DF_symb > t->pcc_max && fa.stream && dev::rx_fft_wave_path(fa)) {
+                // packet groups: front end of group g on st, back end of group g on rx_aux once that
+                // front end is done, so group g+1's front end runs beside group g's back end and the
+                // back end reads Y (plain stores) while it is still in the L2 / Infinity Cache
+                if (!ctx->rx_aux) {
+                    HIPCHK(hipStreamCreateWithFlags(&ctx->rx_aux, hipStreamNonBlocking));
+                    HIPCHK(hipEventCreateWithFlags(&ctx->rx_fork, hipEventDisableTiming));
+                    HIPCHK(hipEventCreateWithFlags(&ctx->rx_join, hipEventDisableTiming));
+                }
                 fa.sym_count = t2->q.N_DF_symb - t->pcc_max;
-                ctx->tic("rx_fft_pdc", st);
-                if (dev::launch_rx_fft(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
-                ctx->toc("rx_fft_pdc", st);
+                fa.y_plain = 1;
+                ctx->tic("rx_pdc_phase", st);  // both streams' launches of the phase, fork to join
+                for (uint32_t g0 = 0; g0 < ng; g0 += G) {
+                    const uint32_t gn = std::min(G, ng - g0);
+                    auto fg = fa;
+                    fg.sel = gsel + 2 * g0;
+                    ctx->tic("rx_fft_pdc", st);
+                    if (dev::launch_rx_fft(fg, gn, st) != hipSuccess) return DNRP_EDEVICE;
+                    ctx->toc("rx_fft_pdc", st);
+                    HIPCHK(hipEventRecord(ctx->rx_fork, st));
+                    HIPCHK(hipStreamWaitEvent(ctx->rx_aux, ctx->rx_fork, 0));
+                    if ((err = launch_back(ctx, t, t2->bplan, gn, gsel + 2 * g0, true, t2->q.N_bps, t2->pdc_k.as<uint32_t>(),
+                                           t2->pdc_sym.as<uint16_t>(), pdc_llr, llr_stride, ctx->rx_aux, t2->sm)) != DNRP_OK)
+                        return err;
+                }
+                HIPCHK(hipEventRecord(ctx->rx_join, ctx->rx_aux));
+                HIPCHK(hipStreamWaitEvent(st, ctx->rx_join, 0));
+                ctx->toc("rx_pdc_phase", st);
+            } else {
+                if (t2->q.N_DF_symb > t->pcc_max) {
+                    fa.sym_count = t2->q.N_DF_symb - t->pcc_max;
+                    ctx->tic("rx_fft_pdc", st);
+                    if (dev::launch_rx_fft(fa, ng, st) != hipSuccess) return DNRP_EDEVICE;
+                    ctx->toc("rx_fft_pdc", st);
+                }
+                if ((err = launch_back(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps, t2->pdc_k.as<uint32_t>(),
+                                       t2->pdc_sym.as<uint16_t>(), pdc_llr, llr_stride, st, t2->sm)) != DNRP_OK)
+                    return err;
             }
-            if ((err = launch_back(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps, t2->pdc_k.as<uint32_t>(),
-                                   t2->pdc_sym.as<uint16_t>(), pdc_llr, llr_stride, st, t2->sm)) != DNRP_OK)
-                return err;
         }
         if (rep) {
             // MIMO report at the packet end (rx_synced.cpp:417-436; the reference runs it after a

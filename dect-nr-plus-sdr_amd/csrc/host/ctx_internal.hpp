@@ -214,6 +214,12 @@ struct dnrp_ctx {
     // per PCC call: the DRS SNR sums (and pilots) come from the front end (DNRP_RX_SNR_FRONT, read
     // once per PCC call so that its PDC call agrees), and the PDC phase may take the fused receiver
     bool rx_snr_front = true, rx_fused = true;
+    // PDC phase in packet groups (DNRP_RX_GROUP packets, 0: one launch set): the front end of group g+1
+    // on the caller's stream beside the back end of group g on rx_aux, Y of a group re-read from the
+    // caches; fork / join through rx_fork / rx_join
+    uint32_t rx_group = 0;
+    hipStream_t rx_aux = nullptr;
+    hipEvent_t rx_fork = nullptr, rx_join = nullptr;
     uint32_t rx_mode = 0;  // DNRP_RX_MODE_* (dnrp_ctx_set_rx_mode)
     pinned st_tx, st_rxin, st_seq, st_rep;
     // retained RX phase-1 state: per PCC-batch slot its (u, b, N_eff_TX) tables and symbol
@@ -247,6 +253,9 @@ struct dnrp_ctx {
     dbuf fec_cbs2, fec_waves2, fec_map2, fec_work16b, fec_tailb, fec_cbout2;  // continuation of undecided blocks
     std::vector<uint32_t> fec_valid_off, fec_start;  // per K index ([idx][rv] for start)
     ~dnrp_ctx() {
+        if (rx_aux) (void)hipStreamDestroy(rx_aux);
+        if (rx_fork) (void)hipEventDestroy(rx_fork);
+        if (rx_join) (void)hipEventDestroy(rx_join);
         for (auto& e : ev)
             for (auto& p : e.second.ev) {
                 (void)hipEventDestroy(p.first);

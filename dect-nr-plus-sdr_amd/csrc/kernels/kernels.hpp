@@ -146,6 +146,8 @@ struct rx_front_args {
     uint32_t zd_dops, zd_row;
     uint32_t fft_pass, fft_tw_lds;  // rx_fft_kernel layout (launch_rx_fft: symbols per pass, LDS twiddles)
     uint32_t stf_chunk;             // rx_stf_ant_kernel: 0, or outputs per resampling chunk (launch_rx_stf)
+    uint32_t y_plain;               // 1: Y stored with plain (cache-allocating) stores, re-read from the
+                                    // caches by the next packet group's back end; 0: nontemporal stores
 };
 bool rx_fft_wave_path(const rx_front_args& a);  // launch_rx_fft takes rx_fft_wave_kernel (snr_part supported)
 hipError_t launch_rx_stf(const rx_front_args& a, uint32_t n, hipStream_t st);

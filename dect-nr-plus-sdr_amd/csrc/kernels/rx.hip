@@ -579,7 +579,7 @@ __global__ void __launch_bounds__(RX_THREADS) __attribute__((amdgpu_waves_per_eu
 #ifndef DNRP_RX_SPW
 #define DNRP_RX_SPW 2
 #endif
-template <int SPW>
+template <int SPW, bool YNT = true>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) rx_fft_wave_ct_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     constexpr int LR = 9, MR = 10, HLR = 24;
@@ -637,9 +637,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) rx
         const bool drs = so != 0xFFFFu;
         if constexpr (!experiment(XS_FE_SKIP_FIR)) rx_resample_ct<LR, MR, HLR>(A, in, S, sp, R, lane);
         rx_fft_bins<true>(A, S, R, lane, [&](uint32_t k, float2 v) {
-            // Y is written once and read by the next launch: nontemporal stores
+            // Y is written once and read by the next launch: nontemporal stores when that launch
+            // comes after the whole batch, plain ones when it follows within a cache-sized group
             typedef float f2v __attribute__((ext_vector_type(2)));
-            if (to_y) __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v*>(Yrow + k));
+            if constexpr (YNT) {
+                if (to_y) __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v*>(Yrow + k));
+            } else {
+                if (to_y) Yrow[k] = v;
+            }
             if (drs) R[k] = v;
         }, w1, wl);
         if (drs) {
@@ -702,9 +707,11 @@ hipError_t launch_rx_fft(const rx_front_args& a_in, uint32_t n, hipStream_t st) 
             // not 16) and no twiddle-load latency in the passes (PDC launch 5.44 -> 5.30 ms per C4
             // chunk, same box)
             const size_t lds1 = size_t(rxw_region(9, 10, W)) * sizeof(float2);
-            if (DNRP_RX_SPW > 1)
-                hipLaunchKernelGGL((rx_fft_wave_ct_kernel<DNRP_RX_SPW>),
-                                   dim3(n * a.N_RX * ((a.sym_count + DNRP_RX_SPW - 1) / DNRP_RX_SPW)), dim3(64), lds1, st, a);
+            const dim3 gs(n * a.N_RX * ((a.sym_count + DNRP_RX_SPW - 1) / DNRP_RX_SPW));
+            if (DNRP_RX_SPW > 1 && a.y_plain)
+                hipLaunchKernelGGL((rx_fft_wave_ct_kernel<DNRP_RX_SPW, false>), gs, dim3(64), lds1, st, a);
+            else if (DNRP_RX_SPW > 1)
+                hipLaunchKernelGGL((rx_fft_wave_ct_kernel<DNRP_RX_SPW>), gs, dim3(64), lds1, st, a);
             else
                 hipLaunchKernelGGL((rx_fft_wave_kernel<9, 10, 24, true, 1, true>), dim3(n * a.N_RX * a.sym_count), dim3(64),
                                    lds1, st, a);
