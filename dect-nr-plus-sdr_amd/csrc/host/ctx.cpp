@@ -2,6 +2,7 @@
 // scrambling sequences, batched TX / RX phase launches.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -547,6 +548,50 @@ rx2_tables* get_rx2(dnrp_ctx* ctx, const dnrp_psdef& d, int* err) {
             return nullptr;
         }
     }
+    // epoch receiver (kernels/rx_epoch.hip): the symbols whose bins each epoch's cells read, minus the
+    // PCC phase's (in Y from the PCC call) and the DRS symbols (the DRS pass); a symbol claimed by two
+    // epochs (or an epoch list past 16 bits) leaves the Y path in charge
+    {
+        const auto& m = t->maps;
+        auto is_drs = [&](uint32_t l) {
+            for (const auto& d : m.drs)
+                if (d.l == l) return true;
+            return false;
+        };
+        bool ok = !sm && plan.dl.size() <= dev::RX_MAX_DOPS;
+        std::vector<uint16_t> off{0}, syms, dsy;
+        std::vector<int> owner(t->q.N_DF_symb + 2, -1);
+        for (size_t e = 0; e < plan.epochs.size() && ok; ++e) {
+            std::vector<uint32_t> ls;
+            for (uint32_t s = plan.epochs[e].seg0; s < plan.epochs[e].seg1; ++s) {
+                const auto& g = plan.segs[s];
+                if (g.kind != geo::OP_PDC) {
+                    ok = false;
+                    break;
+                }
+                for (uint32_t l = 1; l <= t->q.N_DF_symb; ++l)
+                    if (m.pdc_sym_off[l] < g.j1 && m.pdc_sym_off[l + 1] > g.j0 && l > pm && !is_drs(l)) ls.push_back(l);
+            }
+            std::sort(ls.begin(), ls.end());
+            ls.erase(std::unique(ls.begin(), ls.end()), ls.end());
+            for (uint32_t l : ls) {
+                if (owner[l] >= 0) ok = false;
+                owner[l] = static_cast<int>(e);
+                syms.push_back(static_cast<uint16_t>(l));
+            }
+            off.push_back(static_cast<uint16_t>(syms.size()));
+        }
+        for (const auto& d : m.drs)
+            if (d.l > pm && d.l <= t->q.N_DF_symb) dsy.push_back(static_cast<uint16_t>(d.l));
+        t->n_ep_drs = static_cast<uint32_t>(dsy.size());
+        if (syms.empty()) syms.push_back(0);  // non-empty uploads
+        if (dsy.empty()) dsy.push_back(0);
+        t->ep_ok = ok && plan.epochs.size() > 0;
+        if (t->ep_ok && (!t->ep_off.upload(off) || !t->ep_sym.upload(syms) || !t->ep_drs.upload(dsy))) {
+            *err = DNRP_ENOMEM;
+            return nullptr;
+        }
+    }
     auto* r = t.get();
     ctx->rx2t[key] = std::move(t);
     return r;
@@ -625,8 +670,12 @@ bool snr_from_front(dnrp_ctx* ctx, rx1_tables* t) {
     return ctx->rx_snr_front && t->drs_arith && dev::rx_fft_wave_path(front_args(ctx, t, nullptr, nullptr));
 }
 
+dev::rx_cells_args cells_args(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t n, const uint32_t* sel,
+                              bool pdc, uint32_t N_bps, const uint32_t* kk, const uint16_t* cell_sym, int16_t* llr,
+                              uint32_t llr_stride, bool sm);
+
 // back-end launches of one phase: SNR chain, then cells (rx_back.hip); cells = false: the SNR chain
-// only (the fused PDC receiver equalises)
+// only (the fused PDC receiver and the epoch receiver equalise)
 int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t n, const uint32_t* sel, bool pdc,
                 uint32_t N_bps, const uint32_t* kk, const uint16_t* cell_sym, int16_t* llr, uint32_t llr_stride,
                 hipStream_t st, bool sm = false, bool cells = true) {
@@ -659,6 +708,20 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     s.nv_d = ctx->nv_d.as<float>();
     s.sel = sel;
     s.snr_part = snr_from_front(ctx, t) ? ctx->snr_part.as<double2>() : nullptr;
+    dev::rx_cells_args c = cells_args(ctx, t, plan, n, sel, pdc, N_bps, kk, cell_sym, llr, llr_stride, sm);
+    ctx->tic(name, st);
+    if (dev::launch_rx_snr(s, n, st) != hipSuccess) return DNRP_EDEVICE;
+    if (cells && plan.n_epochs &&
+        (sm ? dev::launch_rx_cells_sm(c, n, st) : dev::launch_rx_cells(c, n, st)) != hipSuccess)
+        return DNRP_EDEVICE;
+    ctx->toc(name, st);
+    return DNRP_OK;
+}
+
+// the cells kernels' arguments of one phase (rx_cells_kernel, rx_epoch_kernel)
+dev::rx_cells_args cells_args(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t n, const uint32_t* sel,
+                              bool pdc, uint32_t N_bps, const uint32_t* kk, const uint16_t* cell_sym, int16_t* llr,
+                              uint32_t llr_stride, bool sm) {
     dev::rx_cells_args c{};
     c.N_occ = t->N_occ;
     c.N_RX = ctx->cfg.N_TX_max;
@@ -675,30 +738,24 @@ int launch_back(dnrp_ctx* ctx, rx1_tables* t, const rx_plan_dev& plan, uint32_t 
     fill_pairs(t->N_eff_TX, c.pair, c.mod);
     c.is_pdc = pdc;
     c.sm = sm ? 1u : 0u;
-    c.nv_d = s.nv_d;
+    c.nv_d = ctx->nv_d.as<float>();
     c.epochs = plan.epochs.as<dev::rx_epoch>();
     c.segs = plan.segs.as<dev::rx_seg>();
-    c.dl = s.dl;
-    c.dmeta = s.dmeta;
-    c.drs_k = s.drs_k;
-    c.drs_v = s.drs_v;
+    c.dl = plan.dl.as<uint32_t>();
+    c.dmeta = plan.dmeta.as<uint32_t>();
+    c.drs_k = t->drs_k.as<uint32_t>();
+    c.drs_v = t->drs_v.as<float>();
     c.kk = kk;
     c.cell_sym = cell_sym;
     c.luts = t->luts.as<dev::rx_lut>();
-    c.Y = s.Y;
-    c.lut_d = s.lut_d;
+    c.Y = ctx->Y.as<float2>();
+    c.lut_d = ctx->lut_d.as<uint8_t>();
     c.pcc_seq = ctx->pcc_seq.as<uint8_t>();
     c.pdc_seq = static_cast<const uint8_t* const*>(ctx->pdc_seq_ptrs.p);
     c.llr = llr;
     c.llr_stride = llr_stride;
     c.sel = sel;
-    ctx->tic(name, st);
-    if (dev::launch_rx_snr(s, n, st) != hipSuccess) return DNRP_EDEVICE;
-    if (cells && plan.n_epochs &&
-        (sm ? dev::launch_rx_cells_sm(c, n, st) : dev::launch_rx_cells(c, n, st)) != hipSuccess)
-        return DNRP_EDEVICE;
-    ctx->toc(name, st);
-    return DNRP_OK;
+    return c;
 }
 
 }  // namespace
@@ -1011,6 +1068,8 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         ctx->rx_snr_front = !e || std::atoi(e);
         const char* f = std::getenv("DNRP_RX_FUSED");
         ctx->rx_fused = ctx->rx_snr_front && f && std::atoi(f);
+        const char* ep = std::getenv("DNRP_RX_EPOCH");
+        ctx->rx_epoch = ep && std::atoi(ep);
         const char* gr = std::getenv("DNRP_RX_GROUP");
         ctx->rx_group = gr ? static_cast<uint32_t>(std::atoi(gr)) : 0u;
         // zero-forced DRS pilots of every slot (the fused receiver's only): at most one DRS symbol per
@@ -1199,7 +1258,37 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
             fa.zd = nullptr;  // no reader
             fa.sym_first = t->pcc_max + 1;
             const uint32_t G = ctx->rx_group;
-            if (G && ng > G && t2->q.N_DF_symb > t->pcc_max && fa.stream && dev::rx_fft_wave_path(fa)) {
+            dev::rx_cells_args ec{};
+            const bool epoch = ctx->rx_epoch && t2->ep_ok && !t2->sm && fa.stream && dev::rx_fft_wave_path(fa) &&
+                               t2->bplan.cells_ok && t2->bplan.n_epochs &&
+                               dev::rx_epoch_supported(fa.N_RX, t->N_eff_TX) &&
+                               dev::rx_epoch_lds(ec = cells_args(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps,
+                                                                 t2->pdc_k.as<uint32_t>(), t2->pdc_sym.as<uint16_t>(),
+                                                                 pdc_llr, llr_stride, false)) <= 160 * 1024;
+            if (epoch) {
+                // DRS pass (the phase's DRS symbols: pilots in Y, SNR sums), the SNR chain's LUT picks,
+                // then one workgroup per (packet, epoch): front end of the epoch's symbols + equaliser
+                if (t2->n_ep_drs) {
+                    auto fd = fa;
+                    fd.sym_first = 0;
+                    fd.sym_list = t2->ep_drs.as<uint16_t>();
+                    fd.sym_count = t2->n_ep_drs;
+                    ctx->tic("rx_fft_pdc", st);
+                    if (dev::launch_rx_fft(fd, ng, st) != hipSuccess) return DNRP_EDEVICE;
+                    ctx->toc("rx_fft_pdc", st);
+                }
+                if ((err = launch_back(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps, nullptr, nullptr, pdc_llr,
+                                       llr_stride, st, false, false)) != DNRP_OK)
+                    return err;
+                dev::rx_epoch_args x{};
+                x.F = fa;
+                x.C = ec;
+                x.ep_off = t2->ep_off.as<uint16_t>();
+                x.ep_sym = t2->ep_sym.as<uint16_t>();
+                ctx->tic("rx_epoch", st);
+                if (dev::launch_rx_epoch(x, ng, st) != hipSuccess) return DNRP_EDEVICE;
+                ctx->toc("rx_epoch", st);
+            } else if (G && ng > G && t2->q.N_DF_symb > t->pcc_max && fa.stream && dev::rx_fft_wave_path(fa)) {
                 // packet groups: front end of group g on st, back end of group g on rx_aux once that
                 // front end is done, so group g+1's front end runs beside group g's back end and the
                 // back end reads Y (plain stores) while it is still in the L2 / Infinity Cache

@@ -169,6 +169,12 @@ struct rx2_tables {  // per (psdef): PDC phase
     bool fused_ok = false, drs_y = false;
     uint32_t n_fsym = 0, n_drs_syms = 0;
     dbuf fsym, drs_syms, mimo_zcells;
+    // epoch receiver (kernels/rx_epoch.hip): per plan epoch the front-end symbols it owns (PDC-bearing,
+    // after the PCC phase, not DRS: each in exactly one epoch), and the phase's DRS symbols for the
+    // DRS pass ahead of it
+    bool ep_ok = false;
+    uint32_t n_ep_drs = 0;
+    dbuf ep_off, ep_sym, ep_drs;
 };
 
 struct netid_seq {
@@ -218,6 +224,8 @@ struct dnrp_ctx {
     // on the caller's stream beside the back end of group g on rx_aux, Y of a group re-read from the
     // caches; fork / join through rx_fork / rx_join
     uint32_t rx_group = 0;
+    // PDC phase through the epoch receiver (kernels/rx_epoch.hip) where it applies (DNRP_RX_EPOCH)
+    bool rx_epoch = false;
     hipStream_t rx_aux = nullptr;
     hipEvent_t rx_fork = nullptr, rx_join = nullptr;
     uint32_t rx_mode = 0;  // DNRP_RX_MODE_* (dnrp_ctx_set_rx_mode)

@@ -223,6 +223,19 @@ struct rx_cells_args {      // equalisation + demapping, one WG per (packet, epo
     const uint32_t* sel;            // launch packet -> slot / output row
 };
 hipError_t launch_rx_cells(const rx_cells_args& a, uint32_t n, hipStream_t st);
+
+// PDC phase per (packet, epoch) workgroup (rx_epoch.hip): the front end of the epoch's symbols
+// (ep_sym[ep_off[e] .. ep_off[e + 1]), each symbol in exactly one epoch) into Y, then the epoch's
+// equalisation from those rows. N_b_DFT_os = 1024 with the compile-time 9/10 taps; MRC / SFBC.
+struct rx_epoch_args {
+    rx_front_args F;
+    rx_cells_args C;
+    const uint16_t* ep_off;  // [n_epochs + 1]
+    const uint16_t* ep_sym;
+};
+bool rx_epoch_supported(uint32_t N_RX, uint32_t NT);
+size_t rx_epoch_lds(const rx_cells_args& a);
+hipError_t launch_rx_epoch(const rx_epoch_args& x, uint32_t n, hipStream_t st);
 // spatial multiplexing (a.sm): N_RX x N_SS in {2, 4, 8} x {2, 4} with N_RX >= N_SS
 hipError_t launch_rx_cells_sm(const rx_cells_args& a, uint32_t n, hipStream_t st);
 

@@ -263,6 +263,36 @@ def test_rx_parity_fused_stride(name, stride, monkeypatch):
     _rx_parity_fused(name, stride, monkeypatch)
 
 
+EPOCH_CASES = ["C4", "C3", "C2", "tm5_u2b4", "mrc2_64qam", "mrc4_16qam", "lmode_C4", "lmode_txdiv2", "lmode_siso",
+               "tm1_txdiv2", "tm3_codebook3", "tm7_codebook9", "subslot_tm5", "C1_mcs0", "u2_in_u8b16"]
+
+
+def _rx_parity_epoch(name, stride, monkeypatch):
+    """DNRP_RX_EPOCH=1: the PDC phase through the epoch receiver (rx_epoch.hip: DRS pass, SNR chain, then one
+    workgroup per (packet, epoch) running the front end of the epoch's symbols and equalising them) instead
+    of the batch-wide front end + rx_cells -- same oracle and gates. Geometries outside it (N_b_DFT_os !=
+    1024) run the Y path; where it applies, the launch count proves it ran."""
+    monkeypatch.setenv("DNRP_RX_EPOCH", "1")
+    monkeypatch.setenv("DNRP_TIMING", "1")
+    phy = _rx_parity(name, stride)
+    import dnrp
+    n_ep = phy.kernel_time_total("rx_epoch")[1]
+    if phy.packet_sizes(dnrp.psdef(*TX_CASES[name][0]))["N_b_DFT_os"] == 1024:
+        assert n_ep > 0, name
+    else:
+        assert n_ep == 0, name
+
+
+@pytest.mark.parametrize("name", EPOCH_CASES)
+def test_rx_parity_epoch(name, monkeypatch):
+    _rx_parity_epoch(name, 2, monkeypatch)
+
+
+@pytest.mark.parametrize("name,stride", [("C4", 1), ("C4", 3), ("tm5_u2b4", 3), ("C3", 1), ("tm1_txdiv2", 4)])
+def test_rx_parity_epoch_stride(name, stride, monkeypatch):
+    _rx_parity_epoch(name, stride, monkeypatch)
+
+
 def test_rx_largest_cells_geometry(monkeypatch):
     """8 RX antennas x 4 transmit streams at b = 16 (TM5 into an N_TX_max = 8 context): the largest
     N_RX / NT / b of the cells kernel's LDS staging (pilot rows of 8 x 4 streams, both weight tables).
@@ -551,6 +581,17 @@ def test_rx_negative_fine_peak():
 
 @pytest.mark.parametrize("name,n", [("C4", 4096), ("C3", 8192), ("C4", 16384)])
 def test_full_chunk_edges(name, n):
+    _full_chunk_edges(name, n)
+
+
+@pytest.mark.parametrize("name,n", [("C4", 16384), ("C3", 8192)])
+def test_full_chunk_edges_epoch(name, n, monkeypatch):
+    """The bench chunk through the epoch receiver (DNRP_RX_EPOCH=1): grid and Y offsets past 2^32."""
+    monkeypatch.setenv("DNRP_RX_EPOCH", "1")
+    _full_chunk_edges(name, n)
+
+
+def _full_chunk_edges(name, n):
     """A full bench chunk (C4: 4096 packets, C3: 8192, and the bench's C4 chunk of 16384 packets, whose
     window and Y offsets pass 2^32 float2 elements; max_batch = chunk): TX and RX of the first, middle
     and last packet compared with the oracle (rx_synced.cpp:325-436), chunk-boundary indexing included."""

@@ -14,7 +14,7 @@ for src in "$@"; do
   base=$(basename $src)
   sub=$(basename $(dirname $src))
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result $flags \
-      -I../include -Icsrc/host -Icsrc/kernels -Ibuild/gen $( case "$base" in tx.hip|rx.hip|rx_back.hip|rx_fused.hip) echo -fno-slp-vectorize ;; esac ) \
+      -I../include -Icsrc/host -Icsrc/kernels -Ibuild/gen $( case "$base" in tx.hip|rx.hip|rx_back.hip|rx_fused.hip|rx_epoch.hip) echo -fno-slp-vectorize ;; esac ) \
       -c csrc/$sub/$base -o $out/$base.o
   objs=$(echo $objs | tr ' ' '\n' | grep -v "build/$sub/$base.o" | tr '\n' ' ')
   objs="$objs $out/$base.o"
