@@ -905,6 +905,76 @@ extern "C" int dnrp_pdc_softbuffer_size(uint32_t N_TB_bits, uint32_t Z, uint64_t
     return DNRP_OK;
 }
 
+// device encoder planning shared by the PDC and PLCF batches: code blocks in packet order, each at a
+// 64-bit aligned offset of the packed scratch; per packet its first block, per block its first bit in
+// the packet's d row (kernels/fec.hip fec_encode_kernel, fec_pack_kernel)
+struct enc_plan {
+    std::vector<dnrp::dev::FecEncCb> cbs;
+    std::vector<uint32_t> first, pstart, G;
+    std::vector<uint64_t> oo;
+    uint64_t bits = 0;
+    uint32_t max_bytes = 0;
+    bool bytes = true;  // every block starts on a byte of its row and has whole bytes: direct mode
+    void add(dnrp::dev::FecEncCb cb, uint32_t ps) {
+        // the RSC state map over one lane's chunk (zero input): s = s1 | s2 << 1 | s3 << 2 -> (s2 ^ s3, s1, s2)
+        const uint32_t Lc = dnrp::dev::fec_enc_chunk(cb.K);
+        cb.mA = 0;
+        for (uint32_t b = 0; b < 3; ++b) {
+            uint32_t st = 1u << b;
+            for (uint32_t i = 0; i < Lc; ++i) st = (((st >> 1) ^ (st >> 2)) & 1u) | ((st & 1u) << 1) | (((st >> 1) & 1u) << 2);
+            cb.mA |= st << (3 * b);
+        }
+        cb.oo = bits;
+        cb.pstart = ps;
+        bytes = bytes && ps % 8 == 0 && cb.E % 8 == 0;
+        bits += (cb.E + 63ull) / 64 * 64;
+        oo.push_back(cb.oo);
+        pstart.push_back(ps);
+        cbs.push_back(cb);
+    }
+};
+
+// upload the plan and run encoder + pack (tbcrc: per-packet TB CRCs already enqueued, or null)
+static int run_encode(dnrp_ctx* ctx, enc_plan& P, const uint8_t* tb, const uint32_t* tbcrc, uint8_t* d, uint32_t d_stride,
+                      hipStream_t s) {
+    using namespace dnrp::dev;
+    const size_t n = P.G.size(), nc = P.cbs.size();
+    P.first.push_back(static_cast<uint32_t>(nc));
+    std::vector<uint8_t> args((n + 1) * 4 + nc * 4 + nc * 8 + n * 4 + 64);
+    uint8_t* ap = args.data();
+    const size_t o_first = 0, o_ps = (n + 1) * 4, o_oo = (o_ps + nc * 4 + 7) / 8 * 8, o_G = o_oo + nc * 8;
+    std::memcpy(ap + o_first, P.first.data(), (n + 1) * 4);
+    std::memcpy(ap + o_ps, P.pstart.data(), nc * 4);
+    std::memcpy(ap + o_oo, P.oo.data(), nc * 8);
+    std::memcpy(ap + o_G, P.G.data(), n * 4);
+    if (!ctx->fec_cbs.upload(P.cbs) || !ctx->fec_bits.ensure(P.bits / 8 + 64) || !ctx->fec_waves.upload(args))
+        return DNRP_ENOMEM;
+    FecEncArgs E{};
+    E.tb = tb, E.tab = ctx->fec_tab.as<uint32_t>(), E.cbs = ctx->fec_cbs.as<FecEncCb>();
+    E.tbcrc = tbcrc, E.ebits = ctx->fec_bits.as<uint8_t>();
+    if (P.bytes) E.d = d, E.d_stride = d_stride;  // no scratch, no pack
+    ctx->tic("fec_encode", s);
+    if (launch_fec_encode(E, static_cast<uint32_t>(nc), s)) return DNRP_EDEVICE;
+    ctx->toc("fec_encode", s);
+    if (P.bytes) {
+        HIPCHK(hipStreamSynchronize(s));
+        return DNRP_OK;
+    }
+    const uint8_t* dargs = ctx->fec_waves.as<uint8_t>();
+    FecPackArgs K{};
+    K.ebits = E.ebits;
+    K.cb_first = reinterpret_cast<const uint32_t*>(dargs + o_first);
+    K.pstart = reinterpret_cast<const uint32_t*>(dargs + o_ps);
+    K.oo = reinterpret_cast<const uint64_t*>(dargs + o_oo);
+    K.G = reinterpret_cast<const uint32_t*>(dargs + o_G);
+    K.d = d, K.d_stride = d_stride, K.n = static_cast<uint32_t>(n), K.max_bytes = P.max_bytes;
+    ctx->tic("fec_pack", s);
+    if (launch_fec_pack(K, s)) return DNRP_EDEVICE;
+    ctx->toc("fec_pack", s);
+    HIPCHK(hipStreamSynchronize(s));
+    return DNRP_OK;
+}
+
 extern "C" int dnrp_pdc_encode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_cfg* cfg, const uint8_t* tb,
                                      uint32_t tb_stride, uint8_t* d, uint32_t d_stride, void* stream) {
     using namespace dnrp::dev;
@@ -914,78 +984,46 @@ extern "C" int dnrp_pdc_encode_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_fec_c
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rc = fec_tables(ctx);
     if (rc) return rc;
-    std::vector<std::vector<FecEncCb>> by_idx(kNofCbSizes);
-    std::vector<uint64_t> e_off(m), tb_off_all(m);
-    std::vector<uint32_t> Gs(m), nbytes(m);
-    uint64_t e_total = 0;
-    uint32_t max_bytes = 0;
+    enc_plan P;
+    std::vector<uint64_t> tb_off_all(m);
+    std::vector<uint32_t> nbytes(m);
     for (uint32_t i = 0; i < m; ++i) {
         Segm g;
         if ((rc = segm_of(&cfg[i], &g))) return rc;
         const uint32_t tbs = cfg[i].N_TB_bits, Qm = cfg[i].N_bps, G = cfg[i].G;
         if (tb_stride < tbs / 8 || d_stride < (G + 7) / 8) return DNRP_EINVAL;
-        e_off[i] = e_total, Gs[i] = G, nbytes[i] = tbs / 8, tb_off_all[i] = (uint64_t)i * tb_stride;
-        max_bytes = std::max(max_bytes, (G + 7) / 8);
+        nbytes[i] = tbs / 8, tb_off_all[i] = (uint64_t)i * tb_stride;
+        P.G.push_back(G);
+        P.first.push_back(static_cast<uint32_t>(P.cbs.size()));
+        P.max_bytes = std::max(P.max_bytes, (G + 7) / 8);
         uint32_t rp = 0, wp = 0;
         for (uint32_t r = 0; r < g.C; ++r) {
             const uint32_t K = r < g.C2 ? g.K2 : g.K1, idx = r < g.C2 ? g.K2_idx : g.K1_idx;
             FecEncCb cb{};
-            cb.tb_off = (uint64_t)i * tb_stride, cb.e_off = e_total + wp, cb.pkt = i, cb.tbs = tbs;
+            cb.tb_off = (uint64_t)i * tb_stride, cb.pkt = i, cb.tbs = tbs;
             cb.rp = rp, cb.rlen = g.C > 1 ? K - 24 : K, cb.E = cb_E(g, r, Qm, G);
             cb.start = ctx->fec_start[idx * 4 + cfg[i].rv], cb.crc24b = g.C > 1;
-            by_idx[idx].push_back(cb);
+            cb.K = K, cb.valid_off = ctx->fec_valid_off[idx];
+            qpp_params(idx, &cb.f1, &cb.f2);
+            P.add(cb, wp);
             rp += cb.rlen;
             wp += cb.E;
         }
-        e_total += G;
     }
-    std::vector<FecEncCb> cbs;
-    std::vector<FecWave> waves;
-    uint64_t cd = 0;
-    for (uint32_t idx = 0; idx < kNofCbSizes; ++idx) {
-        const auto& v = by_idx[idx];
-        const uint32_t K = cb_size(idx);
-        for (size_t c0 = 0; c0 < v.size(); c0 += 64) {
-            FecWave w{};
-            w.data_off = cd, w.K = K, w.n = (uint32_t)std::min<size_t>(64, v.size() - c0);
-            w.valid_off = ctx->fec_valid_off[idx];
-            qpp_params(idx, &w.f1, &w.f2);
-            w.first_cb = (uint32_t)cbs.size();
-            cbs.insert(cbs.end(), v.begin() + c0, v.begin() + c0 + w.n);
-            waves.push_back(w);
-            cd += (uint64_t)(K + 3 * (K + 4)) * 64;
-        }
-    }
-    // scratch: c/d streams per wave, unpacked bits, TB CRCs; argument arrays
-    std::vector<uint8_t> args(m * (8 + 8 + 4 + 4 + 4) + 64);
-    uint8_t* ap = args.data();
-    std::memcpy(ap, tb_off_all.data(), m * 8);
-    std::memcpy(ap + m * 8, e_off.data(), m * 8);
-    std::memcpy(ap + m * 16, nbytes.data(), m * 4);
-    std::memcpy(ap + m * 20, Gs.data(), m * 4);
-    if (!ctx->fec_cbs.upload(cbs) || !ctx->fec_waves.upload(waves) || !ctx->fec_work16.ensure(cd + 16) ||
-        !ctx->fec_bits.ensure(e_total + 16) || !ctx->fec_tbarg.upload(args))
-        return DNRP_ENOMEM;
+    // per-packet TB CRC24A first (fec_tbcrc_kernel), then the encoder and the pack
+    std::vector<uint8_t> args(m * (8 + 4 + 4) + 64);
+    std::memcpy(args.data(), tb_off_all.data(), m * 8);
+    std::memcpy(args.data() + m * 8, nbytes.data(), m * 4);
+    if (!ctx->fec_tbarg.upload(args)) return DNRP_ENOMEM;
     uint8_t* dargs = ctx->fec_tbarg.as<uint8_t>();
-    uint32_t* tbcrc = reinterpret_cast<uint32_t*>(dargs + m * 24);
+    uint32_t* tbcrc = reinterpret_cast<uint32_t*>(dargs + m * 12);
     FecTbArgs T{};
-    T.tb = tb, T.tb_off = reinterpret_cast<const uint64_t*>(dargs), T.nbytes = reinterpret_cast<const uint32_t*>(dargs + m * 16);
+    T.tb = tb, T.tb_off = reinterpret_cast<const uint64_t*>(dargs), T.nbytes = reinterpret_cast<const uint32_t*>(dargs + m * 8);
     T.crc_out = tbcrc, T.n = m;
+    ctx->tic("fec_tbcrc", s);
     if (launch_fec_tbcrc(T, s)) return DNRP_EDEVICE;
-    FecEncArgs E{};
-    E.tb = tb, E.tab = ctx->fec_tab.as<uint32_t>(), E.cbs = ctx->fec_cbs.as<FecEncCb>();
-    E.waves = ctx->fec_waves.as<FecWave>(), E.tbcrc = tbcrc;
-    E.cd = ctx->fec_work16.as<uint8_t>(), E.ebits = ctx->fec_bits.as<uint8_t>();
-    ctx->tic("fec_encode", s);
-    if (launch_fec_encode(E, (uint32_t)waves.size(), s)) return DNRP_EDEVICE;
-    ctx->toc("fec_encode", s);
-    FecPackArgs P{};
-    P.ebits = E.ebits, P.e_off = reinterpret_cast<const uint64_t*>(dargs + m * 8);
-    P.G = reinterpret_cast<const uint32_t*>(dargs + m * 20), P.d = d, P.d_stride = d_stride, P.n = m;
-    P.max_bytes = max_bytes;
-    if (launch_fec_pack(P, s)) return DNRP_EDEVICE;
-    HIPCHK(hipStreamSynchronize(s));
-    return DNRP_OK;
+    ctx->toc("fec_tbcrc", s);
+    return run_encode(ctx, P, tb, tbcrc, d, d_stride, s);
 }
 
 extern "C" int dnrp_pcc_decode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* plcf_type_test, const int16_t* llr,
@@ -1036,9 +1074,8 @@ extern "C" int dnrp_pcc_encode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* 
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rc = fec_tables(ctx);
     if (rc) return rc;
-    std::vector<std::vector<FecEncCb>> by_idx(kNofCbSizes);
-    std::vector<uint64_t> e_off(n);
-    std::vector<uint32_t> Gs(n, kPccBits);
+    enc_plan P;
+    P.max_bytes = (kPccBits + 7) / 8;
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t t = plcf_type[i];
         if (t != 1 && t != 2) return DNRP_EINVAL;
@@ -1046,45 +1083,14 @@ extern "C" int dnrp_pcc_encode_batch(dnrp_ctx* ctx, uint32_t n, const uint32_t* 
         if (plcf_stride < nb / 8) return DNRP_EINVAL;
         const bool cl = closed_loop && closed_loop[i], bf = beamforming && beamforming[i];
         FecEncCb cb{};
-        cb.tb_off = (uint64_t)i * plcf_stride, cb.e_off = (uint64_t)i * kPccBits, cb.pkt = i, cb.tbs = nb;
+        cb.tb_off = (uint64_t)i * plcf_stride, cb.pkt = i, cb.tbs = nb;
         cb.rp = 0, cb.rlen = nb + 16, cb.E = kPccBits, cb.start = ctx->fec_start[idx * 4];  // rv 0
         cb.crc16 = 1, cb.mask = cl ? (bf ? kMaskClBf : kMaskCl) : (bf ? kMaskBf : kMaskNone);
-        by_idx[idx].push_back(cb);
-        e_off[i] = (uint64_t)i * kPccBits;
+        cb.K = cb_size(idx), cb.valid_off = ctx->fec_valid_off[idx];
+        qpp_params(idx, &cb.f1, &cb.f2);
+        P.G.push_back(kPccBits);
+        P.first.push_back(static_cast<uint32_t>(P.cbs.size()));
+        P.add(cb, 0);
     }
-    std::vector<FecEncCb> cbs;
-    std::vector<FecWave> waves;
-    uint64_t cd = 0;
-    for (uint32_t idx = 0; idx < kNofCbSizes; ++idx) {
-        const auto& v = by_idx[idx];
-        const uint32_t K = cb_size(idx);
-        for (size_t c0 = 0; c0 < v.size(); c0 += 64) {
-            FecWave w{};
-            w.data_off = cd, w.K = K, w.n = (uint32_t)std::min<size_t>(64, v.size() - c0);
-            w.valid_off = ctx->fec_valid_off[idx];
-            qpp_params(idx, &w.f1, &w.f2);
-            w.first_cb = (uint32_t)cbs.size();
-            cbs.insert(cbs.end(), v.begin() + c0, v.begin() + c0 + w.n);
-            waves.push_back(w);
-            cd += (uint64_t)(K + 3 * (K + 4)) * 64;
-        }
-    }
-    std::vector<uint8_t> args(n * 12 + 16);
-    std::memcpy(args.data(), e_off.data(), n * 8);
-    std::memcpy(args.data() + n * 8, Gs.data(), n * 4);
-    if (!ctx->fec_cbs.upload(cbs) || !ctx->fec_waves.upload(waves) || !ctx->fec_work16.ensure(cd + 16) ||
-        !ctx->fec_bits.ensure((size_t)n * kPccBits + 16) || !ctx->fec_tbarg.upload(args))
-        return DNRP_ENOMEM;
-    FecEncArgs E{};
-    E.tb = plcf, E.tab = ctx->fec_tab.as<uint32_t>(), E.cbs = ctx->fec_cbs.as<FecEncCb>();
-    E.waves = ctx->fec_waves.as<FecWave>(), E.tbcrc = nullptr;
-    E.cd = ctx->fec_work16.as<uint8_t>(), E.ebits = ctx->fec_bits.as<uint8_t>();
-    if (launch_fec_encode(E, (uint32_t)waves.size(), s)) return DNRP_EDEVICE;
-    FecPackArgs P{};
-    P.ebits = E.ebits, P.e_off = ctx->fec_tbarg.as<uint64_t>();
-    P.G = reinterpret_cast<const uint32_t*>(ctx->fec_tbarg.as<uint8_t>() + n * 8), P.d = d, P.d_stride = d_stride;
-    P.n = n, P.max_bytes = (kPccBits + 7) / 8;
-    if (launch_fec_pack(P, s)) return DNRP_EDEVICE;
-    HIPCHK(hipStreamSynchronize(s));
-    return DNRP_OK;
+    return run_encode(ctx, P, plcf, nullptr, d, d_stride, s);
 }

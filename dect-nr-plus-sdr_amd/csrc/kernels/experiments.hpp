@@ -44,6 +44,9 @@ enum xs_bit : unsigned {
     XS_FE_PREFETCH = 1u << 16,
     // MMSE Gram matrix of 16 cells per v_mfma_f32_4x4x1_16b_f32 (x1.7 rx_pdc in C4SM)
     XS_MMSE_MFMA = 1u << 17,
+    // rx_epoch_kernel phase skips (output meaningless): no front-end tasks / no equalisation
+    XS_EP_SKIP_FE = 1u << 18,
+    XS_EP_SKIP_EQ = 1u << 19,
 };
 
 __host__ __device__ constexpr bool experiment(unsigned bit) { return (DNRP_EXPERIMENTS & bit) != 0u; }

@@ -4,7 +4,8 @@
 //   fec_tdec_kernel     wavefront = up to 64 code blocks of one size K, lane = code block: the
 //                       iterations of the host decoder (fec.cpp Tdec / map_decode) with CRC early stop
 //   fec_tbcrc_kernel    wavefront = packet with C > 1: transport-block CRC24A (pdc_enc.cpp:478-488),
-//                       segment CRCs per lane joined by GF(2) shifts
+//                       16-B pieces per lane joined by GF(2) shifts
+// and the encoder: fec_encode_kernel (wavefront = code block) + fec_pack_kernel (scratch -> d rows).
 #include "fec_dev.hpp"
 
 #ifndef FEC_BWD_AHEAD
@@ -310,50 +311,89 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_FE
     A.cb_out[w.first_cb + l] = (used << 4) | (mask << 1) | (ok ? 1u : 0u);
 }
 
-// GF(2)[x] / CRC24A helpers for joining segment CRCs: crc(A || B) = crc(A) x^{|B|} + crc(B)
-__device__ __forceinline__ uint32_t mulmod24(uint32_t a, uint32_t b) {
+// GF(2)[x] helpers for joining segment CRCs (zero initial register, no final XOR, so the CRC is
+// linear): crc(A || B) = crc(A) x^{|B|} + crc(B) mod g, and leading zero bits do not change it.
+// W-bit CRCs with polynomial g = x^W + poly.
+template <int W>
+__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b, uint32_t poly) {
+    constexpr uint32_t M = (1u << W) - 1u;
     uint32_t r = 0;
-    for (int i = 23; i >= 0; --i) {
-        const uint32_t top = (r >> 23) & 1;
-        r = (r << 1) & 0xFFFFFF;
-        if (top) r ^= 0x864CFB;
-        if ((b >> i) & 1) r ^= a;
+#pragma unroll
+    for (int i = W - 1; i >= 0; --i) {
+        const uint32_t top = (r >> (W - 1)) & 1u;
+        r = (r << 1) & M;
+        if (top) r ^= poly;
+        if ((b >> i) & 1u) r ^= a;
     }
     return r;
 }
-__device__ uint32_t xpow24(uint64_t n) {  // x^n mod g
-    uint32_t r = 1, b = 2;  // 1 and x
+template <int W>
+__device__ uint32_t xpow(uint64_t n, uint32_t poly) {  // x^n mod g
+    uint32_t r = 1, b = 2;
     while (n) {
-        if (n & 1) r = mulmod24(r, b);
-        b = mulmod24(b, b);
+        if (n & 1) r = mulmod<W>(r, b, poly);
+        b = mulmod<W>(b, b, poly);
         n >>= 1;
     }
     return r;
 }
+template <int W>
+__device__ __forceinline__ uint32_t xshift(uint32_t n, uint32_t poly) {  // x^n mod g by n shifts (small n)
+    constexpr uint32_t M = (1u << W) - 1u;
+    uint32_t r = 1;
+    for (uint32_t i = 0; i < n; ++i) r = ((r << 1) & M) ^ (((r >> (W - 1)) & 1u) ? poly : 0u);
+    return r;
+}
+constexpr uint32_t CRC24A_POLY = 0x864CFB, CRC24B_POLY = 0x800063, CRC16_POLY = 0x1021;
 
+// Transport-block CRC24A (pdc_enc.cpp:478-488). The TB is read in 1-KiB blocks, one coalesced 16-B
+// piece per lane; each lane's CRC (byte table in LDS) of its piece is joined with its neighbours' in a
+// 6-level tree (multipliers x^128 .. x^4096, equal-length segments), and the running CRC takes the
+// block by crc x^(8 len) + block. A short last block is front-padded (leading zeros leave a CRC
+// unchanged), so its segments keep equal lengths.
 __global__ void __launch_bounds__(64) fec_tbcrc_kernel(FecTbArgs A) {
+    __shared__ uint32_t T[256];
     const uint32_t p = blockIdx.x, l = threadIdx.x;
-    const uint8_t* d = A.tb + A.tb_off[p];
-    const uint32_t nb = A.nbytes[p], seg = (nb + 63) / 64;
-    const uint32_t lo = min(nb, l * seg), hi = min(nb, lo + seg);
-    uint32_t reg = 0;
-    for (uint32_t i = lo; i < hi; ++i) {
-        const uint32_t byte = d[i];
-        for (int t = 7; t >= 0; --t) {
-            const uint32_t top = (reg >> 23) & 1;
-            reg = (reg << 1) & 0xFFFFFF;
-            if (top ^ ((byte >> t) & 1)) reg ^= 0x864CFB;
-        }
+    for (uint32_t v = l; v < 256; v += 64) {  // byte table of CRC24A: T[v] = crc of byte v
+        uint32_t r = v << 16;
+        for (int t = 0; t < 8; ++t) r = ((r << 1) & 0xFFFFFFu) ^ (((r >> 23) & 1u) ? CRC24A_POLY : 0u);
+        T[v] = r;
     }
-    __shared__ uint32_t part[64];
-    part[l] = reg;
     __syncthreads();
-    if (l == 0) {
-        uint32_t crc = 0;
-        for (uint32_t j = 0; j < 64; ++j) {
-            const uint32_t a = min(nb, j * seg), b = min(nb, a + seg);
-            if (b > a) crc = mulmod24(crc, xpow24(8ull * (b - a))) ^ part[j];
+    const uint8_t* d = A.tb + A.tb_off[p];
+    const uint32_t nb = A.nbytes[p];
+    uint32_t lv[7];
+    lv[0] = xshift<24>(128, CRC24A_POLY);
+#pragma unroll
+    for (int t = 0; t < 6; ++t) lv[t + 1] = mulmod<24>(lv[t], lv[t], CRC24A_POLY);  // x^256 .. x^8192
+    uint32_t crc = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
+        const uint32_t len = min(1024u, nb - b0);
+        const int32_t s0 = static_cast<int32_t>(16 * l) - static_cast<int32_t>(1024 - len);  // piece start in the block
+        uint32_t r = 0;
+        if (s0 >= 0 && (((uintptr_t)(d + b0 + s0)) & 15u) == 0) {  // whole aligned piece: one 16-B load
+            const uint4 v = *reinterpret_cast<const uint4*>(d + b0 + s0);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) r = ((r << 8) & 0xFFFFFFu) ^ T[((r >> 16) ^ (w[q] >> (8 * k))) & 0xFFu];
+        } else {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int32_t i = s0 + t;
+                if (i >= 0) r = ((r << 8) & 0xFFFFFFu) ^ T[((r >> 16) ^ d[b0 + i]) & 0xFFu];
+            }
         }
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            const uint32_t o = __shfl_down(r, 1u << t);
+            if ((l & ((2u << t) - 1u)) == 0) r = mulmod<24>(r, lv[t], CRC24A_POLY) ^ o;
+        }
+        const uint32_t blk = __shfl(r, 0);
+        crc = mulmod<24>(crc, len == 1024 ? lv[6] : xpow<24>(8ull * len, CRC24A_POLY), CRC24A_POLY) ^ blk;
+    }
+    if (l == 0) {
         if (A.crc_out) {
             A.crc_out[p] = crc;
         } else {
@@ -363,114 +403,270 @@ __global__ void __launch_bounds__(64) fec_tbcrc_kernel(FecTbArgs A) {
     }
 }
 
-// ---- encoder (fec.cpp dnrp_pdc_encode: pdc_enc.cpp:148-229) ---------------------------------------
-// wavefront = up to 64 code blocks of one size, lane = code block: b bits -> CRC24B -> both
-// constituent encoders (the second on the QPP rows, addresses by the scalar recurrence) with trellis
-// termination -> rate matching into the unpacked bit scratch
-__global__ void __launch_bounds__(64) fec_encode_kernel(FecEncArgs A) {
-    const FecWave w = A.waves[blockIdx.x];
-    const uint32_t l = threadIdx.x, K = w.K, D = K + 4;
-    const bool active = l < w.n;
-    const FecEncCb cb = A.cbs[w.first_cb + (active ? l : 0)];
-    uint8_t* c = A.cd + w.data_off;
-    uint8_t* d0 = c + (size_t)K * 64;
-    uint8_t* d1 = d0 + (size_t)D * 64;
-    uint8_t* d2 = d1 + (size_t)D * 64;
+// ---- encoder (fec.cpp dnrp_pdc_encode: pdc_enc.cpp:148-229; dnrp_pcc_encode: pcc_enc.cpp:166-212) ----
+// One wavefront per code block, its bits shared by the lanes as MSB-first 32-bit words in LDS: c (the
+// block: TB bits, then the TB CRC24A / PLCF CRC16 ^ mask, then the code-block CRC24B), and the three
+// coded streams d0 = c, d1 = z, d2 = z' with their tails (TS 36.212 §5.1.3.2). Each constituent
+// encoder runs lane-parallel: lane l encodes bits [l Lc, (l + 1) Lc) once from the zero state, the
+// entry states follow from an affine prefix scan over the lanes (state map M = A^Lc), and a second
+// pass from the true entry state writes the parity words. Rate matching: 64 consecutive output bits
+// per step -- list entries (start + j) mod 3 (K + 4) read coalesced, the bits gathered from LDS, one
+// ballot -- kept one 8-B word per lane and stored 512 B at a time into the packed scratch, each code
+// block at a 64-bit aligned offset; fec_pack_kernel splices the blocks into the d rows.
+constexpr uint32_t FEC_ENC_WAVES = 4;
+// bits per lane of a K-bit block (multiple of 32, <= 96 for K <= 6144); host: fec_enc_chunk too
+constexpr uint32_t FEC_ENC_WORDS = (6144 + 4 + 31) / 32 + 1;
+
+__device__ __forceinline__ uint32_t lbit(const uint32_t* w, uint32_t k) { return (w[k >> 5] >> (31u - (k & 31u))) & 1u; }
+
+// RSC step, state s = s1 | s2 << 1 | s3 << 2: a = u ^ s2 ^ s3, z = a ^ s1 ^ s3, next = (a, s1, s2)
+__device__ __forceinline__ uint32_t rsc_step(uint32_t& s, uint32_t u) {
+    const uint32_t s1 = s & 1u, s2 = (s >> 1) & 1u, s3 = (s >> 2) & 1u, a = u ^ s2 ^ s3;
+    s = a | (s1 << 1) | (s2 << 2);
+    return a ^ s1 ^ s3;
+}
+struct gf2m3 {  // 3x3 GF(2) matrix as its three 3-bit columns
+    uint32_t c0, c1, c2;
+    __device__ uint32_t apply(uint32_t s) const { return ((s & 1u) ? c0 : 0u) ^ ((s & 2u) ? c1 : 0u) ^ ((s & 4u) ? c2 : 0u); }
+    __device__ gf2m3 sq() const { return {apply(c0), apply(c1), apply(c2)}; }
+};
+
+// one constituent encoder over K input bits in(i): parity words of bits [i0, i0 + n) into z (the lane's
+// whole words: Lc is a multiple of 32, at most 96), returns the encoder's final state (every lane).
+// The lane's input bits are gathered once into registers; mA: the state map M = A^Lc (host, per K)
+template <class In>
+__device__ __forceinline__ uint32_t rsc_wave(In in, uint32_t K, uint32_t Lc, uint32_t mA, uint32_t lane, uint32_t* z) {
+    const uint32_t i0 = lane * Lc, n = i0 < K ? min(Lc, K - i0) : 0u;
+    uint32_t xw[3] = {0u, 0u, 0u};
+    uint32_t s = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t u = in(i0 + i);
+        xw[i >> 5] |= u << (31u - (i & 31u));
+        rsc_step(s, u);
+    }
+    // the inclusive affine scan v_l = F_l + M v_{l-1} over the lanes
+    gf2m3 M{mA & 7u, (mA >> 3) & 7u, (mA >> 6) & 7u};
+    uint32_t v = s;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d);
+        if (lane >= d) v ^= M.apply(o);
+        M = M.sq();
+    }
+    uint32_t st = __shfl_up(v, 1u);
+    if (lane == 0) st = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) {
+        if (32 * q >= n) break;
+        const uint32_t x = xw[q], nb = min(32u, n - 32 * q);
+        uint32_t w = 0;
+        for (uint32_t t = 0; t < nb; ++t) w = (w << 1) | rsc_step(st, (x >> (31u - t)) & 1u);
+        z[(i0 >> 5) + q] = w << (32u - nb);
+    }
+    // the encoder's final state: the last lane's, after its own (possibly short) chunk
+    return __shfl(st, (K - 1) / Lc);
+}
+
+__global__ void __launch_bounds__(64 * FEC_ENC_WAVES) fec_encode_kernel(FecEncArgs A, uint32_t n_cb) {
+    __shared__ uint32_t lds[FEC_ENC_WAVES][4][FEC_ENC_WORDS];
+    __shared__ unsigned long long stage[FEC_ENC_WAVES][64];  // direct mode: a batch of output words
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t ci = blockIdx.x * FEC_ENC_WAVES + wv;
+    if (ci >= n_cb) return;  // uniform per wave; no workgroup barrier below
+    const FecEncCb cb = A.cbs[ci];
+    uint32_t* cw = lds[wv][0];
+    uint32_t* d1 = lds[wv][1];
+    uint32_t* d2 = lds[wv][2];
+    uint32_t* d0 = lds[wv][3];
+    const uint32_t K = cb.K, D = K + 4, nw = (D + 31) / 32;
+    for (uint32_t i = lane; i < FEC_ENC_WORDS; i += 64) cw[i] = d0[i] = d1[i] = d2[i] = 0u;
     const uint8_t* tb = A.tb + cb.tb_off;
+    const uint32_t tbytes = cb.tbs >> 3;
+    // the CRC after the TB: PLCF CRC16 ^ mask over its 40 / 80 bits (every lane), else the TB's CRC24A
     uint32_t tcrc;
-    if (cb.crc16) {  // PLCF CRC16 over its 40 / 80 bits, masked (closed loop / beamforming)
+    if (cb.crc16) {
         uint32_t r16 = 0;
         for (uint32_t pos = 0; pos < cb.tbs; ++pos) {
             const uint32_t top = (r16 >> 15) & 1u;
             r16 = (r16 << 1) & 0xFFFFu;
-            if (top ^ ((tb[pos >> 3] >> (7 - (pos & 7))) & 1u)) r16 ^= 0x1021u;
+            if (top ^ ((tb[pos >> 3] >> (7 - (pos & 7))) & 1u)) r16 ^= CRC16_POLY;
         }
         tcrc = r16 ^ cb.mask;
     } else {
         tcrc = A.tbcrc[cb.pkt];
     }
-    const uint32_t tcrc_top = cb.crc16 ? 15u : 23u;
-    // c = b[rp, rp + rlen) (+ CRC24B), encoder 1 on the fly
-    uint32_t reg = 0, s1 = 0, s2 = 0, s3 = 0, byte = 0;
-    for (uint32_t k = 0; k < K; ++k) {
-        uint32_t bit;
-        if (k < cb.rlen) {
-            const uint32_t pos = cb.rp + k;
-            if ((k == 0 || (pos & 7) == 0) && pos < cb.tbs) byte = tb[pos >> 3];  // one load per byte
-            bit = pos < cb.tbs ? (byte >> (7 - (pos & 7))) & 1u : (tcrc >> (tcrc_top - (pos - cb.tbs))) & 1u;
-            const uint32_t top = (reg >> 23) & 1u;
-            reg = (reg << 1) & 0xFFFFFF;
-            if (top ^ bit) reg ^= 0x800063;
-        } else {
-            bit = (reg >> (23 - (k - cb.rlen))) & 1u;  // the code-block CRC (crc24b blocks only)
+    const uint32_t clen = cb.crc16 ? 16u : 24u;
+    __builtin_amdgcn_wave_barrier();
+    // c words [0, rlen): TB bits from bit rp, the TB / PLCF CRC bits after bit tbs
+    for (uint32_t i = lane; 32 * i < cb.rlen; i += 64) {
+        const uint32_t pos = cb.rp + 32 * i, b0 = pos >> 3, sh = pos & 7u;
+        uint64_t v = 0;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) v = (v << 8) | (b0 + t < tbytes ? tb[b0 + t] : 0u);
+        uint32_t w = static_cast<uint32_t>(v >> (8 - sh));
+        if (pos + 32 > cb.tbs)  // the word reaches the CRC after the TB
+            for (uint32_t t = 0; t < 32; ++t) {
+                const uint32_t q = pos + t;
+                if (q >= cb.tbs && q < cb.tbs + clen) w |= ((tcrc >> (clen - 1 - (q - cb.tbs))) & 1u) << (31 - t);
+            }
+        const uint32_t valid = min(32u, cb.rlen - 32 * i);
+        cw[i] = valid == 32 ? w : w & ~(0xFFFFFFFFu >> valid);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t Lc = fec_enc_chunk(K);
+    if (cb.crc24b) {
+        // CRC24B over c[0, rlen), front-padded to 64 Lc bits so the lanes' segments are equal
+        const int32_t off = static_cast<int32_t>(64 * Lc) - static_cast<int32_t>(cb.rlen);
+        uint32_t r = 0;
+        for (uint32_t t = 0; t < Lc; ++t) {
+            const int32_t k = static_cast<int32_t>(lane * Lc + t) - off;
+            if (k < 0) continue;
+            const uint32_t top = (r >> 23) & 1u;
+            r = (r << 1) & 0xFFFFFFu;
+            if (top ^ lbit(cw, static_cast<uint32_t>(k))) r ^= CRC24B_POLY;
         }
-        c[(size_t)k * 64 + l] = (uint8_t)bit;
-        d0[(size_t)k * 64 + l] = (uint8_t)bit;
-        const uint32_t a = bit ^ s2 ^ s3;
-        d1[(size_t)k * 64 + l] = (uint8_t)(a ^ s1 ^ s3);
-        s3 = s2, s2 = s1, s1 = a;
+        uint32_t mlt = xshift<24>(Lc, CRC24B_POLY);
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            const uint32_t o = __shfl_down(r, 1u << t);
+            if ((lane & ((2u << t) - 1u)) == 0) r = mulmod<24>(r, mlt, CRC24B_POLY) ^ o;
+            mlt = mulmod<24>(mlt, mlt, CRC24B_POLY);
+        }
+        const uint32_t crc = __shfl(r, 0);
+        if (lane < 24) {
+            const uint32_t k = cb.rlen + lane;
+            atomicOr(&cw[k >> 5], ((crc >> (23 - lane)) & 1u) << (31u - (k & 31u)));
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    uint32_t x1[3], z1[3];
-    for (int t = 0; t < 3; ++t) {
-        x1[t] = s2 ^ s3, z1[t] = s1 ^ s3;
-        s3 = s2, s2 = s1, s1 = 0;
-    }
-    // encoder 2 on c[pi(i)] (each lane reads back only its own column)
-    const Qpp q{K, w.f1, w.f2};
-    uint32_t pi = 0, dl = q.delta(0);
-    const uint32_t f2x2 = 2 * w.f2 % K;
-    s1 = s2 = s3 = 0;
-    for (uint32_t i = 0; i < K; ++i) {
-        const uint32_t a = c[(size_t)pi * 64 + l] ^ s2 ^ s3;
-        d2[(size_t)i * 64 + l] = (uint8_t)(a ^ s1 ^ s3);
-        s3 = s2, s2 = s1, s1 = a;
+    // d0 = c (bits < K)
+    for (uint32_t i = lane; i < nw; i += 64) d0[i] = cw[i];
+    // encoder 1 (natural order) -> d1, encoder 2 on the QPP rows c[pi(i)] -> d2
+    const uint32_t f1 = rsc_wave([&](uint32_t i) { return lbit(cw, i); }, K, Lc, cb.mA, lane, d1);
+    const uint32_t f2x2 = 2 * cb.f2 % K;
+    uint32_t pi = 0, dl = 0, inext = 0xFFFFFFFFu;
+    auto qpp = [&](uint32_t i) {  // i runs consecutively per lane: recurrence after the first index
+        if (i != inext) {
+            pi = static_cast<uint32_t>(((uint64_t)cb.f1 * i + (uint64_t)cb.f2 * ((uint64_t)i * i % K)) % K);
+            dl = static_cast<uint32_t>(((uint64_t)cb.f1 + (uint64_t)cb.f2 * (2ull * i + 1)) % K);
+        }
+        const uint32_t r = pi;
         pi += dl;
         pi = pi >= K ? pi - K : pi;
         dl += f2x2;
         dl = dl >= K ? dl - K : dl;
+        inext = i + 1;
+        return r;
+    };
+    const uint32_t f2 = rsc_wave([&](uint32_t i) { return lbit(cw, qpp(i)); }, K, Lc, cb.mA, lane, d2);
+    __builtin_amdgcn_wave_barrier();
+    // trellis termination (TS 36.212 §5.1.3.2.2): x / z of three feedback steps per encoder
+    if (lane == 0) {
+        uint32_t x1[3], z1[3], x2[3], z2[3], s = f1;
+        for (int t = 0; t < 3; ++t) {
+            const uint32_t s1 = s & 1u, s2 = (s >> 1) & 1u, s3 = (s >> 2) & 1u;
+            x1[t] = s2 ^ s3, z1[t] = s1 ^ s3;
+            s = (s1 << 1) | (s2 << 2);
+        }
+        s = f2;
+        for (int t = 0; t < 3; ++t) {
+            const uint32_t s1 = s & 1u, s2 = (s >> 1) & 1u, s3 = (s >> 2) & 1u;
+            x2[t] = s2 ^ s3, z2[t] = s1 ^ s3;
+            s = (s1 << 1) | (s2 << 2);
+        }
+        const uint32_t t0[4] = {x1[0], z1[1], x2[0], z2[1]}, t1[4] = {z1[0], x1[2], z2[0], x2[2]},
+                       t2[4] = {x1[1], z1[2], x2[1], z2[2]};
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t k = K + t, sh = 31u - (k & 31u);
+            d0[k >> 5] |= t0[t] << sh;
+            d1[k >> 5] |= t1[t] << sh;
+            d2[k >> 5] |= t2[t] << sh;
+        }
     }
-    uint32_t x2[3], z2[3];
-    for (int t = 0; t < 3; ++t) {
-        x2[t] = s2 ^ s3, z2[t] = s1 ^ s3;
-        s3 = s2, s2 = s1, s1 = 0;
-    }
-    // tails (TS 36.212 §5.1.3.2.2; fec.cpp turbo_encode)
-    const uint32_t t0[4] = {x1[0], z1[1], x2[0], z2[1]}, t1[4] = {z1[0], x1[2], z2[0], x2[2]},
-                   t2[4] = {x1[1], z1[2], x2[1], z2[2]};
-    for (int t = 0; t < 4; ++t) {
-        d0[(size_t)(K + t) * 64 + l] = (uint8_t)t0[t];
-        d1[(size_t)(K + t) * 64 + l] = (uint8_t)t1[t];
-        d2[(size_t)(K + t) * 64 + l] = (uint8_t)t2[t];
-    }
-    if (!active) return;
-    // rate matching: bit j <- circular-buffer list entry (start + j) mod 3 (K + 4)
-    const uint32_t* valid = A.tab + w.valid_off;
+    __builtin_amdgcn_wave_barrier();
+    // rate matching: output bit j = stream[st][idx] of list entry (start + j) mod 3 D
+    const uint32_t* valid = A.tab + cb.valid_off;
     const uint32_t nvalid = 3 * D;
-    uint8_t* e = A.ebits + cb.e_off;
-    uint32_t qv = cb.start;
-    for (uint32_t j = 0; j < cb.E; ++j) {
-        const uint32_t ent = valid[qv], st = ent >> 16, idx = ent & 0xFFFF;
-        e[j] = d0[(size_t)st * D * 64 + (size_t)idx * 64 + l];
-        if (++qv == nvalid) qv = 0;
+    unsigned long long* out = reinterpret_cast<unsigned long long*>(A.ebits) + (cb.oo >> 6);
+    const uint32_t nm = (cb.E + 63) / 64;
+    uint32_t base = cb.start;  // list index of output bit 64 m
+    unsigned long long acc = 0;
+    for (uint32_t m = 0; m < nm; ++m) {
+        uint32_t q = base + lane;
+        q = q >= nvalid ? q - nvalid : q;
+        const uint32_t j = 64 * m + lane;
+        uint32_t bit = 0;
+        if (j < cb.E) {
+            const uint32_t ent = valid[q], st = ent >> 16, idx = ent & 0xFFFFu;
+            bit = lbit(st == 0 ? d0 : st == 1 ? d1 : d2, idx);
+        }
+        const unsigned long long bal = __ballot(bit);
+        // ballot bit i = output bit 64 m + i -> bytes in stream order, MSB first
+        const unsigned long long v = __builtin_bswap64(__builtin_bitreverse64(bal));
+        if ((m & 63u) == lane) acc = v;
+        if ((m & 63u) == 63u || m + 1 == nm) {
+            if (!A.d) {
+                if (lane <= (m & 63u)) out[(m & ~63u) + lane] = acc;
+            } else {
+                // direct: the block's bytes straight into its packet's d row (whole bytes, host-checked),
+                // 64 consecutive bytes per store instruction through the wave's LDS stage
+                stage[wv][lane] = acc;
+                __builtin_amdgcn_wave_barrier();
+                const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage[wv]);
+                const uint32_t b0 = 8 * (m & ~63u), nbt = min(512u, cb.E / 8 - b0);
+                uint8_t* dst = A.d + (size_t)cb.pkt * A.d_stride + cb.pstart / 8 + b0;
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k)
+                    if (64 * k + lane < nbt) dst[64 * k + lane] = sb[64 * k + lane];
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        base += 64;
+        base = base >= nvalid ? base - nvalid : base;  // nvalid >= 3 (40 + 4) > 64
     }
 }
 
+// packed scratch (each code block from a 64-bit aligned bit offset) -> MSB-first d rows: thread =
+// output byte of a packet; the code block holding each of its bits by the packet's block starts
 __global__ void __launch_bounds__(256) fec_pack_kernel(FecPackArgs A) {
+    const uint8_t* scr = A.ebits;
     for (uint32_t p = blockIdx.y; p < A.n; p += gridDim.y) {  // packets grid-stride: any n
-        const uint32_t G = A.G[p], nb = (G + 7) / 8;
-        const uint8_t* e = A.ebits + A.e_off[p];
+        const uint32_t G = A.G[p], nb = (G + 7) / 8, c0 = A.cb_first[p], c1 = A.cb_first[p + 1];
         for (uint32_t B = blockIdx.x * blockDim.x + threadIdx.x; B < nb; B += gridDim.x * blockDim.x) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) v = (v << 1) | (8 * B + t < G ? e[8 * B + t] : 0u);
+            const uint32_t j0 = 8 * B;
+            uint32_t lo = c0, hi = c1 - 1;  // last block starting at or before j0
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (A.pstart[mid] <= j0) lo = mid;
+                else hi = mid - 1;
+            }
+            uint32_t r = lo;
+            const uint32_t end = r + 1 < c1 ? A.pstart[r + 1] : G;
+            uint32_t v;
+            if ((A.pstart[r] & 7u) == 0 && j0 + 8 <= end) {  // whole byte of one block, byte-aligned
+                v = scr[(A.oo[r] + (j0 - A.pstart[r])) >> 3];
+            } else {
+                v = 0;
+                for (uint32_t t = 0; t < 8; ++t) {
+                    const uint32_t j = j0 + t;
+                    uint32_t bit = 0;
+                    if (j < G) {
+                        while (r + 1 < c1 && j >= A.pstart[r + 1]) ++r;
+                        const uint64_t q = A.oo[r] + (j - A.pstart[r]);
+                        bit = (scr[q >> 3] >> (7u - (q & 7u))) & 1u;
+                    }
+                    v = (v << 1) | bit;
+                }
+            }
             A.d[(size_t)p * A.d_stride + B] = (uint8_t)v;
         }
     }
 }
 
-int launch_fec_encode(const FecEncArgs& a, uint32_t n_waves, hipStream_t s) {
-    if (n_waves == 0) return 0;
-    hipLaunchKernelGGL(fec_encode_kernel, dim3(n_waves), dim3(64), 0, s, a);
+int launch_fec_encode(const FecEncArgs& a, uint32_t n_cb, hipStream_t s) {
+    if (n_cb == 0) return 0;
+    hipLaunchKernelGGL(fec_encode_kernel, dim3((n_cb + FEC_ENC_WAVES - 1) / FEC_ENC_WAVES), dim3(64 * FEC_ENC_WAVES), 0, s,
+                       a, n_cb);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_fec_pack(const FecPackArgs& a, hipStream_t s) {

@@ -77,9 +77,9 @@ struct FecTbArgs {       // transport-block CRC24A of packets with C > 1
     uint32_t n;
 };
 
-struct FecEncCb {        // one code block of dnrp_pdc_encode_batch
+struct FecEncCb {        // one code block of dnrp_pdc_encode_batch / dnrp_pcc_encode_batch
     uint64_t tb_off;     // byte offset of the packet's transport block
-    uint64_t e_off;      // offset of its first rate-matched bit in the unpacked bit scratch
+    uint64_t oo;         // bit offset of its rate-matched bits in the packed scratch (multiple of 64)
     uint32_t pkt;        // packet index (TB CRC)
     uint32_t tbs;        // N_TB_bits of the packet
     uint32_t rp;         // first bit of b = a || CRC24A the block takes
@@ -88,21 +88,32 @@ struct FecEncCb {        // one code block of dnrp_pdc_encode_batch
     uint32_t crc24b;     // 1: append a code-block CRC
     uint32_t crc16;      // 1: PLCF: b = a || CRC16 ^ mask computed here (pcc_enc.cpp:166-183)
     uint32_t mask;       // PLCF CRC mask
+    uint32_t K, f1, f2;  // block size, QPP coefficients
+    uint32_t valid_off;  // the size's circular-buffer list in the table
+    uint32_t pstart;     // first bit of its rate-matched bits in the packet's d row
+    uint32_t mA;         // RSC state map A^Lc (Lc = fec_enc_chunk(K)) as three 3-bit columns
 };
+
+// bits per lane of a K-bit code block in fec_encode_kernel (a multiple of 32, at most 96)
+__host__ __device__ constexpr uint32_t fec_enc_chunk(uint32_t K) {
+    return ((K + 63) / 64 + 31) / 32 * 32 > 32 ? ((K + 63) / 64 + 31) / 32 * 32 : 32;
+}
 
 struct FecEncArgs {
     const uint8_t* tb;
     const uint32_t* tab;
-    const FecEncCb* cbs;
-    const FecWave* waves;     // K, n, valid_off, f1, f2, first_cb; data_off = offset in cd (bytes)
+    const FecEncCb* cbs;      // packet order
     const uint32_t* tbcrc;    // per packet
-    uint8_t* cd;              // per wave: c [K][64] then d0, d1, d2 [K + 4][64]
-    uint8_t* ebits;           // unpacked rate-matched bits
+    uint8_t* ebits;           // packed rate-matched bits (FecEncCb::oo)
+    uint8_t* d;               // non-null: direct mode, every block's bits whole bytes of its d row
+    uint32_t d_stride;
 };
 
-struct FecPackArgs {          // ebits -> packed MSB-first d rows
+struct FecPackArgs {          // packed scratch -> MSB-first d rows
     const uint8_t* ebits;
-    const uint64_t* e_off;    // per packet
+    const uint32_t* cb_first; // per packet its first code block, [n + 1]
+    const uint32_t* pstart;   // per code block: first bit in its packet's row
+    const uint64_t* oo;       // per code block: bit offset in the scratch
     const uint32_t* G;
     uint8_t* d;
     uint32_t d_stride, n, max_bytes;
@@ -112,7 +123,7 @@ int launch_fec_dematch(const FecArgs& a, hipStream_t s);
 int launch_fec_tdec(const FecArgs& a, uint32_t n_waves, hipStream_t s);
 int launch_fec_compact(const FecCompactArgs& a, uint32_t n_waves, hipStream_t s);
 int launch_fec_tbcrc(const FecTbArgs& a, hipStream_t s);
-int launch_fec_encode(const FecEncArgs& a, uint32_t n_waves, hipStream_t s);
+int launch_fec_encode(const FecEncArgs& a, uint32_t n_cb, hipStream_t s);
 int launch_fec_pack(const FecPackArgs& a, hipStream_t s);
 
 }  // namespace dnrp::dev

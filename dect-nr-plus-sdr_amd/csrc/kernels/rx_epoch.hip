@@ -18,6 +18,7 @@
 // exactly one epoch (host-checked), so no workgroup reads a row another one writes.
 // Reference: rx_synced.cpp:711-771 (front end), 893-949 + 1028-1163 + 1335-1392 (equalisation).
 #include "device_common.hpp"
+#include "experiments.hpp"
 #include "kernels.hpp"
 #include "rx_eq.hpp"
 #include "rx_front.hpp"
@@ -46,7 +47,7 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
     {
         const uint32_t region = rxw_region(LR, MR, pp_block<LR, MR, HLR>::W);
         float2* R = smem + w * region;
-        const uint32_t s0 = X.ep_off[ep], ntask = (X.ep_off[ep + 1] - s0) * NRX;
+        const uint32_t s0 = X.ep_off[ep], ntask = experiment(XS_EP_SKIP_FE) ? 0u : (X.ep_off[ep + 1] - s0) * NRX;
         const uint32_t lane0 = tid & 63u;
         const rx_pkt_in in = F.pin[pkt];
         const rx_pkt_state S = F.st[pkt];
@@ -73,6 +74,7 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
         }
     }
     __syncthreads();  // the epoch's rows written (workgroup-scope release / acquire), LDS free again
+    if constexpr (experiment(XS_EP_SKIP_EQ)) return;
 
     // ---- 2. equalisation of the epoch (rx_cells_kernel, MRC / SFBC)
     const uint32_t zst = zfi_stride(A.n_drs);

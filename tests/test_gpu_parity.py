@@ -293,6 +293,16 @@ def test_rx_parity_epoch_stride(name, stride, monkeypatch):
     _rx_parity_epoch(name, stride, monkeypatch)
 
 
+@pytest.mark.parametrize("name", ["C4", "C3", "C2", "tm5_u2b4", "mrc4_16qam", "lmode_C4", "tm1_txdiv2", "subslot_tm5"])
+def test_rx_parity_ypath(name, monkeypatch):
+    """DNRP_RX_EPOCH=0: the PDC phase through the batch-wide front end into Y and rx_cells (the path the
+    epoch receiver replaced as the default) -- same oracle and gates, and no epoch launch."""
+    monkeypatch.setenv("DNRP_RX_EPOCH", "0")
+    monkeypatch.setenv("DNRP_TIMING", "1")
+    phy = _rx_parity(name)
+    assert phy.kernel_time_total("rx_epoch")[1] == 0, name
+
+
 def test_rx_largest_cells_geometry(monkeypatch):
     """8 RX antennas x 4 transmit streams at b = 16 (TM5 into an N_TX_max = 8 context): the largest
     N_RX / NT / b of the cells kernel's LDS staging (pilot rows of 8 x 4 streams, both weight tables).
@@ -585,9 +595,9 @@ def test_full_chunk_edges(name, n):
 
 
 @pytest.mark.parametrize("name,n", [("C4", 16384), ("C3", 8192)])
-def test_full_chunk_edges_epoch(name, n, monkeypatch):
-    """The bench chunk through the epoch receiver (DNRP_RX_EPOCH=1): grid and Y offsets past 2^32."""
-    monkeypatch.setenv("DNRP_RX_EPOCH", "1")
+def test_full_chunk_edges_ypath(name, n, monkeypatch):
+    """The bench chunk through the Y path (DNRP_RX_EPOCH=0): grid and Y offsets past 2^32."""
+    monkeypatch.setenv("DNRP_RX_EPOCH", "0")
     _full_chunk_edges(name, n)
 
 
