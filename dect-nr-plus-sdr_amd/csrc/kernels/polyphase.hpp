@@ -151,7 +151,35 @@ struct pp_const {
         }
     }
 
+    // the same sums with the window read from LDS as it is consumed: input i is loaded LOOK delay
+    // rows before its first use (d = HL + o_max - i), so about o_max + 1 + LOOK inputs are live instead
+    // of all W (the register budget of occupancy-bound callers); bit-identical to run()
+    template <int LOOK = 2>
+    __device__ static __forceinline__ void run_lds(const float2* xw, float2 (&y)[L]) {
+        constexpr int OM = ((L - 1) * M) / L;
+        float2 x[W];
+#pragma unroll
+        for (int i = 0; i <= OM + LOOK && i < W; ++i) x[i] = xw[i];
+#pragma unroll
+        for (int k = 0; k < L; ++k) y[k] = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int d = HL; d >= 0; --d) {
+            // the input that becomes needed LOOK rows from now; a compiler barrier every other row
+            // keeps the loads where they are (hoisted, all W would be live again)
+            constexpr_load(xw, x, HL + OM - d + LOOK + 1);
+            if ((HL - d) % 2 == 1) asm volatile("" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const int o = (k * M) / L, ph = (k * M) % L;
+                constexpr_if_nonzero(TP::h[ph + d * L], x[HL + o - d], y[k]);
+            }
+        }
+    }
+
   private:
+    __device__ static __forceinline__ void constexpr_load(const float2* xw, float2 (&x)[W], const int i) {
+        if (i > ((L - 1) * M) / L && i < W) x[i] = xw[i];
+    }
     __device__ static __forceinline__ void constexpr_if_nonzero(const float t, const float2 xv, float2& acc) {
         if (t != 0.f) {  // compile-time after unrolling: padding taps cost nothing (fma(x, 0, a) == a)
             acc.x = fmaf(xv.x, t, acc.x);

@@ -260,10 +260,37 @@ __global__ void __launch_bounds__(64 * WPG) sync_steps_wave_kernel(sync_args A) 
 // resampled, so every wave keeps its own loads in flight instead of waiting on a staging pass.
 // Per wave LDS: the chunk's input window (carry W - M + M * 64) and a 1024-sample output ring
 // holding the pattern lookback; no workgroup barrier anywhere.
+#ifndef DNRP_SS_SUMG
+#define DNRP_SS_SUMG 8  // step-sum samples per group of LDS reads in flight (two halves of 8)
+#endif
+#ifndef DNRP_SS_LAZY
+#define DNRP_SS_LAZY 0  // 1: the FIR window read from LDS as consumed (pp_const::run_lds), not all at once
+#endif
+#ifndef DNRP_SS_LOOK
+#define DNRP_SS_LOOK 2  // FIR window inputs loaded this many delay rows ahead (pp_const::run_lds)
+#endif
+#ifndef DNRP_SS_WPE
+#define DNRP_SS_WPE 1  // waves per SIMD the register budget must allow (1: the compiler's choice)
+#endif
 #ifndef DNRP_SS_RING
 #define DNRP_SS_RING 1024  // power of two >= 64 * 9 + step + pattern + 9 (host-checked)
 #endif
 constexpr uint32_t SS_RING = DNRP_SS_RING;
+// the pipelined kernel's ring (sync_steps_pipe_kernel). Measured alternative (DESIGN.md
+// §7): 912 slots (a multiple of 16, so a 16-slot step-sum read never wraps; holds the C4 lookback of
+// 64 * 9 + step + pattern + 9 = 905) with the FIR window read lazily (DNRP_SS_LAZY=1) and 4-sample
+// step-sum groups (DNRP_SS_SUMG=4): 126 VGPRs and 12.3 KiB, 12 waves per CU instead of 11 -- sync_steps
+// 14.17 -> 15.07 ms per 16384-slot chunk (the mod-912 indices and shorter read groups cost more than
+// the wave gains); 1024 / lazy / 4: 14.33 ms. Kept: 1024, one load group, two halves of 8.
+#ifndef DNRP_SS_PRING
+#define DNRP_SS_PRING 1024
+#endif
+constexpr uint32_t SS_PRING = DNRP_SS_PRING;
+static_assert(SS_PRING % 16 == 0, "16-slot step-sum reads stay inside the ring");
+__device__ __forceinline__ uint32_t pring(int64_t m) {  // m mod SS_PRING for m >= -2^31
+    if constexpr ((SS_PRING & (SS_PRING - 1)) == 0) return static_cast<uint32_t>(m) & (SS_PRING - 1);
+    return static_cast<uint32_t>((m + (int64_t(1) << 31) / SS_PRING * SS_PRING + SS_PRING) % SS_PRING);
+}
 constexpr uint32_t SS_WPG = 4;
 
 template <int LR, int MR, int HLR>
@@ -419,20 +446,30 @@ __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, f
         }
     }
     __builtin_amdgcn_wave_barrier();
-    float2 xv[W];
-    if constexpr ((MR & 1) == 0) PD::template load<true>(inb + MR * lane, xv);
-    else PD::template load<false>(inb + MR * lane, xv);
     float2 y[LR];
     if constexpr (CT) {
+#if DNRP_SS_LAZY
+        pp_const<taps_sync_9_10>::run_lds<DNRP_SS_LOOK>(inb + MR * lane, y);
+#else
+        float2 xv[W];
+        if constexpr ((MR & 1) == 0) PD::template load<true>(inb + MR * lane, xv);
+        else PD::template load<false>(inb + MR * lane, xv);
         pp_const<taps_sync_9_10>::run(xv, y);
+#endif
     } else {
+        float2 xv[W];
+        if constexpr ((MR & 1) == 0) PD::template load<true>(inb + MR * lane, xv);
+        else PD::template load<false>(inb + MR * lane, xv);
         const float* tp = A.taps;
         asm volatile("" : "+s"(tp));
         PD::run(xv, (ctap_ptr)(tp), y);
     }
     const int64_t mb = ms + LR * (qa + 64 * static_cast<int64_t>(c) + lane);
+    {
+        const uint32_t rb = pring(mb);  // the block's 9 outputs: at most one wrap
 #pragma unroll
-    for (int k = 0; k < LR; ++k) ring[static_cast<uint32_t>(mb + k) & (SS_RING - 1)] = y[k];
+        for (int k = 0; k < LR; ++k) ring[rb + k >= SS_PRING ? rb + k - SS_PRING : rb + k] = y[k];
+    }
     if (lane < CARRY) inb[lane] = inb[NEW + lane];
     __builtin_amdgcn_wave_barrier();
     const int64_t m_end = ms + LR * (qa + 64 * static_cast<int64_t>(c) + 64);
@@ -443,21 +480,22 @@ __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, f
     const bool live = s < s_end;
     const uint32_t n0 = (live ? s : s_next) * 64u + part * 16u;
     const bool corr = live && static_cast<int64_t>(s) * step >= A.pattern;
-    const float2* rv = ring + (n0 & (SS_RING - 1));
-    const float2* ru = ring + ((n0 - A.pattern) & (SS_RING - 1));
+    const float2* rv = ring + pring(n0);
+    const float2* ru = ring + pring(static_cast<int64_t>(n0) - A.pattern);
     float pw = 0.f;
     float2 cc = make_float2(0.f, 0.f);
+    constexpr int SG = DNRP_SS_SUMG;  // samples per group of reads in flight (same summation order)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {  // two halves of 8 samples: 32 VGPRs of reads in flight, not 64
-        float2 v[8], u[8];
+    for (int h = 0; h < 16 / SG; ++h) {
+        float2 v[SG], u[SG];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t jj = (8 * h + j + rot) & 15u;
+        for (int j = 0; j < SG; ++j) {
+            const uint32_t jj = (SG * h + j + rot) & 15u;
             v[j] = rv[jj];
             u[j] = ru[jj];
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < SG; ++j) {
             pw = fmaf(v[j].x, v[j].x, fmaf(v[j].y, v[j].y, pw));
             cc.x = fmaf(u[j].x, v[j].x, fmaf(u[j].y, v[j].y, cc.x));
             cc.y = fmaf(u[j].y, v[j].x, fmaf(-u[j].x, v[j].y, cc.y));
@@ -486,7 +524,7 @@ __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, f
 }
 
 template <int LR, int MR, int HLR, bool CT>
-__global__ void __launch_bounds__(64) sync_steps_pipe_kernel(sync_args A, uint32_t seg_steps, uint32_t n_seg) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DNRP_SS_WPE))) sync_steps_pipe_kernel(sync_args A, uint32_t seg_steps, uint32_t n_seg) {
     using PD = pp_direct<LR, MR, HLR>;
     constexpr int W = PD::W, CARRY = W - MR, NEW = 64 * MR;
     constexpr uint32_t INB = ss_inbuf<LR, MR, HLR>();
@@ -1503,13 +1541,14 @@ hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
         // taps where the run-time taps are the generated ones (neutral, 3.48 ms both)
         const char* pp_e = std::getenv("DNRP_SYNC_PIPE");
         const bool pipe = !pp_e || std::atoi(pp_e);
-        if (a.step == 64 && pipe && a.pattern % 16 == 0) {
+        if (a.step == 64 && pipe && a.pattern % 16 == 0 && 64u * 9u + a.step + a.pattern + 9u <= SS_PRING) {
+            const size_t plds = size_t(ss_inbuf<9, 10, 24>() + SS_PRING) * sizeof(float2);
             if (a.ct_taps)
                 hipLaunchKernelGGL((sync_steps_pipe_kernel<9, 10, 24, true>), dim3(static_cast<uint32_t>(waves)), dim3(64),
-                                   lds / SS_WPG, st, a, seg_steps, n_seg);
+                                   plds, st, a, seg_steps, n_seg);
             else
                 hipLaunchKernelGGL((sync_steps_pipe_kernel<9, 10, 24, false>), dim3(static_cast<uint32_t>(waves)), dim3(64),
-                                   lds / SS_WPG, st, a, seg_steps, n_seg);
+                                   plds, st, a, seg_steps, n_seg);
         } else if (a.step == 64)
             hipLaunchKernelGGL((sync_steps_stream_kernel<9, 10, 24, 16, 1>), dim3(static_cast<uint32_t>(waves)), dim3(64),
                                lds / SS_WPG, st, a, seg_steps, n_seg);
