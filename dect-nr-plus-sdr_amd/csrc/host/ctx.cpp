@@ -643,7 +643,7 @@ dev::rx_front_args front_args(dnrp_ctx* ctx, rx1_tables* t, const float* iq, con
         a.stf_ys_stride = 14 * ctx->cfg.b_max;
     }
     // compile-time-tap front end (rx.hip rx_fft_wave_kernel<.., true>) where the run-time taps are
-    // the generated ones bit for bit (the tap-table variant measured slower)
+    // the generated ones bit for bit (the tap-table variant measured slower, docs/DESIGN_LOG.md §6)
     a.stream = dev::rx_stream_taps_match(t->rs.h.data(), t->rs.h.size()) ? 1u : 0u;
     if (plan && dev::rx_fft_wave_path(a)) {
         a.snr_part = ctx->snr_part.as<double2>();
@@ -981,7 +981,7 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
         if (fits) {
             a.stream = 1;
             // polyphase blocks on the matrix cores (tx.hip, polyphase.hpp mf_blocks): opt-in A/B,
-            // DNRP_TX_MFMA=1 (read per call); the VALU blocks measured faster
+            // DNRP_TX_MFMA=1 (read per call); the VALU blocks measured faster (docs/DESIGN_LOG.md)
             const char* mf_env = std::getenv("DNRP_TX_MFMA");
             a.mfma = (mf_env && std::atoi(mf_env)) ? 1u : 0u;
             a.code_bin = t->code_bin.as<uint32_t>();
@@ -1063,13 +1063,13 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         // A/B switches, read once per PCC call so that its PDC call agrees with it:
         // DNRP_RX_SNR_FRONT=0 -> rx_snr gathers the DRS cells from Y (no front-end sums, no pilots,
         // so no fused receiver); DNRP_RX_FUSED=1 -> the PDC phase through the fused receiver
-        // (rx_fused.hip) instead of Y and rx_cells: parity-tested, slower on MI355X
+        // (rx_fused.hip) instead of Y and rx_cells: parity-tested, slower on MI355X (docs/DESIGN_LOG.md §6)
         const char* e = std::getenv("DNRP_RX_SNR_FRONT");
         ctx->rx_snr_front = !e || std::atoi(e);
         const char* f = std::getenv("DNRP_RX_FUSED");
         ctx->rx_fused = ctx->rx_snr_front && f && std::atoi(f);
         // DNRP_RX_EPOCH=0 -> the PDC phase through Y + rx_cells instead of the epoch receiver
-        // (rx_epoch.hip, the default where it applies: 1.2 ms faster per 16384-slot C4 chunk, DESIGN.md)
+        // (rx_epoch.hip, the default where it applies: 1.2 ms faster per 16384-slot C4 chunk, DESIGN.md §6)
         const char* ep = std::getenv("DNRP_RX_EPOCH");
         ctx->rx_epoch = !ep || std::atoi(ep);
         const char* gr = std::getenv("DNRP_RX_GROUP");

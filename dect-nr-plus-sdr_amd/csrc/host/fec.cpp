@@ -635,7 +635,7 @@ int dnrp_pdc_decode(dnrp_harq_rx* hb, const dnrp_fec_cfg* cfg, const int16_t* ll
 // ---- device turbo decoding -----------------------------------------------------------------------
 // PDC decoding runs the first 3 iterations for every code block, then continues the undecided ones in
 // dense waves (run_tdec; same-box A/B at 5 dB: a split after 2 / 3 / 4 iterations 156 / 145 / 161 ms
-// per 4096 C4 TBs, one pass 0.95 s)
+// per 4096 C4 TBs, one pass 0.95 s, docs/DESIGN_LOG.md §5a)
 static uint32_t pdc_split() { return 3u; }
 
 static int fec_tables(dnrp_ctx* ctx) {

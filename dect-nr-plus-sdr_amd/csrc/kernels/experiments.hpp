@@ -1,7 +1,7 @@
 // Compile-time experiment switches (tools/build_variant.sh NAME "-DDNRP_EXPERIMENTS=<bits>" ...).
 // Two kinds: phase-skip and attribution builds of the hot kernels, whose results are meaningless
 // and only their timings and counters are read; and measured alternatives that compute the same
-// results but lost their A/B, kept buildable for re-measurement. The shipped build
+// results but lost their A/B (docs/DESIGN_LOG.md §6), kept buildable for re-measurement. The shipped build
 // defines no bit, so every switch below is a constant false and the guarded code is the product's.
 #pragma once
 

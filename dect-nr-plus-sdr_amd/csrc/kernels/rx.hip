@@ -450,7 +450,7 @@ hipError_t launch_rx_stf(const rx_front_args& a_in, uint32_t n, hipStream_t st) 
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     if (a.stf_chunk)  // N_b_DFT_os = 8192: the chunked layout, run-time taps
         hipLaunchKernelGGL((rx_stf_ant_kernel<-1, false, true>), dim3(n * a.N_RX), dim3(256), lds, st, a);
-    else if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24)  // compiled-in taps (table taps: 0.50 vs 0.38 ms)
+    else if (a.stream && a.L == 9 && a.M == 10 && a.hl == 24)  // compiled-in taps (table taps: 0.50 vs 0.38 ms, docs/DESIGN_LOG.md §6)
         hipLaunchKernelGGL((rx_stf_ant_kernel<24, true>), dim3(n * a.N_RX), dim3(256), lds, st, a);
     else
         DNRP_HL_DISPATCH(rx_stf_ant_kernel, dim3(n * a.N_RX), dim3(256), lds, st, a);

@@ -26,6 +26,12 @@
 namespace dnrp::dev {
 
 constexpr uint32_t EP_THREADS = 512, EP_WAVES = EP_THREADS / 64;
+#ifndef DNRP_EP_YNT
+#define DNRP_EP_YNT 0  // 1: nontemporal Y stores (A/B; plain stores keep the rows for the equaliser)
+#endif
+#ifndef DNRP_EP_AMAJOR
+#define DNRP_EP_AMAJOR 0  // 1: tasks antenna-major (a wave's tasks are consecutive symbols of one antenna)
+#endif
 
 __host__ __device__ inline size_t ep_front_lds() { return size_t(EP_WAVES) * rxw_region(9, 10, pp_block<9, 10, 24>::W) * sizeof(float2); }
 
@@ -59,7 +65,9 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
             uint32_t lane = tid & 63u;
             float2 w1 = w1_, wl = wl_;
             asm volatile("" : "+v"(lane), "+v"(w1.x), "+v"(w1.y), "+v"(wl.x), "+v"(wl.y));
-            const uint32_t l = X.ep_sym[s0 + t / NRX], a = t % NRX;
+            const uint32_t ns = X.ep_off[ep + 1] - s0;
+            const uint32_t l = DNRP_EP_AMAJOR ? X.ep_sym[s0 + t % ns] : X.ep_sym[s0 + t / NRX];
+            const uint32_t a = DNRP_EP_AMAJOR ? t / ns : t % NRX;
             const float2* src = F.iq + (size_t(in.win) * NRX + a) * F.S_in + in.fine_peak;
             const rx_span_t sp = rx_span<LR, MR, HLR>(F, l);
             if (t != w) __builtin_amdgcn_wave_barrier();  // the previous task's reads of R are done
@@ -70,7 +78,14 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
             __builtin_amdgcn_wave_barrier();
             rx_resample_ct<LR, MR, HLR>(F, in, S, sp, R, lane);
             float2* Yrow = F.Y + ((size_t(pkt) * NRX + a) * F.n_sym_total + l) * F.Nf_pad;
-            rx_fft_bins<true>(F, S, R, lane, [&](uint32_t k, float2 v) { Yrow[k] = v; }, w1, wl);
+            rx_fft_bins<true>(F, S, R, lane, [&](uint32_t k, float2 v) {
+                if constexpr (DNRP_EP_YNT) {
+                    typedef float f2v __attribute__((ext_vector_type(2)));
+                    __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v*>(Yrow + k));
+                } else {
+                    Yrow[k] = v;
+                }
+            }, w1, wl);
         }
     }
     __syncthreads();  // the epoch's rows written (workgroup-scope release / acquire), LDS free again

@@ -343,7 +343,7 @@ __device__ __forceinline__ void eq_compute(const rx_cells_args& A, const cell_se
 // The NT x NT Hermitian solve runs per lane in registers (Cholesky, L^-1): per cell it is ~NRX NT^2
 // complex MACs for the Gram matrix and ~NT^3 for the solve -- a lane-per-subcarrier batch of tiny
 // independent systems, which the lane layout keeps off the matrix cores (measured: the Gram matrix
-// on v_mfma_f32_4x4x1_16b_f32, XS_MMSE_MFMA below, is 1.7x slower).
+// on v_mfma_f32_4x4x1_16b_f32, XS_MMSE_MFMA below, is 1.7x slower; docs/DESIGN_LOG.md §6).
 template <int NRX, int NT>
 struct unit_sm {
     uint32_t si, jj;

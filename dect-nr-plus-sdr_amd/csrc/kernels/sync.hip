@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(64 * WPG) sync_steps_wave_kernel(sync_args A) 
 #endif
 constexpr uint32_t SS_RING = DNRP_SS_RING;
 // the pipelined kernel's ring (sync_steps_pipe_kernel). Measured alternative (DESIGN.md
-// §7): 912 slots (a multiple of 16, so a 16-slot step-sum read never wraps; holds the C4 lookback of
+// §6.2): 912 slots (a multiple of 16, so a 16-slot step-sum read never wraps; holds the C4 lookback of
 // 64 * 9 + step + pattern + 9 = 905) with the FIR window read lazily (DNRP_SS_LAZY=1) and 4-sample
 // step-sum groups (DNRP_SS_SUMG=4): 126 VGPRs and 12.3 KiB, 12 waves per CU instead of 11 -- sync_steps
 // 14.17 -> 15.07 ms per 16384-slot chunk (the mod-912 indices and shorter read groups cost more than
@@ -465,7 +465,10 @@ __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, f
         PD::run(xv, (ctap_ptr)(tp), y);
     }
     const int64_t mb = ms + LR * (qa + 64 * static_cast<int64_t>(c) + lane);
-    {
+    if constexpr ((SS_PRING & (SS_PRING - 1)) == 0) {
+#pragma unroll
+        for (int k = 0; k < LR; ++k) ring[static_cast<uint32_t>(mb + k) & (SS_PRING - 1)] = y[k];
+    } else {
         const uint32_t rb = pring(mb);  // the block's 9 outputs: at most one wrap
 #pragma unroll
         for (int k = 0; k < LR; ++k) ring[rb + k >= SS_PRING ? rb + k - SS_PRING : rb + k] = y[k];
@@ -1538,7 +1541,7 @@ hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
         // one wave per workgroup: a retired segment frees its LDS at once (A/B on MI355X: sync_steps
         // 4.32 -> 3.81 ms, 176.4k -> 186.0k slot-pairs/s against four); DNRP_SYNC_PIPE=0: the
         // single-chunk-prefetch form (read per call: tests switch it at run time). Compile-time sync
-        // taps where the run-time taps are the generated ones (neutral, 3.48 ms both)
+        // taps where the run-time taps are the generated ones (neutral, 3.48 ms both; docs/DESIGN_LOG.md §6)
         const char* pp_e = std::getenv("DNRP_SYNC_PIPE");
         const bool pipe = !pp_e || std::atoi(pp_e);
         if (a.step == 64 && pipe && a.pattern % 16 == 0 && 64u * 9u + a.step + a.pattern + 9u <= SS_PRING) {

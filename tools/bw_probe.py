@@ -1,5 +1,5 @@
 """HBM probe: achievable read, write and read+write (copy) rates on this GPU for large buffers
-(torch kernels), the ceilings the streaming kernels are compared with."""
+(torch kernels), the ceilings the streaming kernels are compared with (docs/DESIGN_LOG.md §6)."""
 import json
 import torch
 
