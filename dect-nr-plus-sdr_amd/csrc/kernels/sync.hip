@@ -1095,6 +1095,69 @@ __device__ __forceinline__ void resample_direct(const sync_args& A, const float2
     }
 }
 
+// resample_direct for one workgroup with the window span staged in LDS first: the span's inputs
+// [ib0, ib0 + n_in) are read by all threads together (coalesced, range-checked: zeros outside
+// [0, S_win)) into stage[], then every thread takes the FIR windows of at most two blocks from LDS
+// (its own and one tail block -- 9 region outputs per block, so a region of stf_len + D + pad =
+// 4640 outputs is 517 blocks for 512 threads), computes them into registers, and after a barrier
+// (every window read: stage[] may alias the outputs' slots) hands the outputs to put. One global
+// load latency instead of two (the tail blocks' second round), the same sums as resample_direct.
+// Preconditions (host, sync_peak_ok): blocks <= 2 T, n_in <= the stage's capacity.
+template <int LR, int MR, int HLR, class PUT>
+__device__ __forceinline__ void resample_staged(const sync_args& A, const float2* x, int64_t y0, uint32_t cnt,
+                                                float2* stage, PUT put) {
+    using PD = pp_direct<LR, MR, HLR>;
+    constexpr int W = PD::W;
+    const uint32_t tid = threadIdx.x, T = blockDim.x;
+    const int64_t ms = A.m_star;
+    const int64_t q0 = floordiv(y0 - ms, LR), q1 = floordiv(y0 + cnt - ms + LR - 1, LR);
+    const uint32_t nb = static_cast<uint32_t>(q1 - q0);
+    const int64_t ib0 = static_cast<int64_t>(A.p_star) + MR * q0 - HLR;
+    const uint32_t n_in = MR * (nb - 1) + W;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(x), 0, static_cast<int>(A.S_win * 8u), 0x00020000);
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    // indices past the stream end read a range-checked zero; a negative start wraps into the
+    // descriptor's "outside" range as well (offsets are unsigned)
+    constexpr uint32_t G = 6;  // loads in flight per thread and group
+    for (uint32_t i0 = 0; i0 < n_in; i0 += G * T) {
+        float2 v[G];
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const int64_t q = ib0 + i0 + g * T + tid;
+            const u2 r = __builtin_amdgcn_raw_buffer_load_b64(xr, q >= 0 ? static_cast<uint32_t>(q * 8) : 0x80000000u, 0, 0);
+            v[g] = make_float2(__uint_as_float(r.x), __uint_as_float(r.y));
+        }
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g)
+            if (i0 + g * T + tid < n_in) stage[i0 + g * T + tid] = v[g];
+    }
+    __syncthreads();
+    float2 y[LR], y2[LR];
+    const uint32_t b2 = tid + T;
+    if (tid < nb) {
+        float2 xv[W];
+        PD::template load<false>(stage + MR * tid, xv);
+        pp_const<taps_sync_9_10>::run(xv, y);
+    }
+    if (b2 < nb) {
+        float2 xv[W];
+        PD::template load<false>(stage + MR * b2, xv);
+        pp_const<taps_sync_9_10>::run(xv, y2);
+    }
+    __syncthreads();  // every window read before the outputs overwrite the stage
+    auto emit = [&](uint32_t b, const float2 (&yy)[LR]) {
+        const int64_t mb = ms + LR * (q0 + b);
+#pragma unroll
+        for (int k = 0; k < LR; ++k) {
+            const int64_t idx = mb + k - y0;
+            if (idx >= 0 && idx < static_cast<int64_t>(cnt))
+                put(static_cast<uint32_t>(idx), (mb + k >= 0) ? yy[k] : make_float2(0.f, 0.f));
+        }
+    };
+    if (tid < nb) emit(tid, y);
+    if (b2 < nb) emit(b2, y2);
+}
+
 // ---- coarse-peak search of the split rounds (sync_peak_kernel)
 // autocorrelator_peak.cpp:145-264 for the pending detection of one (window, antenna), one workgroup
 // each. The per-sample metric is the same expression as peak_search's (exact prefix differences in
@@ -1123,6 +1186,9 @@ __host__ __device__ inline size_t peak8_alias(uint32_t region, uint32_t P, uint3
 
 // CT: the 9/10 sync resampler's taps compiled in (pp_const<taps_sync_9_10>, host-checked bit for
 // bit): immediates next to their FMAs instead of 225 run-time taps held in SGPRs (which spill)
+#ifndef DNRP_PEAK_STAGED
+#define DNRP_PEAK_STAGED 1  // the STF region's input span staged in LDS first (resample_staged)
+#endif
 #ifndef DNRP_PEAK_WPE
 #define DNRP_PEAK_WPE 4  // waves per SIMD the register budget allows
 #endif
@@ -1153,7 +1219,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DNRP_P
     const int64_t yb = static_cast<int64_t>(r0) - A.stf_len - SYNC_PAD_PEAK;
     const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
     // ---- resampled region lb[yb + i] -> lbuf[pidx(i)] (sync_resample's outputs, bit for bit)
-    resample_direct<LR, MR, HLR, CT>(A, x, yb, region, [&](uint32_t i, float2 v) { lbuf[pidx(i)] = v; });
+    if constexpr (CT && LR == 9 && DNRP_PEAK_STAGED)
+        resample_staged<LR, MR, HLR>(A, x, yb, region, lbuf, [&](uint32_t i, float2 v) { lbuf[pidx(i)] = v; });
+    else
+        resample_direct<LR, MR, HLR, CT>(A, x, yb, region, [&](uint32_t i, float2 v) { lbuf[pidx(i)] = v; });
     __syncthreads();
     PEAK_STAMP(1);
     // ---- 8-sample segment sums: products prod[j] = lb[j] conj(lb[j + P]), powers |lb[j]|^2; segment
@@ -1626,8 +1695,14 @@ bool sync_taps_match(const float* h, size_t n) {  // run-time sync taps == compi
 }
 
 bool sync_peak_ok(const sync_args& a) {  // the grid layout's preconditions (every DECT geometry meets them)
+    const uint32_t region = a.stf_len + a.D + SYNC_PAD_PEAK;
+    // resample_staged (9/10): at most 2 blocks per thread, the span inside lbuf + the alias area
+    const uint32_t nb = region / 9 + 2, n_in = 10 * nb + pp_direct<9, 10, 24>::W;
+    const bool staged_ok = !(a.L == 9 && a.M == 10 && a.hl == 24) ||
+                           (nb <= 2 * 512 && size_t(n_in) * sizeof(float2) <= size_t(peak8_lbuf(region)) * sizeof(float2) +
+                                                                               peak8_alias(region, a.pattern, a.D));
     return a.D % 8 == 0 && a.pattern % 8 == 0 && (a.stf_len + SYNC_PAD_PEAK) % 8 == 0 && a.D / 8 <= 512 &&
-           (a.n_uw == 6 || a.n_uw == 8) && sync_peak_lds(a) <= 160 * 1024;
+           (a.n_uw == 6 || a.n_uw == 8) && sync_peak_lds(a) <= 160 * 1024 && staged_ok;
 }
 
 hipError_t launch_sync_peak(const sync_args& a, uint32_t n, hipStream_t st) {
