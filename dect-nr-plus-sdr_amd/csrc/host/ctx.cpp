@@ -1068,10 +1068,12 @@ int dnrp_rx_pcc_batch(dnrp_ctx* ctx, uint32_t n, const dnrp_sync_report* sr, con
         ctx->rx_snr_front = !e || std::atoi(e);
         const char* f = std::getenv("DNRP_RX_FUSED");
         ctx->rx_fused = ctx->rx_snr_front && f && std::atoi(f);
-        // DNRP_RX_EPOCH=0 -> the PDC phase through Y + rx_cells instead of the epoch receiver
-        // (rx_epoch.hip, the default where it applies: 1.2 ms faster per 16384-slot C4 chunk)
+        // DNRP_RX_EPOCH: the PDC phase through the epoch receiver (rx_epoch.hip) -- 1 (default) with 4 or
+        // more RX antennas, where it measured faster (C4: 1.2 ms per 16384-slot chunk; SISO C3 loses,
+        // 7.2 vs 5.5 ms per 8192: one symbol task per wave and epoch), 2 for every geometry it supports,
+        // 0 never (Y + rx_cells); DESIGN.md §6
         const char* ep = std::getenv("DNRP_RX_EPOCH");
-        ctx->rx_epoch = !ep || std::atoi(ep);
+        ctx->rx_epoch = ep ? static_cast<uint32_t>(std::atoi(ep)) : 1u;
         const char* gr = std::getenv("DNRP_RX_GROUP");
         ctx->rx_group = gr ? static_cast<uint32_t>(std::atoi(gr)) : 0u;
         // zero-forced DRS pilots of every slot (the fused receiver's only): at most one DRS symbol per
@@ -1261,7 +1263,8 @@ int dnrp_rx_pdc_batch(dnrp_ctx* ctx, uint32_t m, const dnrp_pdc_req* req, const 
             fa.sym_first = t->pcc_max + 1;
             const uint32_t G = ctx->rx_group;
             dev::rx_cells_args ec{};
-            const bool epoch = ctx->rx_epoch && t2->ep_ok && !t2->sm && fa.stream && dev::rx_fft_wave_path(fa) &&
+            const bool epoch = (ctx->rx_epoch >= 2 || (ctx->rx_epoch == 1 && fa.N_RX >= 4)) && t2->ep_ok && !t2->sm &&
+                               fa.stream && dev::rx_fft_wave_path(fa) &&
                                t2->bplan.cells_ok && t2->bplan.n_epochs &&
                                dev::rx_epoch_supported(fa.N_RX, t->N_eff_TX) &&
                                dev::rx_epoch_lds(ec = cells_args(ctx, t, t2->bplan, ng, gsel, true, t2->q.N_bps,

@@ -224,8 +224,9 @@ struct dnrp_ctx {
     // on the caller's stream beside the back end of group g on rx_aux, Y of a group re-read from the
     // caches; fork / join through rx_fork / rx_join
     uint32_t rx_group = 0;
-    // PDC phase through the epoch receiver (kernels/rx_epoch.hip) where it applies (DNRP_RX_EPOCH)
-    bool rx_epoch = false;
+    // PDC phase through the epoch receiver (kernels/rx_epoch.hip, DNRP_RX_EPOCH): 0 off, 1 where it
+    // applies and pays (N_RX >= 4), 2 wherever it applies (tests)
+    uint32_t rx_epoch = 1;
     hipStream_t rx_aux = nullptr;
     hipEvent_t rx_fork = nullptr, rx_join = nullptr;
     uint32_t rx_mode = 0;  // DNRP_RX_MODE_* (dnrp_ctx_set_rx_mode)

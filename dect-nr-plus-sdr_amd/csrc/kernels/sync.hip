@@ -1187,7 +1187,8 @@ __host__ __device__ inline size_t peak8_alias(uint32_t region, uint32_t P, uint3
 // CT: the 9/10 sync resampler's taps compiled in (pp_const<taps_sync_9_10>, host-checked bit for
 // bit): immediates next to their FMAs instead of 225 run-time taps held in SGPRs (which spill)
 #ifndef DNRP_PEAK_STAGED
-#define DNRP_PEAK_STAGED 1  // the STF region's input span staged in LDS first (resample_staged)
+#define DNRP_PEAK_STAGED 0  // 1: the STF region's input span staged in LDS first (resample_staged); measured
+                            // 2.75 / 2.75 vs 2.72 / 2.71 ms per chunk, not the default
 #endif
 #ifndef DNRP_PEAK_WPE
 #define DNRP_PEAK_WPE 4  // waves per SIMD the register budget allows

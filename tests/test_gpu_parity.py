@@ -268,11 +268,12 @@ EPOCH_CASES = ["C4", "C3", "C2", "tm5_u2b4", "mrc2_64qam", "mrc4_16qam", "lmode_
 
 
 def _rx_parity_epoch(name, stride, monkeypatch):
-    """DNRP_RX_EPOCH=1: the PDC phase through the epoch receiver (rx_epoch.hip: DRS pass, SNR chain, then one
+    """DNRP_RX_EPOCH=2: the PDC phase through the epoch receiver (rx_epoch.hip: DRS pass, SNR chain, then one
     workgroup per (packet, epoch) running the front end of the epoch's symbols and equalising them) instead
-    of the batch-wide front end + rx_cells -- same oracle and gates. Geometries outside it (N_b_DFT_os !=
-    1024) run the Y path; where it applies, the launch count proves it ran."""
-    monkeypatch.setenv("DNRP_RX_EPOCH", "1")
+    of the batch-wide front end + rx_cells, for every geometry it supports (the default, 1, takes it with
+    4+ RX antennas only) -- same oracle and gates. Geometries outside it (N_b_DFT_os != 1024) run the Y
+    path; where it applies, the launch count proves it ran."""
+    monkeypatch.setenv("DNRP_RX_EPOCH", "2")
     monkeypatch.setenv("DNRP_TIMING", "1")
     phy = _rx_parity(name, stride)
     import dnrp
@@ -592,6 +593,15 @@ def test_rx_negative_fine_peak():
 @pytest.mark.parametrize("name,n", [("C4", 4096), ("C3", 8192), ("C4", 16384)])
 def test_full_chunk_edges(name, n):
     _full_chunk_edges(name, n)
+
+
+def test_rx_epoch_default_geometries(monkeypatch):
+    """The default (DNRP_RX_EPOCH unset) takes the epoch receiver with 4 RX antennas (C4) and the Y path for
+    SISO (C3), as measured."""
+    monkeypatch.delenv("DNRP_RX_EPOCH", raising=False)
+    monkeypatch.setenv("DNRP_TIMING", "1")
+    assert _rx_parity("C4").kernel_time_total("rx_epoch")[1] > 0
+    assert _rx_parity("C3").kernel_time_total("rx_epoch")[1] == 0
 
 
 @pytest.mark.parametrize("name,n", [("C4", 16384), ("C3", 8192)])
