@@ -983,7 +983,7 @@ int dnrp_tx_batch(dnrp_ctx* ctx, const dnrp_psdef* psdef, uint32_t n, const dnrp
             // polyphase blocks on the matrix cores (tx.hip, polyphase.hpp mf_blocks): opt-in A/B,
             // DNRP_TX_MFMA=1 (read per call); the VALU blocks measured faster (docs/DESIGN_LOG.md)
             const char* mf_env = std::getenv("DNRP_TX_MFMA");
-            a.mfma = (mf_env && std::atoi(mf_env)) ? 1u : 0u;
+            a.mfma = mf_env ? static_cast<uint32_t>(std::min(2, std::max(0, std::atoi(mf_env)))) : 0u;  // 2: f32 MFMA
             a.code_bin = t->code_bin.as<uint32_t>();
             a.onehot = t->tm.N_TS > 1 && t->code_oh.p ? 1u : 0u;  // transmit diversity or spatial multiplexing
             for (uint32_t i = 0; i < n && a.onehot; ++i)

@@ -444,9 +444,11 @@ __device__ __forceinline__ uint32_t txs_sym(uint32_t r, uint32_t N_DF) {  // sym
     return r <= 1 ? 0u : (r - 1 <= N_DF ? r - 1 : N_DF + 1);
 }
 
-template <bool MF>
-__device__ __forceinline__ float2 txs_slot(float2 v) {  // buffer slot of a piece sample (MF: split fp16 words)
-    if constexpr (MF) return __builtin_bit_cast(float2, mf_split(v));
+// MF: the polyphase blocks' form -- 0 VALU (pp_const), 1 matrix cores in split fp16 (three passes of
+// v_mfma_f32_16x16x32_f16), 2 matrix cores in f32 (v_mfma_f32_16x16x4_f32, exact f32 products)
+template <int MF>
+__device__ __forceinline__ float2 txs_slot(float2 v) {  // buffer slot of a piece sample (MF 1: split fp16 words)
+    if constexpr (MF == 1) return __builtin_bit_cast(float2, mf_split(v));
     else return v;
 }
 
@@ -655,7 +657,7 @@ __device__ __forceinline__ void txs_emit(const float2* buf, __amdgpu_buffer_rsrc
     }
 }
 
-template <int LR, int MR, int HLR, int MODE, bool Q8, bool MF>
+template <int LR, int MR, int HLR, int MODE, bool Q8, int MF>
 #ifndef DNRP_TX_WPE
 #define DNRP_TX_WPE 4  // waves per SIMD (5: 96 VGPRs + 120 B/lane of spills)
 #endif
@@ -725,17 +727,23 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
     // MF: the lane's block taps for the matrix cores (polyphase.hpp mf_blocks), split fp16 hi / lo:
     // B[i = 8 (lane >> 4) + j][c = lane & 15] = h[ph_c + (HL + o_c - i) L] inside output c's span
     mf_h8 gh, gl;
+    float g32[8];  // MF 2: B[k = 4 s + (lane >> 4)][c = lane & 15] of k-step s, f32
     float2 step10 = make_float2(1.f, 0.f), step160 = step10;
-    if constexpr (MF) {
+    if constexpr (MF != 0) {
         const uint32_t c = lane & 15u, hq = lane >> 4;
         const int o = static_cast<int>(MR * c) / LR, ph = static_cast<int>(MR * c) % LR;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int d = HLR + o - static_cast<int>(8 * hq) - j;
-            const float t = (c < LR && d >= 0 && d <= HLR) ? A.taps[ph + d * LR] : 0.f;
-            const mf_h2 hv = __builtin_amdgcn_cvt_pkrtz(t, 0.f);
-            gh[j] = hv.x;
-            gl[j] = __builtin_amdgcn_cvt_pkrtz(t - static_cast<float>(hv.x), 0.f).x;
+            if constexpr (MF == 1) {
+                const int d = HLR + o - static_cast<int>(8 * hq) - j;
+                const float t = (c < LR && d >= 0 && d <= HLR) ? A.taps[ph + d * LR] : 0.f;
+                const mf_h2 hv = __builtin_amdgcn_cvt_pkrtz(t, 0.f);
+                gh[j] = hv.x;
+                gl[j] = __builtin_amdgcn_cvt_pkrtz(t - static_cast<float>(hv.x), 0.f).x;
+            } else {
+                const int d = HLR + o - static_cast<int>(4 * j + hq);
+                g32[j] = (c < LR && d >= 0 && d <= HLR) ? A.taps[ph + d * LR] : 0.f;
+            }
         }
         if (T.P.do_mix) {
             step10 = phasor(10.0 * T.P.inc);
@@ -857,7 +865,7 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
         }
         __builtin_amdgcn_wave_barrier();
         float2 creg = make_float2(0.f, 0.f);
-        if (MF && r >= r_a) {
+        if (MF != 0 && r >= r_a) {
             // 8 groups of 16 blocks on the matrix cores (lane: output phase c = lid & 15 of blocks
             // 16 g + 4 (lid >> 4) + q, phases >= 10 idle), each group's 160 outputs transposed through
             // LDS slots [0, 160) -- dead once the windows of group 1 are read (they start at slot
@@ -871,11 +879,24 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
             if (T.P.do_mix) rot = phasor(T.P.ph0 + static_cast<double>(mb) * T.P.inc);
             prefetch_next(r, lid);
             auto group = [&](int g, float2 (&y)[4]) {
-                uint2 w[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) w[j] = slots[MR * 16 * g + j];
                 mf_f4 cr, ci;
-                mf_blocks(w, gh, gl, cr, ci);
+                if constexpr (MF == 1) {
+                    uint2 w[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) w[j] = slots[MR * 16 * g + j];
+                    mf_blocks(w, gh, gl, cr, ci);
+                } else {
+                    // A[block c][input k = 4 s + hq] of k-step s: one float2 slot per lane and step
+                    const float2* wb = buf + base0 + MR * (16 * g + c) + hq;
+                    cr = mf_f4{0.f, 0.f, 0.f, 0.f};
+                    ci = cr;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float2 xv = wb[4 * j];
+                        cr = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, g32[j], cr, 0, 0, 0);
+                        ci = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, g32[j], ci, 0, 0, 0);
+                    }
+                }
                 float2 rr = rot;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1117,8 +1138,9 @@ hipError_t launch_tx(const tx_args& a, uint32_t n, hipStream_t st) {
         const int mode = a.N_TS == 1 ? TXS_SISO : a.txdiv ? (a.onehot ? TXS_TXDIV1 : TXS_TXDIV) : (a.onehot ? TXS_SM1 : TXS_SM);
 #define DNRP_TXS(MODE, Q8)                                                                                       \
     do {                                                                                                         \
-        if (a.mfma) hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8, true>), g, b, tx_stream_lds(), st, a, n);   \
-        else hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8, false>), g, b, tx_stream_lds(), st, a, n); \
+        if (a.mfma == 2) hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8, 2>), g, b, tx_stream_lds(), st, a, n); \
+        else if (a.mfma) hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8, 1>), g, b, tx_stream_lds(), st, a, n); \
+        else hipLaunchKernelGGL((tx_stream_kernel<10, 9, 22, MODE, Q8, 0>), g, b, tx_stream_lds(), st, a, n);      \
     } while (0)
         if (a.N_bps == 8) {
             if (mode == TXS_SISO) DNRP_TXS(TXS_SISO, true);

@@ -96,11 +96,13 @@ def test_tx_parity(name):
 
 
 @pytest.mark.parametrize("name", sorted(TX_CASES))
-def test_tx_parity_matrix_blocks(name, monkeypatch):
+@pytest.mark.parametrize("form", ["1", "2"])
+def test_tx_parity_matrix_blocks(name, form, monkeypatch):
     """The streaming TX kernel's opt-in matrix-core polyphase blocks (DNRP_TX_MFMA=1: split-fp16
-    v_mfma_f32_16x16x32_f16, polyphase.hpp mf_blocks) against the same oracle and tolerance;
-    configurations outside the streaming kernel's geometry ignore the switch."""
-    monkeypatch.setenv("DNRP_TX_MFMA", "1")
+    v_mfma_f32_16x16x32_f16, polyphase.hpp mf_blocks; DNRP_TX_MFMA=2: f32 v_mfma_f32_16x16x4_f32) against
+    the same oracle and tolerance; configurations outside the streaming kernel's geometry ignore the
+    switch."""
+    monkeypatch.setenv("DNRP_TX_MFMA", form)
     test_tx_parity(name)
 
 
