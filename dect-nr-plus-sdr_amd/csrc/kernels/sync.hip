@@ -1426,6 +1426,9 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
 
 // ===================================================================== fine peak
 constexpr uint32_t SYNC_FINE_THREADS = 512;  // 8 waves: the FFT passes' butterflies 2 per thread
+#ifndef DNRP_FINE_BATCH
+#define DNRP_FINE_BATCH 8  // spectrum x template loads in flight per thread (1: one per loop iteration)
+#endif
 
 __global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -1500,7 +1503,27 @@ __global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args 
     // wave maxima use 0..7), written by thread 0, the only reader: no registers held across the FFTs
     for (uint32_t k = 0; k < A.n_templates; ++k) {
         const float2* T = A.tmpl_f + static_cast<size_t>(k) * nf;
-        for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) xb[ix(i)] = cmul(Sb[i], T[i]);
+        if constexpr (DNRP_FINE_BATCH > 1) {
+            // the spectrum row and the template read DNRP_FINE_BATCH per thread at a time (one L2
+            // round trip per batch instead of one per element), then the products stored
+            constexpr uint32_t U = DNRP_FINE_BATCH;
+            for (uint32_t i0 = 0; i0 < nf; i0 += U * blockDim.x) {
+                float2 sv[U], tv[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t i = min(i0 + u * blockDim.x + threadIdx.x, nf - 1);
+                    sv[u] = Sb[i];
+                    tv[u] = T[i];
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t i = i0 + u * blockDim.x + threadIdx.x;
+                    if (i < nf) xb[ix(i)] = cmul(sv[u], tv[u]);
+                }
+            }
+        } else {
+            for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) xb[ix(i)] = cmul(Sb[i], T[i]);
+        }
         __syncthreads();
         const float2* R = fft(std::integral_constant<int, 1>{}, xb, yb);
         float bv = -1.f;
