@@ -47,6 +47,9 @@ enum xs_bit : unsigned {
     // rx_epoch_kernel phase skips (output meaningless): no front-end tasks / no equalisation
     XS_EP_SKIP_FE = 1u << 18,
     XS_EP_SKIP_EQ = 1u << 19,
+    // rx_epoch_kernel: Y rows of the epoch in one of 64 x 8 x n_epochs packet images picked by
+    // blockIdx (racy, output meaningless): the timing with the rows kept on-die
+    XS_EP_SLOTY = 1u << 20,
 };
 
 __host__ __device__ constexpr bool experiment(unsigned bit) { return (DNRP_EXPERIMENTS & bit) != 0u; }

@@ -77,7 +77,8 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
                 stage_span_lo<20>(R, src, sp.in0, sp.n_in, q_lo, q_hi, lane, 64);
             __builtin_amdgcn_wave_barrier();
             rx_resample_ct<LR, MR, HLR>(F, in, S, sp, R, lane);
-            float2* Yrow = F.Y + ((size_t(pkt) * NRX + a) * F.n_sym_total + l) * F.Nf_pad;
+            const size_t yimg = experiment(XS_EP_SLOTY) ? blockIdx.x % (64u * A.n_epochs) : pkt;
+            float2* Yrow = F.Y + ((yimg * NRX + a) * F.n_sym_total + l) * F.Nf_pad;
             rx_fft_bins<true>(F, S, R, lane, [&](uint32_t k, float2 v) {
                 if constexpr (DNRP_EP_YNT) {
                     typedef float f2v __attribute__((ext_vector_type(2)));
@@ -125,6 +126,7 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
         if (tid < 12) pairs[tid] = A.pair[tid];
     }
     build_pilots<NRX, NT, cells_ai(NRX, NT)>(A, E, Yp, zfi, tid, EP_THREADS);
+    if constexpr (experiment(XS_EP_SLOTY)) Yp = A.Y + size_t(blockIdx.x % (64u * A.n_epochs)) * NRX * A.n_sym_total * A.Nf_pad;
     __syncthreads();
     if (tid >= units) return;
     const uint8_t* __restrict__ seq = A.pdc_seq[row];

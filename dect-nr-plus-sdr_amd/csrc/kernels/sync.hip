@@ -1187,11 +1187,14 @@ __host__ __device__ inline size_t peak8_alias(uint32_t region, uint32_t P, uint3
 // CT: the 9/10 sync resampler's taps compiled in (pp_const<taps_sync_9_10>, host-checked bit for
 // bit): immediates next to their FMAs instead of 225 run-time taps held in SGPRs (which spill)
 #ifndef DNRP_PEAK_STAGED
-#define DNRP_PEAK_STAGED 0  // 1: the STF region's input span staged in LDS first (resample_staged); measured
-                            // 2.75 / 2.75 vs 2.72 / 2.71 ms per chunk, not the default
+#define DNRP_PEAK_STAGED 1  // 1: the STF region's input span staged in LDS first (resample_staged): at 4 waves
+                            // per SIMD neutral (2.75 vs 2.72 ms per chunk); what lets the window loads leave
+                            // the registers for 6 waves per SIMD below
 #endif
 #ifndef DNRP_PEAK_WPE
-#define DNRP_PEAK_WPE 4  // waves per SIMD the register budget allows
+#define DNRP_PEAK_WPE 6  // 6 waves per SIMD = 3 workgroups per CU (80 VGPRs; the metric's double divisions
+                         // spill ~100 B per lane at NUW 8):
+                         // 2.76 -> 2.31-2.36 ms per C4 chunk against 4 (104 VGPRs, 2 workgroups per CU)
 #endif
 template <int LR, int MR, int HLR, bool CT, int NUW>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DNRP_PEAK_WPE))) sync_peak_kernel(sync_args A) {
