@@ -95,8 +95,14 @@ __host__ __device__ inline uint32_t rx_stf_chunk_taps(uint32_t n_stf, uint32_t N
 // float2 slots of rx_stf_ant_kernel's compact area: the 9/10 input span of n_stf outputs (upper bound)
 __host__ __device__ inline uint32_t rx_stf_area(uint32_t n_stf) { return ((n_stf + 18) * 10) / 9 + 33 + 10 + 2; }
 
+#ifndef DNRP_STF_IMAJ
+#define DNRP_STF_IMAJ 1  // compiled-in taps: the FIR input-major from LDS (0: the whole window in registers)
+#endif
+#ifndef DNRP_STF_WPE
+#define DNRP_STF_WPE 8  // waves per SIMD the register budget must allow (256-thread workgroups: = per CU)
+#endif
 template <int HL, bool CT = false, bool CHUNK = false>
-__global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CT ? DNRP_STF_WPE : 1))) rx_stf_ant_kernel(rx_front_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     __shared__ double red[16];
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x / A.N_RX), a = blockIdx.x % A.N_RX;
@@ -150,24 +156,65 @@ __global__ void __launch_bounds__(256) rx_stf_ant_kernel(rx_front_args A) {
         const uint32_t rounds = static_cast<uint32_t>((q1 - q0 + blockDim.x - 1) / blockDim.x);
         for (uint32_t rd = 0; rd < rounds; ++rd) {
             const int64_t q = q0 + threadIdx.x + int64_t(rd) * blockDim.x;
-            float2 xv[W];
-            PD::template load<true>(span + 10 * min<int64_t>(q - q0, q1 - 1 - q0), xv);
-            __syncthreads();
+            float2 y[9];
+            const float2* xw = span + 10 * min<int64_t>(q - q0, q1 - 1 - q0);
+            if constexpr (DNRP_STF_IMAJ) {
+                // input-major, newest input first: window input i (i = W-1 .. 0) updates every output
+                // k whose span holds it (d = 24 + o_k - i), so each output sums d = 0 .. 24 in the
+                // output-major order below, bit for bit; live state is the 9 sums and one input pair,
+                // not the 33-input window (VGPRs: occupancy of this latency-bound kernel)
+#pragma unroll
+                for (int k = 0; k < 9; ++k) y[k] = make_float2(0.f, 0.f);
+                const float4* x4 = reinterpret_cast<const float4*>(xw);  // xw even: 16-B pairs
+                float4 nxt = x4[W / 2 - (W % 2 ? 0 : 1)];
+#pragma unroll
+                for (int j = (W - 1) / 2; j >= 0; --j) {  // pair (2j, 2j + 1), the odd input first
+                    const float4 cur = nxt;
+                    if (j > 0) nxt = x4[j - 1];
+                    asm volatile("" ::: "memory");  // one pair ahead, not the whole window
+#pragma unroll
+                    for (int e = 1; e >= 0; --e) {
+                        const int i = 2 * j + e;
+                        if (i >= W) continue;
+                        const float2 xi = e ? make_float2(cur.z, cur.w) : make_float2(cur.x, cur.y);
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) {
+                            const int o = (k * 10) / 9, ph = (k * 10) % 9, d = 24 + o - i;
+                            if (d < 0 || d > 24) continue;
+                            const float h = taps_rx_9_10::h[ph + d * 9];
+                            y[k].x = fmaf(xi.x, h, y[k].x);
+                            y[k].y = fmaf(xi.y, h, y[k].y);
+                        }
+                    }
+                    // the sums pinned here: the compiler would otherwise sink every FMA behind the
+                    // barrier into its output's store branch with the whole window live again
+                    asm volatile("" : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]),
+                                 "+v"(y[7]), "+v"(y[8]));
+                }
+            } else {
+                float2 xv[W];
+                PD::template load<true>(xw, xv);
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    const int o = (k * 10) / 9, ph = (k * 10) % 9;
+                    float ar = 0.f, ai = 0.f;
+#pragma unroll
+                    for (int d = 0; d <= 24; ++d) {
+                        const float h = taps_rx_9_10::h[ph + d * 9];
+                        ar = fmaf(xv[24 + o - d].x, h, ar);
+                        ai = fmaf(xv[24 + o - d].y, h, ai);
+                    }
+                    y[k] = make_float2(ar, ai);
+                }
+            }
+            __syncthreads();  // every window of the round read before its outputs overwrite the span
             if (q >= q1) continue;
             const int64_t mb = ms + 9 * q;
             float2 r = phasor(static_cast<double>(mb) * in.inc0);
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
-                const int o = (k * 10) / 9, ph = (k * 10) % 9;
-                float ar = 0.f, ai = 0.f;
-#pragma unroll
-                for (int d = 0; d <= 24; ++d) {
-                    const float h = taps_rx_9_10::h[ph + d * 9];
-                    ar = fmaf(xv[24 + o - d].x, h, ar);
-                    ai = fmaf(xv[24 + o - d].y, h, ai);
-                }
                 const int64_t m = mb + k;
-                if (m >= 0 && m < static_cast<int64_t>(n_stf)) sbuf[m] = cmul(make_float2(ar, ai), r);
+                if (m >= 0 && m < static_cast<int64_t>(n_stf)) sbuf[m] = cmul(y[k], r);
                 r = cmul(r, step1);
             }
         }
