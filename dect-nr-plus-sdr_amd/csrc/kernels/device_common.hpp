@@ -589,6 +589,70 @@ __device__ void fft_r4_inplace_ct(float2* x_, const float2* tw) {
     r4_passes<0, LOG2N>(pass);
 }
 
+// 8-point DFT in registers (natural order in and out): two 4-point DFTs of the even and odd inputs
+// and the W8^m butterflies, W8 = exp(SIGN 2 pi i / 8)
+template <int SIGN>
+__device__ __forceinline__ void dft8(float2 (&a)[8]) {
+    constexpr float R2 = 0.70710678118654752440f;
+    float2 e0 = a[0], e1 = a[2], e2 = a[4], e3 = a[6], o0 = a[1], o1 = a[3], o2 = a[5], o3 = a[7];
+    dft4<SIGN>(e0, e1, e2, e3);
+    dft4<SIGN>(o0, o1, o2, o3);
+    // W8^1 = (1 + SIGN j) / sqrt 2, W8^2 = SIGN j, W8^3 = (-1 + SIGN j) / sqrt 2
+    const float2 w1 = SIGN < 0 ? make_float2(R2 * (o1.x + o1.y), R2 * (o1.y - o1.x)) : make_float2(R2 * (o1.x - o1.y), R2 * (o1.x + o1.y));
+    const float2 w2 = SIGN < 0 ? make_float2(o2.y, -o2.x) : make_float2(-o2.y, o2.x);
+    const float2 w3 = SIGN < 0 ? make_float2(R2 * (o3.y - o3.x), -R2 * (o3.x + o3.y)) : make_float2(-R2 * (o3.x + o3.y), R2 * (o3.x - o3.y));
+    a[0] = cadd(e0, o0);
+    a[4] = csub(e0, o0);
+    a[1] = cadd(e1, w1);
+    a[5] = csub(e1, w1);
+    a[2] = cadd(e2, w2);
+    a[6] = csub(e2, w2);
+    a[3] = cadd(e3, w3);
+    a[7] = csub(e3, w3);
+}
+
+// 4096-point in-place radix-8 decimation-in-time FFT by 512 threads (one butterfly per thread and
+// pass, four passes instead of fft_r4_inplace_ct's six): the input at base-8 digit-reversed slots
+// (rev8), output in natural order, slot i at x[r8pad(i)] (r8pad: the stride-8 butterfly reads, the
+// stride-512 digit-reversed writes and the stride-64 / -512 groups on distinct bank pairs)
+__device__ __forceinline__ uint32_t r8pad(uint32_t i) { return i + (i >> 3) + (i >> 9); }
+__device__ __forceinline__ uint32_t rev8(uint32_t i) {  // 12 bits = 4 base-8 digits
+    return ((i & 7u) << 9) | (((i >> 3) & 7u) << 6) | (((i >> 6) & 7u) << 3) | (i >> 9);
+}
+constexpr uint32_t R8_SLOTS = 4096 + 512 + 8;
+
+template <int SIGN>
+__device__ void fft_r8_4096(float2* x_, const float2* tw) {
+    const uint32_t j = threadIdx.x;  // blockDim.x == 512 (caller)
+    const __amdgpu_buffer_rsrc_t twr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(tw), 0, 4096 * 8, 0x00020000);
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    auto pass = [&](auto sc) {
+        constexpr uint32_t s = decltype(sc)::value, Q = 1u << s, tsh = 12 - s - 3;
+        const uint32_t k = j & (Q - 1u), i0 = ((j >> s) << (s + 3)) + k;
+        float2 a[8], w[7];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) a[r] = x_[r8pad(i0 + r * Q)];
+        if constexpr (s > 0) {
+            const uint32_t e8 = (k << tsh) * 8u;
+#pragma unroll
+            for (int r = 0; r < 7; ++r) {
+                const u2 v = __builtin_amdgcn_raw_buffer_load_b64(twr, (r + 1) * e8, 0, 0);
+                w[r] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+            }
+#pragma unroll
+            for (int r = 0; r < 7; ++r) a[r + 1] = cmul(a[r + 1], SIGN > 0 ? cconj(w[r]) : w[r]);
+        }
+        dft8<SIGN>(a);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x_[r8pad(i0 + r * Q)] = a[r];
+        __syncthreads();
+    };
+    pass(std::integral_constant<uint32_t, 0>{});
+    pass(std::integral_constant<uint32_t, 3>{});
+    pass(std::integral_constant<uint32_t, 6>{});
+    pass(std::integral_constant<uint32_t, 9>{});
+}
+
 // base-4 digit reversal of the log2N / 2 digits of i (fft_r4_inplace's input position)
 __device__ __forceinline__ uint32_t rev4(uint32_t i, uint32_t log2N) {
     const uint32_t b = __brev(i) >> (32 - log2N);

@@ -1429,11 +1429,20 @@ __global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
 
 // ===================================================================== fine peak
 constexpr uint32_t SYNC_FINE_THREADS = 512;  // 8 waves: the FFT passes' butterflies 2 per thread
+#ifndef DNRP_FINE_WPE
+#define DNRP_FINE_WPE 1  // waves per SIMD the register budget must allow (1: the compiler's choice; radix 8
+                         // at 8: 64 VGPRs + 160 B of spills, 1.55-1.57 ms per C4 chunk against 1.50-1.51
+                         // at the compiler's 113 VGPRs)
+#endif
+#ifndef DNRP_FINE_R8
+#define DNRP_FINE_R8 1  // 4096-point transforms by fft_r8_4096 (four radix-8 passes; 0: six radix-4 passes):
+                        // sync_fine 1.63-1.65 -> 1.50-1.51 ms per C4 chunk (same box)
+#endif
 #ifndef DNRP_FINE_BATCH
 #define DNRP_FINE_BATCH 8  // spectrum x template loads in flight per thread (1: one per loop iteration)
 #endif
 
-__global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args A) {
+__global__ void __launch_bounds__(SYNC_FINE_THREADS) __attribute__((amdgpu_waves_per_eu(DNRP_FINE_WPE))) sync_fine_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     float* s_val = reinterpret_cast<float*>(smem);  // [16]
     uint32_t* s_idx = reinterpret_cast<uint32_t*>(smem + 8);  // [16]
@@ -1456,11 +1465,16 @@ __global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args 
     // power-of-4 sizes (4096 for C3 / C4): in-place radix-4 DIT on one LDS buffer, the inputs stored
     // at their base-4 digit-reversed positions (ip); otherwise the two-buffer Stockham passes
     const bool ip = (A.log2_fft & 1u) == 0;
-    // in place: bank-padded slots (r4pad), inputs written at their digit-reversed slots
-    auto ix = [&](uint32_t i) { return ip ? r4pad(rev4(i, A.log2_fft)) : i; };
-    auto ox = [&](uint32_t i) { return ip ? r4pad(i) : i; };
+    const bool r8 = DNRP_FINE_R8 && A.log2_fft == 12;  // C3 / C4: radix 8, four passes
+    // in place: bank-padded slots (r4pad / r8pad), inputs written at their digit-reversed slots
+    auto ix = [&](uint32_t i) { return r8 ? r8pad(rev8(i)) : ip ? r4pad(rev4(i, A.log2_fft)) : i; };
+    auto ox = [&](uint32_t i) { return r8 ? r8pad(i) : ip ? r4pad(i) : i; };
     auto fft = [&](auto sign, float2* a, float2* b) -> const float2* {
         constexpr int SG = decltype(sign)::value;
+        if (r8) {
+            fft_r8_4096<SG>(a, A.tw_fft);
+            return a;
+        }
         if (ip) {
             if (A.log2_fft == 12)  // C3 / C4
                 fft_r4_inplace_ct<SG, 12>(a, A.tw_fft);
@@ -1470,7 +1484,7 @@ __global__ void __launch_bounds__(SYNC_FINE_THREADS) sync_fine_kernel(sync_args 
         }
         return fft_pow2<SG>(a, b, A.tw_fft, A.log2_fft);
     };
-    const uint32_t nbuf = ip ? nf + nf / 32 : nf;  // (the host sizes the LDS the same way)
+    const uint32_t nbuf = r8 ? R8_SLOTS : ip ? nf + nf / 32 : nf;  // (the host sizes the LDS the same way)
     float2* xb = smem + 16;
     float2* yb = xb + nbuf;
     // the forward spectrum is read once per template: kept in a global scratch row (L2-resident
@@ -1775,7 +1789,8 @@ hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st) {
 
 hipError_t launch_sync_fine(const sync_args& a, uint32_t n, hipStream_t st) {
     const size_t nbuf = size_t(1) << a.log2_fft;
-    const size_t lds = (16 + ((a.log2_fft & 1u) == 0 ? nbuf + nbuf / 32 : 2 * nbuf)) * sizeof(float2);  // in place: one padded buffer
+    // in place: one padded buffer (radix 8 at 4096 points: R8_SLOTS)
+    const size_t lds = (16 + (DNRP_FINE_R8 && a.log2_fft == 12 ? R8_SLOTS : (a.log2_fft & 1u) == 0 ? nbuf + nbuf / 32 : 2 * nbuf)) * sizeof(float2);
     hipLaunchKernelGGL(sync_fine_kernel, dim3(n * a.max_reports), dim3(SYNC_FINE_THREADS), lds, st, a);
     return hipGetLastError();
 }
