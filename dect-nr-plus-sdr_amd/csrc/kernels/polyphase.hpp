@@ -176,6 +176,43 @@ struct pp_const {
         }
     }
 
+    // the same sums input-major from LDS: window input i (ascending, in 16-B pairs; xw 16-B aligned)
+    // updates every output k whose span holds it (d = HL + o_k - i), so output k still sums
+    // d = HL .. 0 in order, bit-identical to run(); live state is the L sums and one input pair. The
+    // sums are pinned after every pair, or the compiler sinks each output's FMAs into its consumer and
+    // holds the whole window again.
+    __device__ static __forceinline__ void run_imaj(const float2* xw, float2 (&y)[L]) {
+        static_assert(L == 9 || L == 10, "pin list");
+#pragma unroll
+        for (int k = 0; k < L; ++k) y[k] = make_float2(0.f, 0.f);
+        const float4* x4 = reinterpret_cast<const float4*>(xw);
+        float4 nxt = x4[0];
+#pragma unroll
+        for (int j = 0; 2 * j < W; ++j) {
+            const float4 cur = nxt;
+            if (2 * j + 2 < W) nxt = x4[j + 1];
+            asm volatile("" ::: "memory");  // one pair ahead, not the whole window
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int i = 2 * j + e;
+                if (i >= W) continue;
+                const float2 xi = e ? make_float2(cur.z, cur.w) : make_float2(cur.x, cur.y);
+#pragma unroll
+                for (int k = 0; k < L; ++k) {
+                    const int o = (k * M) / L, ph = (k * M) % L, d = HL + o - i;
+                    if (d < 0 || d > HL) continue;
+                    constexpr_if_nonzero(TP::h[ph + d * L], xi, y[k]);
+                }
+            }
+            if constexpr (L == 9)
+                asm volatile("" : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]), "+v"(y[7]),
+                             "+v"(y[8]));
+            else
+                asm volatile("" : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]), "+v"(y[7]),
+                             "+v"(y[8]), "+v"(y[9]));
+        }
+    }
+
   private:
     __device__ static __forceinline__ void constexpr_load(const float2* xw, float2 (&x)[W], const int i) {
         if (i > ((L - 1) * M) / L && i < W) x[i] = xw[i];

@@ -1103,7 +1103,7 @@ __device__ __forceinline__ void resample_direct(const sync_args& A, const float2
 // (every window read: stage[] may alias the outputs' slots) hands the outputs to put. One global
 // load latency instead of two (the tail blocks' second round), the same sums as resample_direct.
 // Preconditions (host, sync_peak_ok): blocks <= 2 T, n_in <= the stage's capacity.
-template <int LR, int MR, int HLR, class PUT>
+template <int LR, int MR, int HLR, bool IMAJ = false, class PUT>
 __device__ __forceinline__ void resample_staged(const sync_args& A, const float2* x, int64_t y0, uint32_t cnt,
                                                 float2* stage, PUT put) {
     using PD = pp_direct<LR, MR, HLR>;
@@ -1134,15 +1134,20 @@ __device__ __forceinline__ void resample_staged(const sync_args& A, const float2
     __syncthreads();
     float2 y[LR], y2[LR];
     const uint32_t b2 = tid + T;
-    if (tid < nb) {
-        float2 xv[W];
-        PD::template load<false>(stage + MR * tid, xv);
-        pp_const<taps_sync_9_10>::run(xv, y);
-    }
-    if (b2 < nb) {
-        float2 xv[W];
-        PD::template load<false>(stage + MR * b2, xv);
-        pp_const<taps_sync_9_10>::run(xv, y2);
+    if constexpr (IMAJ) {  // windows input-major from LDS (stage 16-B aligned, MR even)
+        if (tid < nb) pp_const<taps_sync_9_10>::run_imaj(stage + MR * tid, y);
+        if (b2 < nb) pp_const<taps_sync_9_10>::run_imaj(stage + MR * b2, y2);
+    } else {
+        if (tid < nb) {
+            float2 xv[W];
+            PD::template load<false>(stage + MR * tid, xv);
+            pp_const<taps_sync_9_10>::run(xv, y);
+        }
+        if (b2 < nb) {
+            float2 xv[W];
+            PD::template load<false>(stage + MR * b2, xv);
+            pp_const<taps_sync_9_10>::run(xv, y2);
+        }
     }
     __syncthreads();  // every window read before the outputs overwrite the stage
     auto emit = [&](uint32_t b, const float2 (&yy)[LR]) {
@@ -1396,18 +1401,25 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DNRP_P
 // detection kernel ran, so the same doubles) -> rms[a] into the report and the antenna's CFO term
 // m_a atan2(c_a) / P into A.post; sync_fine_kernel sums the terms in antenna order. One workgroup
 // per (report, antenna) instead of four serial passes inside the detection workgroup.
+#ifndef DNRP_POST_STAGED
+#define DNRP_POST_STAGED 1
+#endif
 template <int LR, int MR, int HLR, bool CT>
-__global__ void __launch_bounds__(SYNC_THREADS) sync_post_kernel(sync_args A) {
+__global__ void __launch_bounds__(SYNC_THREADS) __attribute__((amdgpu_waves_per_eu(CT && DNRP_POST_STAGED ? 8 : 1))) sync_post_kernel(sync_args A) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     double* red = reinterpret_cast<double*>(smem);  // [24]
-    float2* lbuf = smem + 12;
+    float2* lbuf = smem + 12;  // 16-B aligned (resample_staged's stage)
     const uint32_t rep = blockIdx.x / A.n_ant, a = blockIdx.x % A.n_ant, w = rep / A.max_reports;
     sync_res* rp = A.res + rep;
     const float m = rp->coarse_metric[a];
     if (!rp->found || !(m > 0.f)) return;  // uniform: the whole workgroup leaves
     const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
-    // the STF at the coarse peak, resampled straight from the window (sync_resample's values)
-    resample_direct<LR, MR, HLR, CT>(A, x, rp->coarse_local, A.stf_len, [&](uint32_t i, float2 v) { lbuf[i] = v; });
+    // the STF at the coarse peak (sync_resample's values): compiled-in 9/10 taps -> the span staged in
+    // LDS and the FIR input-major from it (DNRP_POST_STAGED, 8 waves per SIMD), else straight from the window
+    if constexpr (CT && LR == 9 && DNRP_POST_STAGED)
+        resample_staged<LR, MR, HLR, true>(A, x, rp->coarse_local, A.stf_len, lbuf, [&](uint32_t i, float2 v) { lbuf[i] = v; });
+    else
+        resample_direct<LR, MR, HLR, CT>(A, x, rp->coarse_local, A.stf_len, [&](uint32_t i, float2 v) { lbuf[i] = v; });
     __syncthreads();
     double cr = 0.0, ci = 0.0, pw = 0.0;
     const uint32_t Lw = A.pattern * A.n_uw;
@@ -1769,12 +1781,21 @@ hipError_t launch_sync_peak(const sync_args& a, uint32_t n, hipStream_t st) {
     return hipGetLastError();
 }
 
-size_t sync_post_lds(const sync_args& a) { return (12 + (a.stf_len + 1) / 2 * 2) * sizeof(float2); }
+// the staged form (sync_post_kernel<9, 10, 24, true>): compiled-in taps and at most 2 blocks per thread;
+// otherwise the run-time-tap form reads the windows straight from the stream (the same sums)
+static bool sync_post_staged(const sync_args& a) {
+    return DNRP_POST_STAGED && a.L == 9 && a.M == 10 && a.hl == 24 && a.ct_taps && (a.stf_len + 8) / 9 + 2 <= 2 * SYNC_THREADS;
+}
+size_t sync_post_lds(const sync_args& a) {  // the staged form's input span (n_in inputs) or the STF
+    const uint32_t nb = (a.stf_len + 8) / 9 + 2, n_in = 10 * nb + pp_direct<9, 10, 24>::W;
+    return (12 + (std::max(a.stf_len, sync_post_staged(a) ? n_in : 0u) + 1) / 2 * 2) * sizeof(float2);
+}
 
 hipError_t launch_sync_post(const sync_args& a, uint32_t n, hipStream_t st) {
     const dim3 g(n * a.max_reports * a.n_ant);
     const size_t lds = sync_post_lds(a);
-    if (a.L == 9 && a.M == 10 && a.hl == 24 && a.ct_taps)
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (sync_post_staged(a) || (!DNRP_POST_STAGED && a.L == 9 && a.M == 10 && a.hl == 24 && a.ct_taps))
         hipLaunchKernelGGL((sync_post_kernel<9, 10, 24, true>), g, dim3(SYNC_THREADS), lds, st, a);
     else if (a.L == 9 && a.M == 10 && a.hl == 24)
         hipLaunchKernelGGL((sync_post_kernel<9, 10, 24, false>), g, dim3(SYNC_THREADS), lds, st, a);
