@@ -826,7 +826,11 @@ __device__ void peak_search(const sync_args& A, const float2* lbuf, uint32_t reg
 // LDS per CU this beats the 2-wave default in the pipelined bench (A/B on MI355X: 181.4k vs 184.9k
 // slot-pairs/s)
 #ifndef SYNC_DETECT_ATTR
-#define SYNC_DETECT_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#define SYNC_DETECT_ATTR __attribute__((amdgpu_waves_per_eu(SPLIT ? DNRP_DET_SPLIT_WPE : 3)))
+#endif
+// the split form (detection conditions only, no resampling, small LDS): its own register budget
+#ifndef DNRP_DET_SPLIT_WPE
+#define DNRP_DET_SPLIT_WPE 6  // 69 VGPRs, 7 waves per SIMD (3: the non-split budget, 129 VGPRs)
 #endif
 
 struct sync_shared {  // block scalars, at the start of the dynamic LDS (no static __shared__)
@@ -1196,6 +1200,9 @@ __host__ __device__ inline size_t peak8_alias(uint32_t region, uint32_t P, uint3
                             // per SIMD neutral (2.75 vs 2.72 ms per chunk); what lets the window loads leave
                             // the registers for 6 waves per SIMD below
 #endif
+#ifndef DNRP_PEAK_IMAJ
+#define DNRP_PEAK_IMAJ 1  // the staged windows input-major (pp_const::run_imaj)
+#endif
 #ifndef DNRP_PEAK_WPE
 #define DNRP_PEAK_WPE 6  // 6 waves per SIMD = 3 workgroups per CU (80 VGPRs; the metric's double divisions
                          // spill ~100 B per lane at NUW 8):
@@ -1229,7 +1236,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DNRP_P
     const float2* x = A.iq + w * A.win_stride + a * A.ant_stride;
     // ---- resampled region lb[yb + i] -> lbuf[pidx(i)] (sync_resample's outputs, bit for bit)
     if constexpr (CT && LR == 9 && DNRP_PEAK_STAGED)
-        resample_staged<LR, MR, HLR>(A, x, yb, region, lbuf, [&](uint32_t i, float2 v) { lbuf[pidx(i)] = v; });
+        resample_staged<LR, MR, HLR, DNRP_PEAK_IMAJ>(A, x, yb, region, lbuf, [&](uint32_t i, float2 v) { lbuf[pidx(i)] = v; });
     else
         resample_direct<LR, MR, HLR, CT>(A, x, yb, region, [&](uint32_t i, float2 v) { lbuf[pidx(i)] = v; });
     __syncthreads();
