@@ -181,16 +181,22 @@ struct pp_const {
     // d = HL .. 0 in order, bit-identical to run(); live state is the L sums and one input pair. The
     // sums are pinned after every pair, or the compiler sinks each output's FMAs into its consumer and
     // holds the whole window again.
+    // PAIRS: 16-B reads of input pairs (xw 16-B aligned), else 8-B reads (any float2 alignment)
+    template <bool PAIRS = true>
     __device__ static __forceinline__ void run_imaj(const float2* xw, float2 (&y)[L]) {
         static_assert(L == 9 || L == 10, "pin list");
 #pragma unroll
         for (int k = 0; k < L; ++k) y[k] = make_float2(0.f, 0.f);
-        const float4* x4 = reinterpret_cast<const float4*>(xw);
-        float4 nxt = x4[0];
+        auto pair = [&](int j) -> float4 {
+            if constexpr (PAIRS) return reinterpret_cast<const float4*>(xw)[j];
+            const float2 a = xw[2 * j], b = 2 * j + 1 < W ? xw[2 * j + 1] : make_float2(0.f, 0.f);
+            return make_float4(a.x, a.y, b.x, b.y);
+        };
+        float4 nxt = pair(0);
 #pragma unroll
         for (int j = 0; 2 * j < W; ++j) {
             const float4 cur = nxt;
-            if (2 * j + 2 < W) nxt = x4[j + 1];
+            if (2 * j + 2 < W) nxt = pair(j + 1);
             asm volatile("" ::: "memory");  // one pair ahead, not the whole window
 #pragma unroll
             for (int e = 0; e < 2; ++e) {

@@ -42,6 +42,10 @@ __device__ __forceinline__ rx_span_t rx_span(const rx_front_args& A, uint32_t l)
     return s;
 }
 
+#ifndef DNRP_FE_IMAJ
+#define DNRP_FE_IMAJ 0  // 1: the polyphase windows input-major from LDS (pp_const::run_imaj): rx_epoch 26.84 /
+                        // 26.78 vs 26.62 / 26.69 ms (the kernel's VGPR peak is elsewhere), off
+#endif
 // R[i] = input in0 + i (staged), i < n_in  ->  R[j] = mixed output m0 + j, j < 1024
 template <int LR, int MR, int HLR>
 __device__ __forceinline__ void rx_resample_ct(const rx_front_args& A, const rx_pkt_in& in, const rx_pkt_state& S,
@@ -60,9 +64,14 @@ __device__ __forceinline__ void rx_resample_ct(const rx_front_args& A, const rx_
     for (int rd = 0; rd < BR; ++rd) {
         const int qr = static_cast<int>(lane) + 64 * rd;
         const int q = sp.qb0 + qr;
-        float2 xv[PD::W], y[LR];
-        PD::template load<(MR % 2) == 0>(R + MR * min(qr, sp.qb1 - 1 - sp.qb0), xv);
-        pp_const<taps_rx_9_10>::run(xv, y);
+        float2 y[LR];
+        if constexpr (DNRP_FE_IMAJ && (MR % 2) == 0) {  // window input-major from LDS (R 16-B aligned)
+            pp_const<taps_rx_9_10>::run_imaj<true>(R + MR * min(qr, sp.qb1 - 1 - sp.qb0), y);
+        } else {
+            float2 xv[PD::W];
+            PD::template load<(MR % 2) == 0>(R + MR * min(qr, sp.qb1 - 1 - sp.qb0), xv);
+            pp_const<taps_rx_9_10>::run(xv, y);
+        }
         __builtin_amdgcn_wave_barrier();
         if (q < sp.qb1) {
             const int mb = static_cast<int>(A.m_star) + LR * q;

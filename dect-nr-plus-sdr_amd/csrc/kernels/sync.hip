@@ -266,6 +266,10 @@ __global__ void __launch_bounds__(64 * WPG) sync_steps_wave_kernel(sync_args A) 
 #ifndef DNRP_SS_LAZY
 #define DNRP_SS_LAZY 0  // 1: the FIR window read from LDS as consumed (pp_const::run_lds), not all at once
 #endif
+#ifndef DNRP_SS_IMAJ
+#define DNRP_SS_IMAJ 1  // the FIR window input-major from LDS (pp_const::run_imaj): 131 VGPRs against 159, sync_steps
+                        // 13.80 -> 13.31 ms per C4 chunk at the same 11 waves per CU (0: window loaded whole)
+#endif
 #ifndef DNRP_SS_LOOK
 #define DNRP_SS_LOOK 2  // FIR window inputs loaded this many delay rows ahead (pp_const::run_lds)
 #endif
@@ -448,7 +452,9 @@ __device__ __forceinline__ void ss_pipe_chunk(const sync_args& A, float2* inb, f
     __builtin_amdgcn_wave_barrier();
     float2 y[LR];
     if constexpr (CT) {
-#if DNRP_SS_LAZY
+#if DNRP_SS_IMAJ
+        pp_const<taps_sync_9_10>::run_imaj(inb + MR * lane, y);  // inb 16-B aligned, MR even
+#elif DNRP_SS_LAZY
         pp_const<taps_sync_9_10>::run_lds<DNRP_SS_LOOK>(inb + MR * lane, y);
 #else
         float2 xv[W];

@@ -658,6 +658,10 @@ __device__ __forceinline__ void txs_emit(const float2* buf, __amdgpu_buffer_rsrc
 }
 
 template <int LR, int MR, int HLR, int MODE, bool Q8, int MF>
+#ifndef DNRP_TX_IMAJ
+#define DNRP_TX_IMAJ 0  // 1: the polyphase windows input-major from LDS (pp_const::run_imaj; 96 VGPRs against
+                        // 120 at the same LDS-bound 16 waves per CU): TX 17.13 / 17.07 vs 16.99 / 16.99 ms, off
+#endif
 #ifndef DNRP_TX_WPE
 #define DNRP_TX_WPE 4  // waves per SIMD (5: 96 VGPRs + 120 B/lane of spills)
 #endif
@@ -937,9 +941,13 @@ __global__ void __launch_bounds__(64 * TXS_WPG) __attribute__((amdgpu_waves_per_
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
                 __builtin_amdgcn_sched_barrier(0);  // one window live at a time
-                float2 xv[PD::W];
-                PD::template load<false>(buf + base0 + MR * (lid + 64 * b), xv);
-                pp_const<taps_tx_10_9>::run(xv, y[b]);
+                if constexpr (DNRP_TX_IMAJ) {  // window input-major from LDS (8-B reads: MR odd)
+                    pp_const<taps_tx_10_9>::run_imaj<false>(buf + base0 + MR * (lid + 64 * b), y[b]);
+                } else {
+                    float2 xv[PD::W];
+                    PD::template load<false>(buf + base0 + MR * (lid + 64 * b), xv);
+                    pp_const<taps_tx_10_9>::run(xv, y[b]);
+                }
                 if (T.P.do_mix) {
                     const int mb = mfirst0 + static_cast<int>(1280 * r) + LR * static_cast<int>(lid + 64 * b);
                     float2 rot = phasor(T.P.ph0 + static_cast<double>(mb) * T.P.inc);
