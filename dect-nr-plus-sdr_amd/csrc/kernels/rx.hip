@@ -297,9 +297,10 @@ __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
         const double2 c = A.stf_cs[size_t(pkt) * 8 + a];
         cs_re += c.x;
         cs_im += c.y;
-        if (a < 8) S.rms[a] = A.stf_rms[size_t(pkt) * 8 + a];
     }
-    for (uint32_t a = A.N_RX; a < 8; ++a) S.rms[a] = 0.f;
+#pragma unroll
+    for (uint32_t a = 0; a < 8; ++a)  // compile-time slots: S stays in registers, not a scratch struct
+        S.rms[a] = a < A.N_RX ? A.stf_rms[size_t(pkt) * 8 + a] : 0.f;
     __syncthreads();
     // fractional CFO re-estimate (rx_synced.cpp:523-558) and mixer adjustment (mixer.cpp:35-39)
     const float delta = atan2f(static_cast<float>(cs_im), static_cast<float>(cs_re)) / static_cast<float>(P);
