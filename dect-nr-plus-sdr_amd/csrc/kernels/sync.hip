@@ -291,9 +291,11 @@ constexpr uint32_t SS_RING = DNRP_SS_RING;
 #endif
 constexpr uint32_t SS_PRING = DNRP_SS_PRING;
 static_assert(SS_PRING % 16 == 0, "16-slot step-sum reads stay inside the ring");
-__device__ __forceinline__ uint32_t pring(int64_t m) {  // m mod SS_PRING for m >= -2^31
+__device__ __forceinline__ uint32_t pring(int64_t m) {  // m mod SS_PRING for -2^20 <= m < 2^31 - 2^21
     if constexpr ((SS_PRING & (SS_PRING - 1)) == 0) return static_cast<uint32_t>(m) & (SS_PRING - 1);
-    return static_cast<uint32_t>((m + (int64_t(1) << 31) / SS_PRING * SS_PRING + SS_PRING) % SS_PRING);
+    // 32-bit: a constant-divisor modulo is a multiply-high and a few adds, the 64-bit one an emulation
+    constexpr uint32_t OFF = ((1u << 20) + SS_PRING - 1) / SS_PRING * SS_PRING;
+    return (static_cast<uint32_t>(static_cast<int32_t>(m)) + OFF) % SS_PRING;
 }
 constexpr uint32_t SS_WPG = 4;
 
