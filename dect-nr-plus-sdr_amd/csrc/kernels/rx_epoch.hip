@@ -35,6 +35,14 @@ constexpr uint32_t EP_THREADS = 512, EP_WAVES = EP_THREADS / 64;
 
 __host__ __device__ inline size_t ep_front_lds() { return size_t(EP_WAVES) * rxw_region(9, 10, pp_block<9, 10, 24>::W) * sizeof(float2); }
 
+#ifndef DNRP_EP_PREFETCH
+#define DNRP_EP_PREFETCH 1  // the pilot buffer's source loads issued before the phase barrier
+#endif
+#ifndef DNRP_EP_PRE_CELLS
+#define DNRP_EP_PRE_CELLS 0  // 1: the pilot cells too (NT x NRX float2 over the barrier: spills at 4x4;
+                             // rx_epoch 27.40 / 27.50 vs 26.73 / 26.85 ms with the offsets only, 27.09 / 26.99 without)
+#endif
+
 template <int NRX, int NT, int NBPS>
 __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu(4))) rx_epoch_kernel(rx_epoch_args X) {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -89,6 +97,61 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
             }, w1, wl);
         }
     }
+    // The pilot buffer's global loads (build_pilots' sources and cells: three dependent round trips)
+    // issued by every wave right after its last front-end task, while the workgroup waits at the phase
+    // barrier for the waves still transforming; stored to LDS after it (the LDS is the front end's
+    // until then). One thread per (pilot index pi, interlace slot po), NT x NRX cells each; the same
+    // loads and values as build_pilots. pre = the geometry fits (2 n_drs <= threads).
+    const rx_epoch* E = A.epochs + ep;
+    const float2* Yp = A.Y + size_t(pkt) * NRX * A.n_sym_total * A.Nf_pad;
+    const uint8_t* lutp = A.lut_d + size_t(pkt) * RX_MAX_DOPS;
+    const uint32_t nd = A.n_drs;
+    const bool pre = DNRP_EP_PREFETCH && 2 * nd <= EP_THREADS;  // uniform
+    const uint32_t pi = tid >> 1, po = tid & 1u;
+    const bool pact = pre && tid < 2 * nd;
+    float2 pv[NT][NRX];
+    float pdv[NT];
+    uint32_t pyk[NT];  // the cell offset of stream t's pilot (DNRP_EP_PRE_CELLS 0: cells loaded after the barrier)
+    uint32_t pok = 0;  // bit t: stream t's slot po has a source
+    const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
+    if (pact) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const uint32_t s0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(E->src[t][0])),
+                           s1 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(E->src[t][1]));
+            const uint32_t src = po ? s1 : s0;
+            const bool ok = src != 0xFFFFu;
+            const uint32_t op = ok ? src : 0u;
+            const uint32_t par = A.n_dops ? (A.dmeta[op] >> 16) & 0xFFu : 0u, l = A.n_dops ? A.dl[op] : 0u;
+            const uint32_t kb = ok ? par * 4 + (t & 3u) : (t & 3u), yo = ok ? l * A.Nf_pad : 0u;
+            pok |= ok ? 1u << t : 0u;
+            pdv[t] = A.drs_v[t * nd + pi];
+            pyk[t] = yo + A.drs_k[kb * nd + pi];
+            if constexpr (DNRP_EP_PRE_CELLS) {
+#pragma unroll
+                for (int a = 0; a < NRX; ++a) pv[t][a] = Yp[a * ast + pyk[t]];
+            }
+        }
+    }
+    // the weight tables' sources (LUT profile pick -> table -> rows: uniform) and the segment
+    // descriptors, also before the barrier
+    const uint32_t units = E->units, seg0 = E->seg0, nseg = E->seg1 - E->seg0;
+    const uint32_t dc = nseg ? A.segs[seg0].drs_cnt : 0u;
+    const uint32_t prof = dc ? lutp[dc - 1] : 0u;
+    const rx_lut LW0 = A.luts[prof], LW1 = A.luts[3 + prof];  // the two modes' weight tables (uniform)
+    cell_seg pc{};
+    const bool has_c = units && tid < nseg;
+    if (DNRP_EP_PREFETCH && has_c) {
+        const rx_seg Sg = A.segs[seg0 + tid];
+        const rx_lut LT = A.luts[Sg.mode * 3 + prof];
+        pc.u0 = Sg.u0;
+        pc.j0 = Sg.j0;
+        pc.l = Sg.l;
+        pc.info = (Sg.mode & 1u) | (Sg.swap & 3u) << 1 | (Sg.off & 0xFFu) << 4 | LT.n << 12;
+        pc.pw = LT.pw + size_t(Sg.rel) * 4 * (A.N_occ + 1);
+        pc.wbase = (Sg.mode & 1u) * A.wcap[0];
+        pc.pad = 0;
+    }
     __syncthreads();  // the epoch's rows written (workgroup-scope release / acquire), LDS free again
     if constexpr (experiment(XS_EP_SKIP_EQ)) return;
 
@@ -98,19 +161,15 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
     float* wtab = reinterpret_cast<float*>(zfi + NRX * NT * zst);            // slots: mode l, mode lr
     cell_seg* sg = reinterpret_cast<cell_seg*>(wtab + A.wcap[0] + A.wcap[1]);  // CELL_MAX_SEGS
     uint32_t* pairs = reinterpret_cast<uint32_t*>(sg + CELL_MAX_SEGS);       // 12
-    const rx_epoch* E = A.epochs + ep;
-    const uint32_t units = E->units, seg0 = E->seg0, nseg = E->seg1 - E->seg0;
-    const float2* Yp = A.Y + size_t(pkt) * NRX * A.n_sym_total * A.Nf_pad;
-    const uint8_t* lutp = A.lut_d + size_t(pkt) * RX_MAX_DOPS;
-    const uint32_t dc = nseg ? A.segs[seg0].drs_cnt : 0u;
-    const uint32_t prof = dc ? lutp[dc - 1] : 0u;
     if (units) {
 #pragma unroll
         for (uint32_t m = 0; m < 2; ++m) {
-            const rx_lut LT = A.luts[m * 3 + prof];
+            const rx_lut LT = m ? LW1 : LW0;
             for (uint32_t i = tid; i < LT.nw; i += EP_THREADS) wtab[m * A.wcap[0] + i] = LT.w[i];
         }
-        if (tid < nseg) {
+        if (DNRP_EP_PREFETCH && has_c) {
+            sg[tid] = pc;
+        } else if (tid < nseg) {
             const rx_seg Sg = A.segs[seg0 + tid];
             const rx_lut LT = A.luts[Sg.mode * 3 + prof];
             cell_seg c;
@@ -125,7 +184,29 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
         }
         if (tid < 12) pairs[tid] = A.pair[tid];
     }
-    build_pilots<NRX, NT, cells_ai(NRX, NT)>(A, E, Yp, zfi, tid, EP_THREADS);
+    if (pre) {
+        constexpr bool AI = cells_ai(NRX, NT);
+        auto zi = [&](uint32_t a, uint32_t t, uint32_t idx) {
+            return AI ? ((t * (NRX / 2) + a / 2) * zst + idx) * 2 + (a & 1u) : (a * NT + t) * zst + idx;
+        };
+        for (uint32_t e = tid; e < NRX * NT * ZFI_PAD; e += EP_THREADS)
+            zfi[zi(e / ZFI_PAD / NT, e / ZFI_PAD % NT, 2 * nd + e % ZFI_PAD)] = make_float2(0.f, 0.f);
+        if (pact) {
+            if constexpr (!DNRP_EP_PRE_CELLS) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int a = 0; a < NRX; ++a) pv[t][a] = Yp[a * ast + pyk[t]];
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int a = 0; a < NRX; ++a)
+                    zfi[zi(a, t, 2 * pi + po)] = ((pok >> t) & 1u) ? cscale(pv[t][a], pdv[t]) : make_float2(0.f, 0.f);
+        }
+    } else {
+        build_pilots<NRX, NT, cells_ai(NRX, NT)>(A, E, Yp, zfi, tid, EP_THREADS);
+    }
     if constexpr (experiment(XS_EP_SLOTY)) Yp = A.Y + size_t(blockIdx.x % (64u * A.n_epochs)) * NRX * A.n_sym_total * A.Nf_pad;
     __syncthreads();
     if (tid >= units) return;
