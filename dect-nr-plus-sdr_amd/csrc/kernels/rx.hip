@@ -95,6 +95,10 @@ __host__ __device__ inline uint32_t rx_stf_chunk_taps(uint32_t n_stf, uint32_t N
 // float2 slots of rx_stf_ant_kernel's compact area: the 9/10 input span of n_stf outputs (upper bound)
 __host__ __device__ inline uint32_t rx_stf_area(uint32_t n_stf) { return ((n_stf + 18) * 10) / 9 + 33 + 10 + 2; }
 
+#ifndef DNRP_STF_STAGE_U
+#define DNRP_STF_STAGE_U 10  // span loads in flight per thread (C4's ~2400-input STF span by 256 threads: one
+                             // round trip; 8: two -- measured neutral, 1.04 ms either way)
+#endif
 #ifndef DNRP_STF_IMAJ
 #define DNRP_STF_IMAJ 1  // compiled-in taps: the FIR input-major from LDS (0: the whole window in registers)
 #endif
@@ -144,7 +148,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CT ? D
         const int64_t in0 = static_cast<int64_t>(A.p_star) + 10 * q0 - 24;  // relative to the fine peak
         const uint32_t n_in = static_cast<uint32_t>(10 * (q1 - 1 - q0) + W);
         float2* span = compact ? smem + ((rx_stf_area(n_stf) - n_in) & ~1u) : inbuf;
-        stage_span_lo<8>(span, x + in.fine_peak, in0, n_in, in.fine_peak < 0 ? -in.fine_peak : 0,
+        stage_span_lo<DNRP_STF_STAGE_U>(span, x + in.fine_peak, in0, n_in, in.fine_peak < 0 ? -in.fine_peak : 0,
                          static_cast<int64_t>(A.S_in) - in.fine_peak, threadIdx.x, blockDim.x);
         __syncthreads();
         const float2 step1 = phasor(in.inc0);

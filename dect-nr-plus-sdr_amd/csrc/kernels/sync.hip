@@ -1115,6 +1115,10 @@ __device__ __forceinline__ void resample_direct(const sync_args& A, const float2
 // (every window read: stage[] may alias the outputs' slots) hands the outputs to put. One global
 // load latency instead of two (the tail blocks' second round), the same sums as resample_direct.
 // Preconditions (host, sync_peak_ok): blocks <= 2 T, n_in <= the stage's capacity.
+#ifndef DNRP_STAGE_G
+#define DNRP_STAGE_G 11  // span loads in flight per thread: sync_peak's 5200-input span by 512 threads and
+                         // sync_post's 2600 by 256 in one round trip (6: two)
+#endif
 template <int LR, int MR, int HLR, bool IMAJ = false, class PUT>
 __device__ __forceinline__ void resample_staged(const sync_args& A, const float2* x, int64_t y0, uint32_t cnt,
                                                 float2* stage, PUT put) {
@@ -1130,7 +1134,7 @@ __device__ __forceinline__ void resample_staged(const sync_args& A, const float2
     typedef uint32_t u2 __attribute__((ext_vector_type(2)));
     // indices past the stream end read a range-checked zero; a negative start wraps into the
     // descriptor's "outside" range as well (offsets are unsigned)
-    constexpr uint32_t G = 6;  // loads in flight per thread and group
+    constexpr uint32_t G = DNRP_STAGE_G;  // loads in flight per thread and group
     for (uint32_t i0 = 0; i0 < n_in; i0 += G * T) {
         float2 v[G];
 #pragma unroll
