@@ -290,9 +290,21 @@ __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
     const uint32_t pkt = rx_slot_of(A.sel, blockIdx.x);
     const uint32_t Nd = A.plan.N, N = A.N_occ;
     const uint32_t n_stf = A.STF_CP + Nd, n = A.b * 14;
-    float2* Ys = smem;  // [N_RX][n]
-    for (uint32_t a = 0; a < A.N_RX; ++a)
-        for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) Ys[a * n + w] = A.stf_ys[(size_t(pkt) * 8 + a) * A.stf_ys_stride + w];
+    float2* Ys = smem;          // [N_RX][n]
+    float2* St = Ys + A.N_RX * n;  // [n]: the STF value of cell w (subcarrier rstf(w))
+    auto rstf = [&](uint32_t w) { return w < n / 2 ? 4 * w : 4 * w + 4; };
+    for (uint32_t w0 = 0; w0 < n; w0 += blockDim.x) {  // every antenna's cells in flight together
+        const uint32_t w = w0 + threadIdx.x;
+        float2 yv[8], sv = make_float2(0.f, 0.f);
+        if (w < n) sv = A.stf[rstf(w)];
+#pragma unroll
+        for (uint32_t a = 0; a < 8; ++a)
+            if (a < A.N_RX && w < n) yv[a] = A.stf_ys[(size_t(pkt) * 8 + a) * A.stf_ys_stride + w];
+#pragma unroll
+        for (uint32_t a = 0; a < 8; ++a)
+            if (a < A.N_RX && w < n) Ys[a * n + w] = yv[a];
+        if (w < n) St[w] = sv;
+    }
     const rx_pkt_in in = A.pin[pkt];
     const uint32_t P = n_stf / A.n_pattern;
     double cs_re = 0.0, cs_im = 0.0;
@@ -317,12 +329,11 @@ __global__ void __launch_bounds__(256) rx_stf_kernel(rx_front_args A) {
     }
     S.cfo_fine = in.cfo_rad + delta;
     // STF zero-forcing and fractional STO (rx_synced.cpp:663-709, estimator_sto.cpp:124-146)
-    auto rstf = [&](uint32_t w) { return w < n / 2 ? 4 * w : 4 * w + 4; };
     auto zf = [&](uint32_t a, uint32_t w, double inc) {
         const uint32_t r = rstf(w);
         float2 y = Ys[a * n + w];
         if (inc != 0.0) y = cmul(y, phasor(-inc * static_cast<double>(N / 2) + inc * static_cast<double>(r)));
-        const float2 s = A.stf[r];
+        const float2 s = St[w];
         return make_float2((y.x * s.x + y.y * s.y) / cnorm(s), (y.y * s.x - y.x * s.y) / cnorm(s));
     };
     double inc = 0.0;
@@ -506,7 +517,7 @@ hipError_t launch_rx_stf(const rx_front_args& a_in, uint32_t n, hipStream_t st) 
         hipLaunchKernelGGL((rx_stf_ant_kernel<24, true>), dim3(n * a.N_RX), dim3(256), lds, st, a);
     else
         DNRP_HL_DISPATCH(rx_stf_ant_kernel, dim3(n * a.N_RX), dim3(256), lds, st, a);
-    hipLaunchKernelGGL(rx_stf_kernel, dim3(n), dim3(256), size_t(a.N_RX) * a.b * 14 * sizeof(float2), st, a);
+    hipLaunchKernelGGL(rx_stf_kernel, dim3(n), dim3(256), size_t(a.N_RX + 1) * a.b * 14 * sizeof(float2), st, a);
     return hipGetLastError();
 }
 
