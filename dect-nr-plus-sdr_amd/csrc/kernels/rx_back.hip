@@ -160,6 +160,10 @@ hipError_t launch_rx_snr(const rx_snr_args& a, uint32_t n, hipStream_t st) {
 
 // ===================================================================== cells
 constexpr uint32_t CELL_THREADS = 512;
+#ifndef DNRP_CELLS_PILOT_PRE
+#define DNRP_CELLS_PILOT_PRE 0  // 1: pilot sources issued before the weight-table staging: neutral (rx_pcc 0.347 /
+                                // 0.349 vs 0.345 / 0.349 ms, C4SM rx_pdc 17.58 / 17.66 vs 17.58 / 17.67), off
+#endif
 
 template <int NRX, int NT, bool SM = false, int NBPS = 0>
 __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A) {
@@ -185,6 +189,13 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
     const uint8_t* lutp = A.lut_d + size_t(pkt) * RX_MAX_DOPS;
     const uint32_t dc = nseg ? A.segs[seg0].drs_cnt : 0u;
     const uint32_t prof = dc ? lutp[dc - 1] : 0u;
+    // the pilot buffer's dependent source loads first (pilot_offsets, where 2 n_drs <= threads), so
+    // they overlap the weight-table staging instead of following it
+    const bool ppre = DNRP_CELLS_PILOT_PRE && 2 * A.n_drs <= CELL_THREADS;  // uniform
+    const bool pact = ppre && tid < 2 * A.n_drs;
+    uint32_t pyk[NT] = {}, pok = 0;
+    float pdv[NT] = {};
+    if (pact) pilot_offsets<NT>(A, E, tid, pyk, pdv, pok);
     if (units) {
 #pragma unroll
         for (uint32_t m = 0; m < 2; ++m) {
@@ -206,7 +217,12 @@ __global__ void __launch_bounds__(CELL_THREADS) rx_cells_kernel(rx_cells_args A)
         }
         if (tid < 12) pairs[tid] = A.pair[tid];
     }
-    if constexpr (!experiment(XS_CELLS_SKIP_PRO)) build_pilots<NRX, NT, cells_ai(NRX, NT)>(A, E, Yp, zfi, tid, CELL_THREADS);
+    if constexpr (!experiment(XS_CELLS_SKIP_PRO)) {
+        if (ppre)
+            pilot_cells<NRX, NT>(A, Yp, zfi, tid, CELL_THREADS, pact, pyk, pdv, pok);
+        else
+            build_pilots<NRX, NT, cells_ai(NRX, NT)>(A, E, Yp, zfi, tid, CELL_THREADS);
+    }
     __syncthreads();
     if constexpr (experiment(XS_CELLS_SKIP_MAIN)) {
         if (tid < units) A.llr[size_t(row) * A.llr_stride + tid] = static_cast<int16_t>(zfi[tid].x);

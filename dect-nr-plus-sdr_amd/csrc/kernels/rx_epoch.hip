@@ -38,10 +38,6 @@ __host__ __device__ inline size_t ep_front_lds() { return size_t(EP_WAVES) * rxw
 #ifndef DNRP_EP_PREFETCH
 #define DNRP_EP_PREFETCH 1  // the pilot buffer's source loads issued before the phase barrier
 #endif
-#ifndef DNRP_EP_PRE_CELLS
-#define DNRP_EP_PRE_CELLS 0  // 1: the pilot cells too (NT x NRX float2 over the barrier: spills at 4x4;
-                             // rx_epoch 27.40 / 27.50 vs 26.73 / 26.85 ms with the offsets only, 27.09 / 26.99 without)
-#endif
 
 template <int NRX, int NT, int NBPS>
 __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu(4))) rx_epoch_kernel(rx_epoch_args X) {
@@ -107,32 +103,10 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
     const uint8_t* lutp = A.lut_d + size_t(pkt) * RX_MAX_DOPS;
     const uint32_t nd = A.n_drs;
     const bool pre = DNRP_EP_PREFETCH && 2 * nd <= EP_THREADS;  // uniform
-    const uint32_t pi = tid >> 1, po = tid & 1u;
     const bool pact = pre && tid < 2 * nd;
-    float2 pv[NT][NRX];
-    float pdv[NT];
-    uint32_t pyk[NT];  // the cell offset of stream t's pilot (DNRP_EP_PRE_CELLS 0: cells loaded after the barrier)
-    uint32_t pok = 0;  // bit t: stream t's slot po has a source
-    const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
-    if (pact) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const uint32_t s0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(E->src[t][0])),
-                           s1 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(E->src[t][1]));
-            const uint32_t src = po ? s1 : s0;
-            const bool ok = src != 0xFFFFu;
-            const uint32_t op = ok ? src : 0u;
-            const uint32_t par = A.n_dops ? (A.dmeta[op] >> 16) & 0xFFu : 0u, l = A.n_dops ? A.dl[op] : 0u;
-            const uint32_t kb = ok ? par * 4 + (t & 3u) : (t & 3u), yo = ok ? l * A.Nf_pad : 0u;
-            pok |= ok ? 1u << t : 0u;
-            pdv[t] = A.drs_v[t * nd + pi];
-            pyk[t] = yo + A.drs_k[kb * nd + pi];
-            if constexpr (DNRP_EP_PRE_CELLS) {
-#pragma unroll
-                for (int a = 0; a < NRX; ++a) pv[t][a] = Yp[a * ast + pyk[t]];
-            }
-        }
-    }
+    uint32_t pyk[NT] = {}, pok = 0;
+    float pdv[NT] = {};
+    if (pact) pilot_offsets<NT>(A, E, tid, pyk, pdv, pok);
     // the weight tables' sources (LUT profile pick -> table -> rows: uniform) and the segment
     // descriptors, also before the barrier
     const uint32_t units = E->units, seg0 = E->seg0, nseg = E->seg1 - E->seg0;
@@ -185,25 +159,7 @@ __global__ void __launch_bounds__(EP_THREADS) __attribute__((amdgpu_waves_per_eu
         if (tid < 12) pairs[tid] = A.pair[tid];
     }
     if (pre) {
-        constexpr bool AI = cells_ai(NRX, NT);
-        auto zi = [&](uint32_t a, uint32_t t, uint32_t idx) {
-            return AI ? ((t * (NRX / 2) + a / 2) * zst + idx) * 2 + (a & 1u) : (a * NT + t) * zst + idx;
-        };
-        for (uint32_t e = tid; e < NRX * NT * ZFI_PAD; e += EP_THREADS)
-            zfi[zi(e / ZFI_PAD / NT, e / ZFI_PAD % NT, 2 * nd + e % ZFI_PAD)] = make_float2(0.f, 0.f);
-        if (pact) {
-            if constexpr (!DNRP_EP_PRE_CELLS) {
-#pragma unroll
-                for (int t = 0; t < NT; ++t)
-#pragma unroll
-                    for (int a = 0; a < NRX; ++a) pv[t][a] = Yp[a * ast + pyk[t]];
-            }
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int a = 0; a < NRX; ++a)
-                    zfi[zi(a, t, 2 * pi + po)] = ((pok >> t) & 1u) ? cscale(pv[t][a], pdv[t]) : make_float2(0.f, 0.f);
-        }
+        pilot_cells<NRX, NT>(A, Yp, zfi, tid, EP_THREADS, pact, pyk, pdv, pok);
     } else {
         build_pilots<NRX, NT, cells_ai(NRX, NT)>(A, E, Yp, zfi, tid, EP_THREADS);
     }

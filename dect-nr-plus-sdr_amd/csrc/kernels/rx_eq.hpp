@@ -637,4 +637,55 @@ __device__ __forceinline__ void build_pilots(const rx_cells_args& A, const rx_ep
     }
 }
 
+// build_pilots in two halves for one thread per (pilot index pi, interlace slot po) -- the fast form
+// where 2 n_drs <= threads: pilot_offsets issues the dependent source loads (the epoch's DRS ops ->
+// their parity and symbol -> the pilot's subcarrier and DRS value) and returns each stream's cell
+// offset in the packet's Y rows; pilot_cells loads the cells and stores the zero-forced pilots (plus
+// the row padding). Same loads and values as build_pilots.
+template <int NT>
+__device__ __forceinline__ void pilot_offsets(const rx_cells_args& A, const rx_epoch* E, uint32_t tid, uint32_t (&pyk)[NT],
+                                              float (&pdv)[NT], uint32_t& pok) {
+    const uint32_t nd = A.n_drs, pi = tid >> 1, po = tid & 1u;
+    pok = 0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const uint32_t s0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(E->src[t][0])),
+                       s1 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(E->src[t][1]));
+        const uint32_t src = po ? s1 : s0;
+        const bool ok = src != 0xFFFFu;
+        const uint32_t op = ok ? src : 0u;
+        const uint32_t par = A.n_dops ? (A.dmeta[op] >> 16) & 0xFFu : 0u, l = A.n_dops ? A.dl[op] : 0u;
+        const uint32_t kb = ok ? par * 4 + (t & 3u) : (t & 3u), yo = ok ? l * A.Nf_pad : 0u;
+        pok |= ok ? 1u << t : 0u;
+        pdv[t] = A.drs_v[t * nd + pi];
+        pyk[t] = yo + A.drs_k[kb * nd + pi];
+    }
+}
+
+template <int NRX, int NT>
+__device__ __forceinline__ void pilot_cells(const rx_cells_args& A, const float2* Yp, float2* zfi, uint32_t tid,
+                                            uint32_t nthreads, bool act, const uint32_t (&pyk)[NT], const float (&pdv)[NT],
+                                            uint32_t pok) {
+    constexpr bool AI = cells_ai(NRX, NT);
+    const uint32_t nd = A.n_drs, zst = zfi_stride(nd), pi = tid >> 1, po = tid & 1u;
+    const size_t ast = size_t(A.n_sym_total) * A.Nf_pad;
+    auto zi = [&](uint32_t a, uint32_t t, uint32_t idx) {
+        return AI ? ((t * (NRX / 2) + a / 2) * zst + idx) * 2 + (a & 1u) : (a * NT + t) * zst + idx;
+    };
+    for (uint32_t e = tid; e < NRX * NT * ZFI_PAD; e += nthreads)
+        zfi[zi(e / ZFI_PAD / NT, e / ZFI_PAD % NT, 2 * nd + e % ZFI_PAD)] = make_float2(0.f, 0.f);
+    if (act) {
+        float2 pv[NT][NRX];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int a = 0; a < NRX; ++a) pv[t][a] = Yp[a * ast + pyk[t]];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int a = 0; a < NRX; ++a)
+                zfi[zi(a, t, 2 * pi + po)] = ((pok >> t) & 1u) ? cscale(pv[t][a], pdv[t]) : make_float2(0.f, 0.f);
+    }
+}
+
 }  // namespace dnrp::dev
