@@ -1666,6 +1666,12 @@ size_t sync_detect_lds(const sync_args& a) {
     } while (0)
 
 constexpr int SYNC_WPG = SYNC_WPG_DEF;  // waves per workgroup of the wave kernel
+#ifndef DNRP_SS_SEG_CHUNKS
+#define DNRP_SS_SEG_CHUNKS 96u  // at most this many chunks of 64 polyphase blocks per sync_steps segment (each
+                                // segment re-resamples its lag history first). C4 (1440 steps per window):
+                                // 32 -> 5 x 288 steps 12.95 / 12.79 ms, 64 -> 3 x 480 12.71 / 12.74, 96 -> 2 x 720
+                                // 12.55 / 12.65, 160 -> 1 x 1440 12.61 / 12.65 (same box)
+#endif
 
 hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
     // DNRP_SYNC_STREAM=0 selects the wave kernel below (read per call: tests switch it at run time)
@@ -1674,7 +1680,11 @@ hipError_t launch_sync_steps(const sync_args& a, uint32_t n, hipStream_t st) {
     if (ss_env && a.L == 9 && a.M == 10 && a.hl == 24 && a.step % 4 == 0 && a.step >= 4 &&
         64u * 9u + a.step + a.pattern + 9u <= SS_RING) {
         // segments of ~32 chunks per (window, antenna): enough waves to fill the chip, little warm-up
-        const uint32_t seg_steps = std::max(1u, (32u * 64u * 9u) / a.step);
+        // segments of at most DNRP_SS_SEG_CHUNKS chunks, balanced: ceil(n_steps / max) segments of
+        // equal length (a short last segment leaves its waves idle at the tail)
+        const uint32_t seg_max = std::max(1u, (DNRP_SS_SEG_CHUNKS * 64u * 9u) / a.step);
+        const uint32_t n_seg0 = (a.n_steps + seg_max - 1) / seg_max;
+        const uint32_t seg_steps = std::max(1u, (a.n_steps + n_seg0 - 1) / n_seg0);
         const uint32_t n_seg = (a.n_steps + seg_steps - 1) / seg_steps;
         const uint64_t waves = uint64_t(n) * a.n_ant * n_seg;
         const size_t lds = SS_WPG * size_t(ss_inbuf<9, 10, 24>() + SS_RING) * sizeof(float2);
